@@ -1,0 +1,243 @@
+"""mscclpp_amd benchmark (driver contract: one JSON line on rank 0).
+
+N = 1  -> BASELINE.json configs[1]: the 1-GPU LL16 pack + sum + unpack self-reduce, fp16, 48 MiB,
+          device-resident (the HBM-roofline check of the LL hot path).
+N > 1  -> BASELINE.json configs[2]: ncclAllReduce of a 48 MiB fp16 bucket (2048 x 12288, the
+          README's GPT-3 TP bucket) per rank, one process per GPU, one-sided puts over xGMI
+          through libmscclpp_amd.so (no RCCL underneath).  Launched by torch.distributed.run.
+
+value = algbw = S / t (GB/s): S = bucket bytes per rank, t = max over ranks of the time per step
+inside the timed region (barrier + synchronize on both sides).  Inputs are resident in HBM before
+the timed region starts.  The roofline object prices the dominant kernel with its live HIP-event
+duration; cpu_baseline times the CPU oracle (oracle/liboracle.so) on a bounded sample.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.6          # per link, task-stated
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--bytes", type=int, default=48 << 20)
+    p.add_argument("--algo", default=None, help="force an AllReduce algorithm (N>1): packet|allpair|fullmesh|rsag")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline_self_reduce(nbytes, budget_s):
+    """Oracle (scalar C port, 1 thread) pack+sum+unpack on the same workload, bounded in time."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    count = nbytes // 2
+    x = O.lcg(O.F16, count, 0, 0)
+    y = O.lcg(O.F16, count, 1, 0)
+    iters, t0 = 0, time.perf_counter()
+    while True:
+        O.self_reduce(O.F16, O.SUM, x, y, iters + 1)
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or iters >= 200:
+            break
+    return {"value": round(nbytes * iters / el / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{iters} x oracle_self_reduce fp16 {nbytes >> 20} MiB (scalar C, 1 thread) in {el:.1f} s"}
+
+
+def cpu_baseline_allreduce(nbytes, n, budget_s):
+    """Oracle fullmesh-order AllReduce arithmetic for n ranks on a bounded slice of the bucket."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    sample = min(nbytes, 8 << 20)
+    count = sample // 2
+    ins = [O.lcg(O.F16, count, r, 0).view(np.uint32) for r in range(n)]
+    nw = sample // 4
+    iters, t0 = 0, time.perf_counter()
+    while True:
+        O.allreduce_sliced(O.F16, O.SUM, ins, nw, nw // n, 0)
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or iters >= 1000:
+            break
+    return {"value": round(sample * iters / el / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{iters} x oracle {n}-rank fullmesh-order fp16 sum of {sample >> 20} MiB (scalar C, 1 thread)"}
+
+
+def bench_single(args):
+    import mscclpp_amd as m
+
+    S = args.bytes
+    count = S // 2
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.rand(count, generator=g).to(torch.float16).to(dev)
+    y = torch.rand(count, generator=g).to(torch.float16).to(dev)
+    out = torch.empty_like(x)
+    pk = m.DeviceBuffer(2 * S)
+    flags = torch.ones(m.FLAG_SLOTS, dtype=torch.int32, device=dev)
+    err = torch.zeros(16, dtype=torch.int32, device=dev)
+
+    def step():
+        m.self_reduce_ll16(x, y, pk.ptr, out, flags, err)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # per-launch kernel duration (events on the launch stream = torch's current stream)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b in evs:
+        a.record()
+        step()
+        b.record()
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    # timed region: exactly K steps, synchronize on both sides
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / args.steps
+    assert int(err[0].item()) == 0, "device error word set"
+    # correctness spot check of the last step
+    ref = (x.float() + y.float()).clamp(-65504, 65504).half()
+    assert torch.equal(out, ref), "self-reduce mismatch"
+    achieved = 7 * S / (kern_ms * 1e-3) / 1e9
+    res = {
+        "metric": "device-resident AllReduce algbw GB/s fp16 at 1/2/4/8 MI355X; % xGMI roofline",
+        "value": round(S / t / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16",
+        "data": "synthetic",
+        "config": {"workload": "ll16_self_reduce_fp16_48MiB (BASELINE configs[1]: pack+sum+unpack, 1 GPU)",
+                   "bytes": S, "parallelism": "single-gpu"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "selfReduceLL16Kernel", "kernel_us": round(kern_ms * 1e3, 2),
+                     "algorithmic_bytes_per_launch": 7 * S},
+    }
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_self_reduce(S, args.cpu_seconds)
+    pk.free()
+    return res
+
+
+def bench_multi(args):
+    import torch.distributed as dist
+
+    import mscclpp_amd as m
+
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = m.Communicator.from_torch_dist()
+    S = args.bytes
+    count = S // 2
+    dev = torch.device("cuda", local)
+    g = torch.Generator(device="cpu").manual_seed(rank)
+    x = torch.rand(count, generator=g).to(torch.float16).to(dev)
+    out = torch.empty_like(x)
+
+    def step():
+        comm.all_reduce(x, out, algo=args.algo)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b in evs:
+        a.record()
+        step()
+        b.record()
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t_local = (time.perf_counter() - t0) / args.steps
+    dist.barrier()
+    tt = torch.tensor([t_local, kern_ms], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t, kern_ms = float(tt[0]), float(tt[1])
+    errc = comm.device_error()
+    # correctness: compare with a gloo all-reduce of the same inputs in fp32 (tolerance check)
+    ref = x.float().cpu()
+    dist.all_reduce(ref)
+    ok = torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=5e-4 * world)
+    algbw = S / t / 1e9
+    n = world
+    ceiling = n * XGMI_LINK_GBS / 2  # all-pairs algbw ceiling
+    res = {
+        "metric": "device-resident AllReduce algbw GB/s fp16 at 1/2/4/8 MI355X; % xGMI roofline",
+        "value": round(algbw, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f16",
+        "data": "synthetic",
+        "config": {"workload": f"allreduce_fp16_{S >> 20}MiB (BASELINE configs[2]: 2048x12288 fp16 bucket per rank)",
+                   "bytes": S, "parallelism": f"allreduce{world}", "algo": args.algo or "auto"},
+        "busbw": round(algbw * 2 * (n - 1) / n, 2),
+        "xgmi": {"allpairs_algbw_ceiling": round(ceiling, 1), "frac": round(algbw / ceiling, 4),
+                 "link_GBs": XGMI_LINK_GBS},
+        "roofline": {"bound": "hbm", "achieved": round(S * (2 + 2 * (n - 1) / n) / (kern_ms * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None, "kernel": "allreduce (per launch)",
+                     "kernel_us": round(kern_ms * 1e3, 2)},
+        "correct": bool(ok and errc == 0),
+    }
+    res["roofline"]["frac"] = round(res["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if rank == 0 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_allreduce(S, n, args.cpu_seconds)
+    comm.destroy()
+    dist.barrier()
+    dist.destroy_process_group()
+    return res if rank == 0 else None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        res = bench_multi(args)
+    else:
+        res = bench_single(args)
+    if res is not None:
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,115 @@
+// mscclpp_amd device core: gfx950 memory operations with explicit cache scope, bounded spins and
+// the device-side error word.  HIP for CDNA4 (gfx950) only.
+//
+// Replaces the reference's include/mscclpp/device.hpp, atomic_device.hpp:43-65 and
+// poll_device.hpp:12-18 (POLL_MAYBE_JAILBREAK).  Differences by design:
+//  * every scope is explicit.  The reference's HIP atomics ignore their scope argument and become
+//    system-scope __atomic_* (atomic_device.hpp:49-65); here the scope is part of each call.
+//  * 16-byte accesses use buffer instructions with cache-policy bits (sc0 sc1 = system,
+//    sc1 = agent, nt = streaming) so a whole LL16 packet moves in one dwordx4.
+//  * every spin is bounded by wall-clock time (s_memrealtime, 100 MHz) in every build, and a
+//    timeout records a code in a device error word instead of hanging the GPU.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mscclpp_amd {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Cache-policy bits of gfx950 buffer instructions (aux operand): sc0 = 1, nt = 2, sc1 = 16.
+enum CachePolicy : int {
+  kPlain = 0,
+  kNonTemporal = 2,   // streaming: keep out of the way of reused lines
+  kAgent = 16,        // sc1: bypass the CU's L1, coherent across the XCDs of one GPU
+  kSystem = 17,       // sc0 sc1: write-through / read-through to memory, coherent across GPUs
+};
+
+// Error codes written to the device error word (first writer wins).
+enum DeviceError : uint32_t {
+  kErrNone = 0,
+  kErrPacketTimeout = 1,     // an LL packet flag never arrived
+  kErrSemaphoreTimeout = 2,  // a semaphore wait never completed
+  kErrFifoTimeout = 3,       // a FIFO push found the ring full for too long
+  kErrBadGeometry = 4,       // host passed inconsistent sizes
+};
+
+// Buffer resource over a raw pointer.  num_records = 0xFFFFFFFF: the whole 32-bit offset space is
+// addressable; callers rebase the pointer for regions beyond 4 GiB.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0xFFFFFFFF, 0x00020000);
+}
+
+template <int Policy>
+__device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, Policy);
+}
+template <int Policy>
+__device__ __forceinline__ void store16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, Policy);
+}
+template <int Policy>
+__device__ __forceinline__ u32x2 load8(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, Policy);
+}
+template <int Policy>
+__device__ __forceinline__ void store8(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, u32x2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, byte_off, 0, Policy);
+}
+template <int Policy>
+__device__ __forceinline__ uint32_t load4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, Policy);
+}
+template <int Policy>
+__device__ __forceinline__ void store4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, byte_off, 0, Policy);
+}
+
+// Wall clock in 10 ns ticks (s_memrealtime runs at a constant 100 MHz on gfx950).
+__device__ __forceinline__ uint64_t wall_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+// Bounded spin bookkeeping.  `budget_ticks` == 0 means "never time out" (not used by the library;
+// every library call passes a finite budget).
+struct SpinGuard {
+  uint64_t deadline;
+  uint32_t iter;
+  __device__ __forceinline__ explicit SpinGuard(uint64_t budget_ticks)
+      : deadline(budget_ticks ? wall_ticks() + budget_ticks : ~0ull), iter(0) {}
+  // Returns true when the caller must give up.  Reads the clock once every 256 polls.
+  __device__ __forceinline__ bool expired() {
+    if ((++iter & 255u) != 0) return false;
+    return wall_ticks() > deadline;
+  }
+};
+
+__device__ __forceinline__ void report_error(uint32_t* err, uint32_t code) {
+  if (err) {
+    uint32_t expected = kErrNone;
+    __hip_atomic_compare_exchange_strong(err, &expected, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Relaxed system-scope 64-bit load / store / add (global_* sc0 sc1), used for tokens and flags.
+__device__ __forceinline__ uint64_t ld_relaxed_sys(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_acquire_sys(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_relaxed_sys(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_release_sys(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t add_release_sys(uint64_t* p, uint64_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t add_relaxed_sys(uint64_t* p, uint64_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace mscclpp_amd

@@ -1,0 +1,102 @@
+/*
+ * mscclpp_amd extension C ABI (libmscclpp_amd.so).  Plain pointers and sizes only.
+ *
+ * The NCCL drop-in entry points live in nccl.h.  This header adds what the reference exposes
+ * through its C++ API (include/mscclpp/core.hpp, algorithm.hpp, gpu_utils.hpp) and that the
+ * parity tests and the benchmark need:
+ *   - uncached device allocation and flag buffers (gpu_utils.cc:139-147, algorithm.cc:251-268)
+ *   - the 1-GPU LL16 pack+sum+unpack microbench kernel (BASELINE config 2)
+ *   - explicit-view AllReduce launchers: every rank's buffers and mapped peer pointers are passed
+ *     in, so the same kernels run either one rank per process (views = 1) or several ranks of a
+ *     single process on one GPU (views = n, "in-process ranks", used by the parity tests)
+ *   - Algorithm::execute with an explicit algorithm (algorithm.hpp:108-113)
+ *
+ * Return codes are ncclResult_t values (0 = success, 1 = HIP error, 3 = internal, 4 = invalid
+ * argument, 5 = invalid usage).
+ */
+#ifndef MSCCLPP_AMD_H_
+#define MSCCLPP_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "nccl.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSCCLPP_AMD_MAX_RANKS 8
+#define MSCCLPP_AMD_FLAG_SLOTS 1024
+#define MSCCLPP_AMD_MAX_CHANNELS 64
+
+/* dtype / op codes of the extension API (ncclDataType_t / ncclRedOp_t are mapped onto these) */
+enum { MSCCLPP_AMD_F16 = 0, MSCCLPP_AMD_BF16 = 1, MSCCLPP_AMD_F32 = 2, MSCCLPP_AMD_I32 = 3, MSCCLPP_AMD_U32 = 4 };
+enum { MSCCLPP_AMD_SUM = 0, MSCCLPP_AMD_MIN = 1 };
+
+/* AllReduce algorithms (names follow the reference's AlgorithmCollection keys) */
+enum {
+  MSCCLPP_AMD_ALGO_AUTO = 0,
+  MSCCLPP_AMD_ALGO_PACKET = 1,   /* default_allreduce_packet: LL16 two-hop (allreduce_packet.cu:15-151) */
+  MSCCLPP_AMD_ALGO_ALLPAIR = 2,  /* default_allreduce_allpair_packet: LL8 one-hop (allreduce_allpair_packet.cu:15-69) */
+  MSCCLPP_AMD_ALGO_FULLMESH = 3, /* default_allreduce_fullmesh: bulk all-pairs RS+AG (allreduce_fullmesh.cu:24-166) */
+  MSCCLPP_AMD_ALGO_RSAG = 4      /* default_allreduce_rsag: ring-order bulk RS+AG (allreduce_rsag.cu:33-128) */
+};
+
+/* One rank's view of the buffers of an AllReduce.  Pointers to other ranks' memory are the
+ * addresses at which this rank has them mapped (IPC), or plain device pointers for in-process
+ * ranks.  Entry [rank] of every peer array is this rank's own buffer. */
+typedef struct {
+  const void* input;
+  void* output;
+  void* scratch;                                   /* own scratch (two halves) */
+  void* peerScratch[MSCCLPP_AMD_MAX_RANKS];        /* rank q's scratch as mapped here */
+  void* peerOutput[MSCCLPP_AMD_MAX_RANKS];         /* rank q's output (bulk direct writes) */
+  uint64_t* tokens;                                /* own inbound tokens [MAX_RANKS][MAX_CHANNELS] */
+  uint64_t* peerTokens[MSCCLPP_AMD_MAX_RANKS];     /* rank q's tokens as mapped here */
+  uint64_t* expected;                              /* own expected counters [MAX_RANKS][MAX_CHANNELS] */
+  uint32_t* flags;                                 /* MSCCLPP_AMD_FLAG_SLOTS words, initialised to 1 */
+  uint32_t* err;                                   /* device error word (0 = ok) */
+  uint64_t scratchBytes;
+  int32_t rank;
+  int32_t pad;
+} mscclppAmdRankView;
+
+/* ---- memory ------------------------------------------------------------------------------- */
+int mscclppAmdMallocUncached(void** ptr, size_t bytes);
+int mscclppAmdMalloc(void** ptr, size_t bytes);
+int mscclppAmdFree(void* ptr);
+int mscclppAmdFlagsInit(uint32_t* flags, void* stream);
+
+/* ---- 1-GPU microbench (BASELINE config 2) ------------------------------------------------- */
+/* out = x (op) unpack(pack(y, flag)); pkts: 2*bytes of (uncached) device memory; bytes % 16 == 0.
+ * nblocks <= 0 selects the default grid.  budgetTicks: spin budget in 10 ns ticks. */
+int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts, void* out, size_t bytes, int dtype, int op,
+                             uint32_t* flags, int nblocks, uint64_t budgetTicks, uint32_t* err, void* stream);
+
+/* ---- explicit-view AllReduce ------------------------------------------------------------- */
+/* Launch `algo` for `nviews` ranks of an `nranks`-rank AllReduce in ONE kernel launch (views[i]
+ * is handled by blockIdx.y == i).  nviews == 1 is the one-rank-per-process form; nviews ==
+ * nranks runs every rank of the collective inside this process. */
+int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes,
+                              int dtype, int op, int nblocks, int nthreads, uint64_t budgetTicks, void* stream);
+/* Scratch bytes per rank (both halves) that `algo` needs for `bytes` (0 if unsupported). */
+size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype);
+/* Algorithm the selector picks (algorithm_selector.cc:91-139 restated for gfx950). */
+int mscclppAmdSelectAlgo(int nranks, size_t bytes, int dtype);
+
+/* ---- communicator extensions -------------------------------------------------------------- */
+int mscclppAmdCommAllReduce(ncclComm_t comm, const void* sendbuff, void* recvbuff, size_t count, int ncclDtype,
+                            int ncclOp, int algo, int nblocks, int nthreads, void* stream);
+int mscclppAmdCommBarrier(ncclComm_t comm);
+int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear);
+int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes);
+int mscclppAmdCommFlags(ncclComm_t comm, uint32_t** flags);
+/* Bootstrap all-gather of `bytes` per rank (host memory), for harnesses. */
+int mscclppAmdCommAllGatherHost(ncclComm_t comm, const void* sendbuf, void* recvbuf, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSCCLPP_AMD_H_ */

@@ -1,0 +1,285 @@
+"""mscclpp_amd: MI355X-native LL-packet AllReduce (drop-in for mscclpp's in-kernel AllReduce path).
+
+The product is the C-ABI shared library ``mscclpp_amd/lib/libmscclpp_amd.so`` (HIP kernels for
+gfx950 + C++ host runtime; headers in ``include/mscclpp_amd``).  This module is the thin Python
+host mirror used by the tests and the benchmark: it loads the library with ctypes and exposes
+the reference's operator surface for this path (``ncclAllReduce`` / ``Algorithm::execute`` with
+the same argument meaning and error behaviour).  PyTorch is used only for device memory and
+streams.  There is no fallback: if the library is missing, importing a GPU entry point raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  -- must be loaded first so the library binds to torch's HIP runtime
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmscclpp_amd.so")
+
+# dtype / op / algorithm codes (include/mscclpp_amd/mscclpp_amd.h)
+F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
+SUM, MIN = 0, 1
+ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG = 0, 1, 2, 3, 4
+ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4}
+MAX_RANKS = 8
+FLAG_SLOTS = 1024
+MAX_CHANNELS = 64
+
+# ncclDataType_t / ncclRedOp_t (include/mscclpp_amd/nccl.h, values of the reference nccl.h:217-253)
+NCCL_DTYPES = {torch.float16: 6, torch.bfloat16: 9, torch.float32: 7, torch.int32: 2}
+NCCL_OPS = {"sum": 0, "min": 3}
+DTYPE_CODES = {torch.float16: F16, torch.bfloat16: BF16, torch.float32: F32, torch.int32: I32}
+
+ERRORS = {0: "ncclSuccess", 1: "ncclUnhandledCudaError", 2: "ncclSystemError", 3: "ncclInternalError",
+          4: "ncclInvalidArgument", 5: "ncclInvalidUsage", 6: "ncclRemoteError", 7: "ncclInProgress"}
+
+
+class MscclppError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        super().__init__(f"{what}: {ERRORS.get(code, code)}")
+
+
+class RankView(ctypes.Structure):
+    _fields_ = [
+        ("input", ctypes.c_void_p),
+        ("output", ctypes.c_void_p),
+        ("scratch", ctypes.c_void_p),
+        ("peerScratch", ctypes.c_void_p * MAX_RANKS),
+        ("peerOutput", ctypes.c_void_p * MAX_RANKS),
+        ("tokens", ctypes.c_void_p),
+        ("peerTokens", ctypes.c_void_p * MAX_RANKS),
+        ("expected", ctypes.c_void_p),
+        ("flags", ctypes.c_void_p),
+        ("err", ctypes.c_void_p),
+        ("scratchBytes", ctypes.c_uint64),
+        ("rank", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
+    ]
+
+
+class UniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libmscclpp_amd.so (raises if it has not been built: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i32, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    sig = {
+        "mscclppAmdMallocUncached": [ctypes.POINTER(vp), sz],
+        "mscclppAmdMalloc": [ctypes.POINTER(vp), sz],
+        "mscclppAmdFree": [vp],
+        "mscclppAmdFlagsInit": [vp, vp],
+        "mscclppAmdSelfReduceLL16": [vp, vp, vp, vp, sz, i32, i32, vp, i32, u64, vp, vp],
+        "mscclppAmdAllReduceLaunch": [i32, ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, i32, u64, vp],
+        "mscclppAmdSelectAlgo": [i32, sz, i32],
+        "ncclGetUniqueId": [ctypes.POINTER(UniqueId)],
+        "ncclCommInitRank": [ctypes.POINTER(vp), i32, UniqueId, i32],
+        "ncclCommDestroy": [vp],
+        "ncclAllReduce": [vp, vp, sz, i32, i32, vp, vp],
+        "ncclCommCount": [vp, ctypes.POINTER(i32)],
+        "ncclCommUserRank": [vp, ctypes.POINTER(i32)],
+        "ncclCommCuDevice": [vp, ctypes.POINTER(i32)],
+        "ncclCommGetAsyncError": [vp, ctypes.POINTER(i32)],
+        "ncclGetVersion": [ctypes.POINTER(i32)],
+        "mscclppAmdCommAllReduce": [vp, vp, vp, sz, i32, i32, i32, i32, i32, vp],
+        "mscclppAmdCommBarrier": [vp],
+        "mscclppAmdCommGetDeviceError": [vp, ctypes.POINTER(ctypes.c_uint32), i32],
+        "mscclppAmdCommScratch": [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)],
+        "mscclppAmdCommFlags": [vp, ctypes.POINTER(vp)],
+        "mscclppAmdCommAllGatherHost": [vp, vp, vp, sz],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = ctypes.c_int
+    L.mscclppAmdScratchRequired.argtypes = [i32, i32, sz, i32]
+    L.mscclppAmdScratchRequired.restype = sz
+    L.ncclGetErrorString.argtypes = [i32]
+    L.ncclGetErrorString.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def check(code, what="mscclpp_amd"):
+    if code != 0:
+        raise MscclppError(code, what)
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class DeviceBuffer:
+    """Raw device allocation owned by the library (uncached = hipDeviceMallocUncached)."""
+
+    def __init__(self, nbytes, uncached=True):
+        self.nbytes = nbytes
+        p = ctypes.c_void_p()
+        fn = lib().mscclppAmdMallocUncached if uncached else lib().mscclppAmdMalloc
+        check(fn(ctypes.byref(p), nbytes), "device alloc")
+        self.ptr = p.value
+
+    def free(self):
+        if self.ptr:
+            lib().mscclppAmdFree(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def flags_init(flags_tensor, stream=None):
+    check(lib().mscclppAmdFlagsInit(ctypes.c_void_p(flags_tensor.data_ptr()), stream_ptr(stream)), "flags init")
+
+
+def self_reduce_ll16(x, y, pkts_ptr, out, flags, err, op=SUM, nblocks=0, budget_ticks=0, stream=None):
+    """out = x (op) unpack(pack(y)) -- the 1-GPU LL16 hot path (BASELINE config 2)."""
+    assert x.dtype == y.dtype == out.dtype and x.numel() == y.numel() == out.numel()
+    nbytes = x.numel() * x.element_size()
+    code = lib().mscclppAmdSelfReduceLL16(
+        ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(pkts_ptr),
+        ctypes.c_void_p(out.data_ptr()), nbytes, DTYPE_CODES[x.dtype], op, ctypes.c_void_p(flags.data_ptr()),
+        nblocks, budget_ticks or 2_000_000_000, ctypes.c_void_p(err.data_ptr()), stream_ptr(stream))
+    check(code, "self_reduce_ll16")
+
+
+def scratch_required(algo, nranks, nbytes, dtype_code):
+    return lib().mscclppAmdScratchRequired(algo, nranks, nbytes, dtype_code)
+
+
+class InProcessRanks:
+    """n ranks of one AllReduce inside this process on one GPU (parity tests).
+
+    Every rank gets its own scratch, flags, tokens and error word; peer arrays hold the other
+    ranks' plain device pointers, so the kernels run exactly the multi-rank protocol (one launch,
+    blockIdx.y = rank) without IPC.
+    """
+
+    def __init__(self, nranks, scratch_bytes, bulk_scratch_bytes=0):
+        self.n = nranks
+        self.scratch = [DeviceBuffer(scratch_bytes) for _ in range(nranks)]
+        self.scratch_bytes = scratch_bytes
+        self.bulk = [DeviceBuffer(bulk_scratch_bytes) for _ in range(nranks)] if bulk_scratch_bytes else None
+        self.bulk_bytes = bulk_scratch_bytes
+        tok_elems = MAX_RANKS * MAX_CHANNELS
+        self.tokens = [DeviceBuffer(tok_elems * 8) for _ in range(nranks)]
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.expected = [torch.zeros(tok_elems, dtype=torch.int64, device=dev) for _ in range(nranks)]
+        self.flags = [torch.ones(FLAG_SLOTS, dtype=torch.int32, device=dev) for _ in range(nranks)]
+        self.err = [torch.zeros(64, dtype=torch.int32, device=dev) for _ in range(nranks)]
+
+    def views(self, inputs, outputs, bulk=False):
+        arr = (RankView * self.n)()
+        scr = self.bulk if bulk else self.scratch
+        sbytes = self.bulk_bytes if bulk else self.scratch_bytes
+        for r in range(self.n):
+            v = arr[r]
+            v.input = inputs[r].data_ptr()
+            v.output = outputs[r].data_ptr()
+            v.scratch = scr[r].ptr
+            for q in range(self.n):
+                v.peerScratch[q] = scr[q].ptr
+                v.peerOutput[q] = outputs[q].data_ptr()
+                v.peerTokens[q] = self.tokens[q].ptr
+            v.tokens = self.tokens[r].ptr
+            v.expected = self.expected[r].data_ptr()
+            v.flags = self.flags[r].data_ptr()
+            v.err = self.err[r].data_ptr()
+            v.scratchBytes = sbytes
+            v.rank = r
+        return arr
+
+    def all_reduce(self, inputs, outputs, algo, op=SUM, nblocks=0, nthreads=0, budget_ticks=500_000_000, stream=None):
+        dt = DTYPE_CODES[inputs[0].dtype]
+        nbytes = inputs[0].numel() * inputs[0].element_size()
+        bulk = algo in (ALGO_FULLMESH, ALGO_RSAG)
+        arr = self.views(inputs, outputs, bulk=bulk)
+        code = lib().mscclppAmdAllReduceLaunch(algo, arr, self.n, self.n, nbytes, dt, op, nblocks, nthreads,
+                                               budget_ticks, stream_ptr(stream))
+        check(code, "in-process all_reduce")
+
+    def errors(self):
+        return [int(e[0].item()) for e in self.err]
+
+    def scratch_tensor(self, r, nbytes=None, bulk=False):
+        """Zero-copy uint8 view of rank r's scratch (for packet-image checks)."""
+        buf = (self.bulk if bulk else self.scratch)[r]
+        return device_view(buf.ptr, nbytes or buf.nbytes)
+
+
+class _CudaArray:
+    def __init__(self, ptr, nbytes):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 2}
+
+
+def device_view(ptr, nbytes):
+    """uint8 torch tensor aliasing raw device memory owned by the library."""
+    return torch.as_tensor(_CudaArray(ptr, nbytes), device="cuda")
+
+
+class Communicator:
+    """ncclComm_t wrapper (one rank per process).  Mirrors ncclCommInitRank / ncclAllReduce."""
+
+    def __init__(self, rank, nranks, unique_id_bytes):
+        uid = UniqueId()
+        ctypes.memmove(ctypes.addressof(uid), unique_id_bytes, 128)
+        c = ctypes.c_void_p()
+        check(lib().ncclCommInitRank(ctypes.byref(c), nranks, uid, rank), "ncclCommInitRank")
+        self.comm = c
+        self.rank, self.nranks = rank, nranks
+
+    @staticmethod
+    def unique_id():
+        uid = UniqueId()
+        check(lib().ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+        return bytes(uid.internal) + b"\0" * (128 - len(bytes(uid.internal)))
+
+    @classmethod
+    def from_torch_dist(cls, group=None):
+        import torch.distributed as dist
+
+        rank, n = dist.get_rank(group), dist.get_world_size(group)
+        obj = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return cls(rank, n, obj[0])
+
+    def all_reduce(self, send, recv=None, op="sum", algo=None, nblocks=0, nthreads=0, stream=None):
+        """ncclAllReduce(send, recv, count, dtype, op, comm, stream); algo forces an algorithm."""
+        recv = send if recv is None else recv
+        dt = NCCL_DTYPES[send.dtype]
+        if algo is None:
+            code = lib().ncclAllReduce(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(recv.data_ptr()),
+                                       send.numel(), dt, NCCL_OPS[op], self.comm, stream_ptr(stream))
+        else:
+            code = lib().mscclppAmdCommAllReduce(self.comm, ctypes.c_void_p(send.data_ptr()),
+                                                 ctypes.c_void_p(recv.data_ptr()), send.numel(), dt, NCCL_OPS[op],
+                                                 ALGO_NAMES.get(algo, algo) if isinstance(algo, str) else algo,
+                                                 nblocks, nthreads, stream_ptr(stream))
+        check(code, "ncclAllReduce")
+        return recv
+
+    def barrier(self):
+        check(lib().mscclppAmdCommBarrier(self.comm), "barrier")
+
+    def device_error(self, clear=True):
+        c = ctypes.c_uint32()
+        check(lib().mscclppAmdCommGetDeviceError(self.comm, ctypes.byref(c), 1 if clear else 0), "device error")
+        return c.value
+
+    def destroy(self):
+        if self.comm:
+            check(lib().ncclCommDestroy(self.comm), "ncclCommDestroy")
+            self.comm = None

@@ -1,0 +1,654 @@
+// Host runtime + C ABI of libmscclpp_amd.so.
+//
+//  * memory helpers        -- GpuBuffer / uncached allocation (reference gpu_utils.cc:139-147) and
+//                             the flag buffer (algorithm.cc:251-268)
+//  * AllReduce launcher     -- explicit rank views -> LL16 / LL8 / bulk kernels
+//  * algorithm selector     -- algorithm_selector.cc:91-139 restated for gfx950 + xGMI
+//  * ncclComm + NCCL ABI    -- nccl.cc:187-905: bootstrap, IPC-mapped scratch and semaphores,
+//                             per-buffer registration cache (algorithm.cc:42-68 context cache)
+// Every C entry point catches C++ exceptions and returns an ncclResult_t (SURVEY §8b "Errors").
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "bootstrap.hpp"
+#include "mscclpp_amd/mscclpp_amd.h"
+#include "mscclpp_amd/nccl.h"
+
+namespace mscclpp_amd {
+int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
+                      int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
+int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
+                        int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
+size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype);
+size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype);
+struct BulkGeom;
+size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks);
+}  // namespace mscclpp_amd
+
+using namespace mscclpp_amd;
+
+namespace {
+
+struct HipError : std::runtime_error {
+  hipError_t code;
+  HipError(hipError_t c, const char* what) : std::runtime_error(what), code(c) {}
+};
+
+#define HIPCHECK(cmd)                                                                               \
+  do {                                                                                              \
+    hipError_t e_ = (cmd);                                                                          \
+    if (e_ != hipSuccess) {                                                                         \
+      char buf_[256];                                                                               \
+      snprintf(buf_, sizeof(buf_), "%s:%d %s -> %s", __FILE__, __LINE__, #cmd, hipGetErrorString(e_)); \
+      throw HipError(e_, buf_);                                                                     \
+    }                                                                                               \
+  } while (0)
+
+thread_local std::string gLastError;
+
+int logLevel() {
+  static int lvl = [] {
+    const char* e = std::getenv("MSCCLPP_LOG_LEVEL");
+    if (!e) return 1;
+    std::string s(e);
+    if (s == "DEBUG" || s == "TRACE") return 3;
+    if (s == "INFO") return 2;
+    if (s == "WARN") return 1;
+    return 0;
+  }();
+  return lvl;
+}
+
+void warn(const std::string& m) {
+  gLastError = m;
+  if (logLevel() >= 1) fprintf(stderr, "[mscclpp_amd WARN] %s\n", m.c_str());
+}
+void info(const std::string& m) {
+  if (logLevel() >= 2) fprintf(stderr, "[mscclpp_amd INFO] %s\n", m.c_str());
+}
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const HipError& e) {
+    warn(e.what());
+    return ncclUnhandledCudaError;
+  } catch (const std::exception& e) {
+    warn(e.what());
+    return ncclInternalError;
+  } catch (...) {
+    warn("unknown exception");
+    return ncclInternalError;
+  }
+}
+
+uint64_t spinBudgetTicks() {
+  static uint64_t t = [] {
+    const char* e = std::getenv("MSCCLPP_AMD_SPIN_TIMEOUT_MS");
+    uint64_t ms = e ? std::strtoull(e, nullptr, 10) : 20000;
+    if (ms == 0) ms = 20000;
+    return ms * 100000ull;  // s_memrealtime ticks at 100 MHz
+  }();
+  return t;
+}
+
+void* allocUncached(size_t bytes) {
+  void* p = nullptr;
+  HIPCHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
+  HIPCHECK(hipMemset(p, 0, bytes));
+  return p;
+}
+
+int dtypeFromNccl(ncclDataType_t t) {
+  switch (t) {
+    case ncclFloat16: return MSCCLPP_AMD_F16;
+    case ncclBfloat16: return MSCCLPP_AMD_BF16;
+    case ncclFloat32: return MSCCLPP_AMD_F32;
+    case ncclInt32: return MSCCLPP_AMD_I32;
+    case ncclUint32: return MSCCLPP_AMD_U32;
+    default: return -1;
+  }
+}
+size_t ncclTypeBytes(ncclDataType_t t) {
+  switch (t) {
+    case ncclInt8: case ncclUint8: case ncclFloat8e4m3: case ncclFloat8e5m2: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+    default: return 0;
+  }
+}
+int opFromNccl(ncclRedOp_t op) {
+  if (op == ncclSum) return MSCCLPP_AMD_SUM;
+  if (op == ncclMin) return MSCCLPP_AMD_MIN;
+  return -1;
+}
+
+int envAlgo() {
+  const char* e = std::getenv("MSCCLPP_AMD_ALGO");
+  if (!e) return MSCCLPP_AMD_ALGO_AUTO;
+  std::string s(e);
+  if (s == "packet") return MSCCLPP_AMD_ALGO_PACKET;
+  if (s == "allpair" || s == "allpair_packet") return MSCCLPP_AMD_ALGO_ALLPAIR;
+  if (s == "fullmesh") return MSCCLPP_AMD_ALGO_FULLMESH;
+  if (s == "rsag") return MSCCLPP_AMD_ALGO_RSAG;
+  return MSCCLPP_AMD_ALGO_AUTO;
+}
+
+}  // namespace
+
+// =============================================================================================
+// ncclComm
+// =============================================================================================
+struct IpcBlob {
+  hipIpcMemHandle_t handle;
+  uint64_t base;    // allocation base in the owner's address space (cache key)
+  uint64_t offset;  // pointer - base
+  uint64_t bytes;
+};
+
+struct ncclComm {
+  std::unique_ptr<Bootstrap> boot;
+  int rank = 0, nranks = 1, device = 0;
+  // LL scratch (two halves, packets), bulk scratch, semaphores, flags, error word
+  void* llScratch = nullptr;
+  size_t llBytes = 0;
+  void* bulkScratch = nullptr;
+  size_t bulkBytes = 0;
+  uint64_t* tokens = nullptr;
+  uint64_t* expected = nullptr;
+  uint32_t* flags = nullptr;
+  uint32_t* err = nullptr;
+  std::array<void*, MSCCLPP_AMD_MAX_RANKS> peerLL{}, peerBulk{};
+  std::array<uint64_t*, MSCCLPP_AMD_MAX_RANKS> peerTokens{};
+  // peer mappings opened through IPC: (peer, peer allocation base) -> mapped base here
+  std::map<std::pair<int, uint64_t>, void*> opened;
+  // registered output buffers: local allocation base -> per-peer mapped pointers of that buffer
+  struct Reg {
+    uint64_t bytes;
+    std::array<uint64_t, MSCCLPP_AMD_MAX_RANKS> peerBase;  // mapped peer allocation bases
+    std::array<uint64_t, MSCCLPP_AMD_MAX_RANKS> peerOffsetBase;
+  };
+  std::map<std::pair<uint64_t, uint64_t>, std::array<void*, MSCCLPP_AMD_MAX_RANKS>> outRegs;
+  std::mutex mu;
+
+  // Exchange an IPC handle for [ptr, ptr+bytes) and return every rank's pointer as mapped here.
+  std::array<void*, MSCCLPP_AMD_MAX_RANKS> exchange(void* ptr) {
+    IpcBlob mine{};
+    void* base = nullptr;
+    size_t sz = 0;
+    HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)ptr));
+    HIPCHECK(hipIpcGetMemHandle(&mine.handle, base));
+    mine.base = (uint64_t)base;
+    mine.offset = (uint64_t)((char*)ptr - (char*)base);
+    mine.bytes = sz;
+    std::vector<IpcBlob> all(nranks);
+    boot->allGather(&mine, all.data(), sizeof(IpcBlob));
+    std::array<void*, MSCCLPP_AMD_MAX_RANKS> res{};
+    for (int r = 0; r < nranks; ++r) {
+      if (r == rank) {
+        res[r] = ptr;
+        continue;
+      }
+      auto key = std::make_pair(r, all[r].base);
+      auto it = opened.find(key);
+      void* mapped = nullptr;
+      if (it == opened.end()) {
+        HIPCHECK(hipIpcOpenMemHandle(&mapped, all[r].handle, hipIpcMemLazyEnablePeerAccess));
+        opened[key] = mapped;
+      } else {
+        mapped = it->second;
+      }
+      res[r] = (char*)mapped + all[r].offset;
+    }
+    return res;
+  }
+
+  void forgetMapping(int peer, void* mappedBase) {
+    for (auto it = opened.begin(); it != opened.end(); ++it) {
+      if (it->first.first == peer && it->second == mappedBase) {
+        (void)hipIpcCloseMemHandle(it->second);
+        opened.erase(it);
+        return;
+      }
+    }
+  }
+
+  // Grow a scratch region collectively (every rank calls with the same size at the same call).
+  void ensure(void*& buf, size_t& have, std::array<void*, MSCCLPP_AMD_MAX_RANKS>& peers, size_t need) {
+    if (need <= have) return;
+    size_t want = have ? have : (size_t)64 << 20;
+    while (want < need) want *= 2;
+    HIPCHECK(hipDeviceSynchronize());
+    boot->barrier();  // every rank has drained its previous use of the old buffers
+    for (int r = 0; r < nranks; ++r)
+      if (r != rank && peers[r]) forgetMapping(r, peers[r]);
+    if (buf) HIPCHECK(hipFree(buf));
+    buf = allocUncached(want);
+    have = want;
+    peers = exchange(buf);
+    boot->barrier();
+    info("rank " + std::to_string(rank) + " scratch grown to " + std::to_string(want));
+  }
+
+  std::array<void*, MSCCLPP_AMD_MAX_RANKS> registerOutput(void* out) {
+    void* base = nullptr;
+    size_t sz = 0;
+    HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)out));
+    auto key = std::make_pair((uint64_t)base, (uint64_t)sz);
+    auto it = outRegs.find(key);
+    std::array<void*, MSCCLPP_AMD_MAX_RANKS> peersOfBase;
+    if (it == outRegs.end()) {
+      peersOfBase = exchange(base);  // collective: every rank registers its matching buffer now
+      outRegs[key] = peersOfBase;
+    } else {
+      peersOfBase = it->second;
+    }
+    // The offset of `out` inside its allocation must be the same on every rank for the cached
+    // mapping to be reused; exchange offsets (cheap) to check and build exact pointers.
+    uint64_t off = (uint64_t)((char*)out - (char*)base);
+    std::vector<uint64_t> offs(nranks);
+    boot->allGather(&off, offs.data(), sizeof(off));
+    std::array<void*, MSCCLPP_AMD_MAX_RANKS> res{};
+    for (int r = 0; r < nranks; ++r) res[r] = (r == rank) ? out : (char*)peersOfBase[r] + offs[r];
+    return res;
+  }
+
+  mscclppAmdRankView baseView(const void* in, void* out) {
+    mscclppAmdRankView v{};
+    v.input = in;
+    v.output = out;
+    v.tokens = tokens;
+    v.expected = expected;
+    v.flags = flags;
+    v.err = err;
+    v.rank = rank;
+    for (int r = 0; r < nranks; ++r) v.peerTokens[r] = peerTokens[r];
+    return v;
+  }
+
+  int allReduce(const void* in, void* out, size_t bytes, int dtype, int op, int algo, int nblocks, int nthreads,
+                hipStream_t stream) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = envAlgo();
+    if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = mscclppAmdSelectAlgo(nranks, bytes, dtype);
+    mscclppAmdRankView v = baseView(in, out);
+    if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR) {
+      const size_t need = algo == MSCCLPP_AMD_ALGO_PACKET ? ll16ScratchRequired(nranks, bytes, dtype)
+                                                          : ll8ScratchRequired(nranks, bytes, dtype);
+      ensure(llScratch, llBytes, peerLL, need);
+      v.scratch = llScratch;
+      v.scratchBytes = llBytes;
+      for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerLL[r];
+      return launchAllReduceLL(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
+    }
+    if (algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG) {
+      // a bucket up to 1 GiB fits in one pass with the default 1 GiB bulk scratch
+      size_t need = bytes + 16 * (size_t)nranks * 64;
+      const size_t cap = (size_t)1 << 30;
+      if (need > cap) need = cap;
+      ensure(bulkScratch, bulkBytes, peerBulk, need);
+      v.scratch = bulkScratch;
+      v.scratchBytes = bulkBytes;
+      for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
+      auto outs = registerOutput(out);
+      for (int r = 0; r < nranks; ++r) v.peerOutput[r] = outs[r];
+      return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
+    }
+    return ncclInvalidArgument;
+  }
+
+  void destroy() {
+    (void)hipDeviceSynchronize();
+    if (boot) {
+      try {
+        boot->barrier();
+      } catch (...) {
+      }
+    }
+    for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
+    opened.clear();
+    if (llScratch) (void)hipFree(llScratch);
+    if (bulkScratch) (void)hipFree(bulkScratch);
+    if (tokens) (void)hipFree(tokens);
+    if (expected) (void)hipFree(expected);
+    if (flags) (void)hipFree(flags);
+    if (err) (void)hipFree(err);
+    llScratch = bulkScratch = nullptr;
+    tokens = expected = nullptr;
+    flags = err = nullptr;
+  }
+};
+
+// =============================================================================================
+// C ABI: memory, microbench, launcher, selector
+// =============================================================================================
+extern "C" {
+
+int mscclppAmdMallocUncached(void** ptr, size_t bytes) {
+  return guarded([&] {
+    if (!ptr || !bytes) return (int)ncclInvalidArgument;
+    *ptr = allocUncached(bytes);
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdMalloc(void** ptr, size_t bytes) {
+  return guarded([&] {
+    if (!ptr || !bytes) return (int)ncclInvalidArgument;
+    HIPCHECK(hipMalloc(ptr, bytes));
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdFree(void* ptr) {
+  return guarded([&] {
+    if (ptr) HIPCHECK(hipFree(ptr));
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdFlagsInit(uint32_t* flags, void* stream) {
+  return guarded([&] {
+    if (!flags) return (int)ncclInvalidArgument;
+    std::vector<uint32_t> ones(MSCCLPP_AMD_FLAG_SLOTS, 1u);
+    HIPCHECK(hipMemcpyAsync(flags, ones.data(), ones.size() * 4, hipMemcpyHostToDevice, (hipStream_t)stream));
+    HIPCHECK(hipStreamSynchronize((hipStream_t)stream));
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes,
+                              int dtype, int op, int nblocks, int nthreads, uint64_t budgetTicks, void* stream) {
+  return guarded([&] {
+    if (!views || nviews < 1 || nranks < 2 || nranks > MSCCLPP_AMD_MAX_RANKS || bytes == 0) return (int)ncclInvalidArgument;
+    if (nviews != 1 && nviews != nranks) return (int)ncclInvalidArgument;
+    if (dtype < 0 || dtype > MSCCLPP_AMD_U32 || op < 0 || op > MSCCLPP_AMD_MIN) return (int)ncclInvalidArgument;
+    if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = mscclppAmdSelectAlgo(nranks, bytes, dtype);
+    if (budgetTicks == 0) budgetTicks = spinBudgetTicks();
+    if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR)
+      return launchAllReduceLL(algo, views, nviews, nranks, bytes, dtype, op, nblocks, nthreads, budgetTicks,
+                               (hipStream_t)stream);
+    if (algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG)
+      return launchAllReduceBulk(algo, views, nviews, nranks, bytes, dtype, op, nblocks, nthreads, budgetTicks,
+                                 (hipStream_t)stream);
+    return (int)ncclInvalidArgument;
+  });
+}
+
+size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype) {
+  if (algo == MSCCLPP_AMD_ALGO_PACKET) return ll16ScratchRequired(nranks, bytes, dtype);
+  if (algo == MSCCLPP_AMD_ALGO_ALLPAIR) return ll8ScratchRequired(nranks, bytes, dtype);
+  if (algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG) {
+    return bulkScratchRequired(nranks, bytes, (size_t)1 << 40, nullptr, 64);
+  }
+  return 0;
+}
+
+// algorithm_selector.cc:91-139 for an AMD node: <= 16 KiB one-hop LL8, <= 1 MiB two-hop LL16,
+// larger buckets the bulk all-pairs path.
+int mscclppAmdSelectAlgo(int nranks, size_t bytes, int dtype) {
+  (void)nranks;
+  (void)dtype;
+  if (bytes <= ((size_t)1 << 14)) return MSCCLPP_AMD_ALGO_ALLPAIR;
+  if (bytes <= ((size_t)1 << 20)) return MSCCLPP_AMD_ALGO_PACKET;
+  return MSCCLPP_AMD_ALGO_FULLMESH;
+}
+
+// =============================================================================================
+// NCCL ABI (nccl.cc)
+// =============================================================================================
+ncclResult_t ncclGetVersion(int* version) {
+  if (!version) return ncclInvalidArgument;
+  *version = NCCL_VERSION_CODE;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclGetUniqueId(ncclUniqueId* uniqueId) {
+  return (ncclResult_t)guarded([&] {
+    if (!uniqueId) return (int)ncclInvalidArgument;
+    BootstrapId id = bootstrapCreateRoot();
+    std::memcpy(uniqueId, &id, sizeof(id));
+    return (int)ncclSuccess;
+  });
+}
+
+ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank) {
+  return (ncclResult_t)guarded([&] {
+    if (!comm) return (int)ncclInvalidArgument;
+    if (nranks <= 0 || rank < 0 || rank >= nranks) return (int)ncclInvalidArgument;
+    if (nranks > MSCCLPP_AMD_MAX_RANKS) {
+      warn("mscclpp_amd covers one MI355X node: at most 8 ranks");
+      return (int)ncclInvalidUsage;
+    }
+    BootstrapId id;
+    std::memcpy(&id, &commId, sizeof(id));
+    if (!bootstrapIdValid(id)) return (int)ncclInvalidArgument;
+    auto c = std::make_unique<ncclComm>();
+    c->rank = rank;
+    c->nranks = nranks;
+    HIPCHECK(hipGetDevice(&c->device));
+    const char* to = std::getenv("MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S");
+    c->boot = std::make_unique<Bootstrap>(rank, nranks, id, to ? std::atoi(to) : 600);
+    const size_t tokBytes = sizeof(uint64_t) * MSCCLPP_AMD_MAX_RANKS * MSCCLPP_AMD_MAX_CHANNELS;
+    c->tokens = (uint64_t*)allocUncached(tokBytes);
+    HIPCHECK(hipMalloc((void**)&c->expected, tokBytes));
+    HIPCHECK(hipMemset(c->expected, 0, tokBytes));
+    HIPCHECK(hipMalloc((void**)&c->flags, MSCCLPP_AMD_FLAG_SLOTS * sizeof(uint32_t)));
+    {
+      std::vector<uint32_t> ones(MSCCLPP_AMD_FLAG_SLOTS, 1u);
+      HIPCHECK(hipMemcpy(c->flags, ones.data(), ones.size() * 4, hipMemcpyHostToDevice));
+    }
+    HIPCHECK(hipMalloc((void**)&c->err, 256));
+    HIPCHECK(hipMemset(c->err, 0, 256));
+    if (nranks > 1) {
+      auto toks = c->exchange(c->tokens);
+      for (int r = 0; r < nranks; ++r) c->peerTokens[r] = (uint64_t*)toks[r];
+      c->ensure(c->llScratch, c->llBytes, c->peerLL, (size_t)64 << 20);
+    }
+    HIPCHECK(hipDeviceSynchronize());
+    c->boot->barrier();
+    *comm = c.release();
+    return (int)ncclSuccess;
+  });
+}
+
+ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank, ncclConfig_t*) {
+  return ncclCommInitRank(comm, nranks, commId, rank);
+}
+
+ncclResult_t ncclCommInitAll(ncclComm_t* comm, int ndev, const int*) {
+  if (ndev == 1) {
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return r;
+    return ncclCommInitRank(comm, 1, id, 0);
+  }
+  warn("ncclCommInitAll with more than one device is unavailable (one process per GPU), as in nccl.cc:351-360");
+  return ncclInternalError;
+}
+
+ncclResult_t ncclCommFinalize(ncclComm_t comm) {
+  if (!comm) return ncclInvalidArgument;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  if (!comm) return ncclInvalidArgument;
+  return (ncclResult_t)guarded([&] {
+    comm->destroy();
+    delete comm;
+    return (int)ncclSuccess;
+  });
+}
+
+ncclResult_t ncclCommAbort(ncclComm_t comm) {
+  if (!comm) return ncclSuccess;
+  return ncclCommDestroy(comm);
+}
+
+const char* ncclGetErrorString(ncclResult_t result) {
+  switch (result) {
+    case ncclSuccess: return "no error";
+    case ncclUnhandledCudaError: return "unhandled HIP error";
+    case ncclSystemError: return "unhandled system error";
+    case ncclInternalError: return "internal error";
+    case ncclInvalidArgument: return "invalid argument";
+    case ncclInvalidUsage: return "invalid usage";
+    case ncclRemoteError: return "remote process exited or there was a network error";
+    case ncclInProgress: return "NCCL operation in progress";
+    default: return "unknown result code";
+  }
+}
+
+const char* ncclGetLastError(ncclComm_t) { return gLastError.c_str(); }
+
+ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
+  if (!comm || !asyncError) return ncclInvalidArgument;
+  uint32_t code = 0;
+  if (hipMemcpy(&code, comm->err, sizeof(code), hipMemcpyDeviceToHost) != hipSuccess) {
+    *asyncError = ncclUnhandledCudaError;
+    return ncclSuccess;
+  }
+  *asyncError = code ? ncclRemoteError : ncclSuccess;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+  if (!comm || !count) return ncclInvalidArgument;
+  *count = comm->nranks;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device) {
+  if (!comm || !device) return ncclInvalidArgument;
+  *device = comm->device;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
+  if (!comm || !rank) return ncclInvalidArgument;
+  *rank = comm->rank;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                           ncclRedOp_t op, ncclComm_t comm, void* stream) {
+  return (ncclResult_t)guarded([&] {
+    if (!comm) return (int)ncclInvalidArgument;
+    const size_t tb = ncclTypeBytes(datatype);
+    const size_t bytes = count * tb;
+    if (comm->nranks == 1) {  // nccl.cc:610-615
+      if (sendbuff != recvbuff && bytes)
+        HIPCHECK(hipMemcpyAsync(recvbuff, sendbuff, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+      return (int)ncclSuccess;
+    }
+    if (!sendbuff || !recvbuff || count == 0 || tb == 0) return (int)ncclInvalidArgument;  // nccl.cc:617-622
+    const int dt = dtypeFromNccl(datatype);
+    const int o = opFromNccl(op);
+    if (dt < 0 || o < 0) {
+      warn("unsupported dtype/op for AllReduce (supported: fp16, bf16, fp32, int32, uint32 x sum, min)");
+      return (int)ncclInvalidArgument;
+    }
+    return comm->allReduce(sendbuff, recvbuff, bytes, dt, o, MSCCLPP_AMD_ALGO_AUTO, 0, 0, (hipStream_t)stream);
+  });
+}
+
+ncclResult_t ncclReduceScatter(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, void*) {
+  warn("ncclReduceScatter: not on the AllReduce hot path yet (SURVEY §8f row 2)");
+  return ncclInvalidUsage;
+}
+
+ncclResult_t ncclAllGather(const void*, void*, size_t, ncclDataType_t, ncclComm_t, void*) {
+  warn("ncclAllGather: not on the AllReduce hot path yet (SURVEY §8f row 2)");
+  return ncclInvalidUsage;
+}
+
+ncclResult_t ncclGroupStart(void) { return ncclSuccess; }
+ncclResult_t ncclGroupEnd(void) { return ncclSuccess; }
+
+ncclResult_t ncclMemAlloc(void** ptr, size_t size) {
+  return (ncclResult_t)guarded([&] {
+    if (!ptr || !size) return (int)ncclInvalidArgument;
+    HIPCHECK(hipMalloc(ptr, size));
+    return (int)ncclSuccess;
+  });
+}
+
+ncclResult_t ncclMemFree(void* ptr) {
+  return (ncclResult_t)guarded([&] {
+    if (ptr) HIPCHECK(hipFree(ptr));
+    return (int)ncclSuccess;
+  });
+}
+
+// =============================================================================================
+// communicator extensions
+// =============================================================================================
+int mscclppAmdCommAllReduce(ncclComm_t comm, const void* sendbuff, void* recvbuff, size_t count, int ncclDtype,
+                            int ncclOp, int algo, int nblocks, int nthreads, void* stream) {
+  return guarded([&] {
+    if (!comm || !sendbuff || !recvbuff || count == 0) return (int)ncclInvalidArgument;
+    const size_t tb = ncclTypeBytes((ncclDataType_t)ncclDtype);
+    const int dt = dtypeFromNccl((ncclDataType_t)ncclDtype);
+    const int o = opFromNccl((ncclRedOp_t)ncclOp);
+    if (dt < 0 || o < 0 || tb == 0) return (int)ncclInvalidArgument;
+    if (comm->nranks == 1) {
+      if (sendbuff != recvbuff)
+        HIPCHECK(hipMemcpyAsync(recvbuff, sendbuff, count * tb, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+      return (int)ncclSuccess;
+    }
+    return comm->allReduce(sendbuff, recvbuff, count * tb, dt, o, algo, nblocks, nthreads, (hipStream_t)stream);
+  });
+}
+
+int mscclppAmdCommBarrier(ncclComm_t comm) {
+  return guarded([&] {
+    if (!comm) return (int)ncclInvalidArgument;
+    comm->boot->barrier();
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear) {
+  return guarded([&] {
+    if (!comm || !code) return (int)ncclInvalidArgument;
+    HIPCHECK(hipMemcpy(code, comm->err, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (clear) HIPCHECK(hipMemset(comm->err, 0, sizeof(uint32_t)));
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes) {
+  if (!comm || !scratch || !bytes) return ncclInvalidArgument;
+  *scratch = comm->llScratch;
+  *bytes = comm->llBytes;
+  return ncclSuccess;
+}
+
+int mscclppAmdCommFlags(ncclComm_t comm, uint32_t** flags) {
+  if (!comm || !flags) return ncclInvalidArgument;
+  *flags = comm->flags;
+  return ncclSuccess;
+}
+
+int mscclppAmdCommAllGatherHost(ncclComm_t comm, const void* sendbuf, void* recvbuf, size_t bytes) {
+  return guarded([&] {
+    if (!comm) return (int)ncclInvalidArgument;
+    comm->boot->allGather(sendbuf, recvbuf, bytes);
+    return (int)ncclSuccess;
+  });
+}
+
+}  // extern "C"

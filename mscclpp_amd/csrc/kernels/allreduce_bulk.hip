@@ -1,0 +1,208 @@
+// Bulk (non-LL) all-pairs AllReduce for large buckets over xGMI.
+//
+// Reference behaviour: allreduceFullmesh (src/ext/collectives/allreduce/allreduce_fullmesh.cu:24-166,
+// the AMD default above 1 MiB, algorithm_selector.cc:129-131) -- a signal-gated reduce-scatter by
+// one-sided puts into peer scratch, a local reduction (own slice first, then peers ascending,
+// :101-107) and an all-gather by direct writes into every peer's output buffer (:110-113).  The
+// ORDER=1 variant sums in ring order x_r, x_{r+1}, ... (allreduceRsAg, allreduce_rsag.cu:85-94),
+// the order-stable fp32 sum of BASELINE config 5.
+//
+// MI355X design:
+//  * The whole per-rank slice is exchanged in at most a few passes; scratch is sized for it (HBM is
+//    288 GB), so a 48 MiB bucket is one pass with one RS handshake and one AG handshake per block.
+//  * Each workgroup owns one channel (its sub-range of every slice) and one semaphore per peer, so
+//    workgroups never wait on each other, and every workgroup streams to all 7 peers at once,
+//    starting at a different peer (rotation by block index) to keep all 7 xGMI links busy.
+//  * Remote stores are 16-byte system-scope write-through buffer stores; each storing wave drains
+//    (s_waitcnt vmcnt(0)) before the workgroup barrier, and one lane per peer then signals with a
+//    system-scope release atomic add (MemoryDevice2DeviceSemaphore::signal, semaphore_device.hpp:84-90).
+//  * Waits are relaxed system-scope polls followed by one system-scope acquire, bounded in time.
+#include "common.hpp"
+
+namespace mscclpp_amd {
+
+struct BulkGeom {
+  uint64_t bytes;       // total bytes per rank
+  uint64_t slice;       // bytes per rank slice (multiple of 16)
+  uint64_t pass;        // slice bytes handled per pass (multiple of 16)
+  uint64_t blk;         // bytes of a pass handled by one workgroup (multiple of 16)
+  uint32_t npasses;
+  uint32_t pad;
+};
+
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// All lanes of the block: publish every prior store, then lane p < nranks signals peer p on
+// channel `ch`; then lanes wait for the peers' matching signals.
+__device__ __forceinline__ void block_handshake(const mscclppAmdRankView& v, int nranks, int rank, uint32_t ch,
+                                                uint64_t budget) {
+  drain_stores();
+  __syncthreads();
+  const int p = (int)threadIdx.x;
+  if (p < nranks && p != rank) {
+    // my token slot inside peer p's token array: [rank][ch]
+    uint64_t* remote = v.peerTokens[p] + (uint64_t)rank * kMaxChannels + ch;
+    add_release_sys(remote, 1);
+    uint64_t* mine = v.tokens + (uint64_t)p * kMaxChannels + ch;
+    uint64_t* exp = v.expected + (uint64_t)p * kMaxChannels + ch;
+    const uint64_t want = *exp + 1;
+    *exp = want;
+    SpinGuard g(budget);
+    while (ld_relaxed_sys(mine) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (g.expired()) {
+        report_error(v.err, kErrSemaphoreTimeout);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+template <int DT, int OP, int NV, int ORDER>
+__global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, BulkGeom g, int nranks, uint64_t budget) {
+  const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
+  const int rank = v.rank;
+  const uint32_t T = blockDim.x, tid = threadIdx.x, b = blockIdx.x, G = gridDim.x;
+  const uint8_t* in = (const uint8_t*)v.input;
+  uint8_t* out = (uint8_t*)v.output;
+  uint8_t* scr = (uint8_t*)v.scratch;
+  constexpr int U = 2;  // units per lane per step
+
+  for (uint32_t ps = 0; ps < g.npasses; ++ps) {
+    const uint64_t pOff = (uint64_t)ps * g.pass;          // offset inside a slice
+    const uint64_t bOff = pOff + (uint64_t)b * g.blk;     // this block's sub-range start in a slice
+    uint64_t bLen = 0;
+    if ((uint64_t)b * g.blk < g.pass && bOff < g.slice) {
+      bLen = g.blk;
+      if (bOff + bLen > pOff + g.pass) bLen = pOff + g.pass - bOff;
+      if (bOff + bLen > g.slice) bLen = g.slice - bOff;
+    }
+    const uint32_t nUnits = (uint32_t)((bLen + 15) / 16);
+
+    // ---- reduce-scatter: put my copy of every peer's slice sub-range into that peer's scratch
+    if (nUnits) {
+#pragma unroll 1
+      for (int i = 0; i < nranks - 1; ++i) {
+        // rotate the first peer by block index so concurrent blocks start on different links
+        const int k = (i + (int)b) % (nranks - 1);
+        const int q = k < rank ? k : k + 1;
+        const uint64_t srcOff = (uint64_t)q * g.slice + bOff;
+        const auto rsrc = make_rsrc(in + srcOff);
+        const uint64_t valid = g.bytes > srcOff ? g.bytes - srcOff : 0;
+        for (uint32_t u0 = tid; u0 < nUnits; u0 += T * U) {
+          u32x4 w[U];
+#pragma unroll
+          for (int k2 = 0; k2 < U; ++k2) {
+            const uint32_t u = u0 + k2 * T;
+            if (u < nUnits) w[k2] = load_payload<kNonTemporal>(rsrc, in + srcOff, (uint64_t)u * 16, clamp_valid(valid, (uint64_t)u * 16, 16));
+          }
+          // remote scratch of peer q: region of source `rank`
+          const auto rq = make_rsrc((uint8_t*)v.peerScratch[q] + (uint64_t)rank * g.pass + (bOff - pOff));
+#pragma unroll
+          for (int k2 = 0; k2 < U; ++k2) {
+            const uint32_t u = u0 + k2 * T;
+            if (u < nUnits) store16<kSystem>(rq, u * 16u, w[k2]);
+          }
+        }
+      }
+    }
+    block_handshake(v, nranks, rank, b, budget);
+
+    // ---- reduce my slice sub-range; write it locally and into every peer's output (all-gather)
+    if (nUnits) {
+      const uint64_t myOff = (uint64_t)rank * g.slice + bOff;
+      const uint64_t valid = g.bytes > myOff ? g.bytes - myOff : 0;
+      const auto rin = make_rsrc(in + myOff);
+      const auto rout = make_rsrc(out + myOff);
+      const auto rscr = make_rsrc(scr + (bOff - pOff));
+      for (uint32_t u = tid; u < nUnits; u += T) {
+        const uint32_t vb = clamp_valid(valid, (uint64_t)u * 16, 16);
+        u32x4 acc = load_payload<kNonTemporal>(rin, in + myOff, (uint64_t)u * 16, vb);
+        u32x4 w[kMaxRanks];
+#pragma unroll
+        for (int k = 1; k < kMaxRanks; ++k) {
+          if (k < nranks) {
+            const int src = ORDER == 0 ? (k - 1 < rank ? k - 1 : k) : (rank + k) % nranks;
+            w[k] = load16<kSystem>(rscr, (uint32_t)((uint64_t)src * g.pass) + u * 16u);
+          }
+        }
+#pragma unroll
+        for (int k = 1; k < kMaxRanks; ++k)
+          if (k < nranks) acc = reduce4<DT, OP>(acc, w[k]);
+        store_payload<kPlain>(rout, out + myOff, (uint64_t)u * 16, acc, vb);
+#pragma unroll 1
+        for (int i = 0; i < nranks - 1; ++i) {
+          const int k = (i + (int)b) % (nranks - 1);
+          const int q = k < rank ? k : k + 1;
+          uint8_t* po = (uint8_t*)v.peerOutput[q] + myOff;
+          if (vb >= 16)
+            store16<kSystem>(make_rsrc(po), u * 16u, acc);
+          else
+            store_tail(po + (uint64_t)u * 16, acc, vb);
+        }
+      }
+    }
+    block_handshake(v, nranks, rank, b, budget);
+  }
+  (void)G;
+}
+
+size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks) {
+  BulkGeom g{};
+  g.bytes = bytes;
+  const uint64_t per = (bytes + nranks - 1) / nranks;
+  g.slice = (per + 15) & ~15ull;
+  // largest pass whose n regions fit the scratch budget
+  uint64_t pass = g.slice;
+  const uint64_t cap = maxScratch / (uint64_t)nranks;
+  if (pass > cap) pass = cap / ((uint64_t)16 * nblocks) * ((uint64_t)16 * nblocks);
+  if (pass == 0) return 0;
+  g.pass = pass;
+  g.npasses = (uint32_t)((g.slice + pass - 1) / pass);
+  g.blk = ((pass + nblocks - 1) / nblocks + 15) & ~15ull;
+  if (out) *out = g;
+  return (size_t)(nranks * pass);
+}
+
+template <int DT, int OP, int NV, int ORDER>
+static void launchBulkT(const Views<NV>& vw, const BulkGeom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
+                        hipStream_t s) {
+  hipLaunchKernelGGL((allreduceBulkKernel<DT, OP, NV, ORDER>), dim3(nblocks, NV), dim3(nthreads), 0, s, vw, g, nranks,
+                     budget);
+}
+
+template <int DT, int OP>
+static void launchBulk(const mscclppAmdRankView* views, int nviews, const BulkGeom& g, int nranks, int nblocks,
+                       int nthreads, uint64_t budget, hipStream_t s, int order) {
+  if (nviews == 1) {
+    Views<1> vw;
+    vw.v[0] = views[0];
+    if (order == 0)
+      launchBulkT<DT, OP, 1, 0>(vw, g, nranks, nblocks, nthreads, budget, s);
+    else
+      launchBulkT<DT, OP, 1, 1>(vw, g, nranks, nblocks, nthreads, budget, s);
+  } else {
+    Views<kMaxRanks> vw{};
+    for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
+    if (order == 0)
+      launchBulkT<DT, OP, kMaxRanks, 0>(vw, g, nranks, nblocks, nthreads, budget, s);
+    else
+      launchBulkT<DT, OP, kMaxRanks, 1>(vw, g, nranks, nblocks, nthreads, budget, s);
+  }
+}
+
+int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
+                        int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s) {
+  if (nblocks <= 0) nblocks = 64;
+  if (nthreads <= 0) nthreads = 512;
+  if (nblocks > kMaxChannels || nthreads > 512 || nthreads % 64 || nthreads < 64) return 4;
+  BulkGeom g{};
+  if (!bulkScratchRequired(nranks, bytes, views[0].scratchBytes, &g, nblocks)) return 5;
+  const int order = algo == MSCCLPP_AMD_ALGO_RSAG ? 1 : 0;
+  MSCCLPP_AMD_DISPATCH(dtype, op, launchBulk, views, nviews, g, nranks, nblocks, nthreads, budget, s, order);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+}  // namespace mscclpp_amd

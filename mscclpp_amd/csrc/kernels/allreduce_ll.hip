@@ -1,0 +1,386 @@
+// LL-packet AllReduce kernels for gfx950 over xGMI.
+//
+//  allreduceLL16  -- two-hop LL16 (reference: allreducePacket, src/ext/collectives/allreduce/
+//                    allreduce_packet.cu:15-151).  Step 1 packs this rank's copy of slice q into
+//                    rank q's scratch (one-sided put over xGMI); step 2 polls the n-1 packet
+//                    streams of its own slice, sums (own first, then peers ascending), writes the
+//                    result locally and broadcasts it as LL16 packets; step 3 unpacks the peers'
+//                    reduced slices.  Scratch layout, flag lifecycle and sum order follow the
+//                    reference exactly.
+//  allreduceLL8   -- one-hop LL8 (reference: allreduceAllPairs, allreduce_allpair_packet.cu:15-69).
+//                    Every rank puts its whole buffer as LL8 packets into every peer's scratch and
+//                    reduces all n streams locally.
+//
+// gfx950 choices (vs. the reference's CUDA-shaped loops): one lane moves 16 payload bytes = two
+// LL16 packets (or four LL8 packets) as two 16-byte buffer stores with system-scope write-through
+// (sc0 sc1); polls are 16-byte system-scope loads issued for all peers before any spin; peer
+// pointers come from kernel arguments (scalar loads), not from channel handles copied to LDS; loops
+// over peers are unrolled to the 8-GPU maximum with predicates so the per-peer values stay in VGPRs.
+#include "common.hpp"
+
+namespace mscclpp_amd {
+
+struct LL16Geom {
+  uint64_t bytes;   // payload bytes actually in the buffers
+  uint64_t W;       // 32-bit words the algorithm covers (allreduce_packet.cu:51-54)
+  uint64_t wpr;     // words per rank slice, even (:62-63)
+  uint64_t ppr;     // packets per rank slice
+  uint64_t roff;    // byte offset of the reduced-slice region inside a scratch half (:74)
+  uint32_t units;   // 2-packet units per slice = ceil(ppr / 2)
+  uint32_t pad;
+};
+
+struct LL8Geom {
+  uint64_t bytes;
+  uint64_t W;       // words (= LL8 packets) per rank buffer (allreduce_allpair_packet.cu:20)
+  uint32_t units;   // ceil(W / 4)
+  uint32_t pad;
+};
+
+// ---- LL16 unit helpers (a unit is 2 packets, or 1 for the odd last packet of a slice) ----------
+template <int Policy>
+__device__ __forceinline__ void ll16_put(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, u32x4 w, uint32_t flag, bool two) {
+  store16<Policy>(pk, pbyte, LL16Packet::make(w.x, w.y, flag));
+  if (two) store16<Policy>(pk, pbyte + 16, LL16Packet::make(w.z, w.w, flag));
+}
+__device__ __forceinline__ bool ll16_try(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, u32x4& w, bool two) {
+  u32x4 a = load16<kSystem>(pk, pbyte);
+  u32x4 c = two ? load16<kSystem>(pk, pbyte + 16) : u32x4{0, flag, 0, flag};
+  w = u32x4{a.x, a.z, c.x, c.z};
+  return LL16Packet::ready(a, flag) && LL16Packet::ready(c, flag);
+}
+__device__ __forceinline__ u32x4 ll16_get(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, bool two,
+                                          uint64_t budget, uint32_t* err) {
+  u32x4 w;
+  if (ll16_try(pk, pbyte, flag, w, two)) return w;
+  SpinGuard g(budget);
+  while (!ll16_try(pk, pbyte, flag, w, two)) {
+    __builtin_amdgcn_s_sleep(1);
+    if (g.expired()) {
+      report_error(err, kErrPacketTimeout);
+      return u32x4{0, 0, 0, 0};
+    }
+  }
+  return w;
+}
+
+template <int DT, int OP, int NV>
+__global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16Geom g, int nranks, uint64_t budget) {
+  const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
+  const int rank = v.rank;
+  const int nPeers = nranks - 1;
+  const uint32_t T = blockDim.x, tid = threadIdx.x, G = gridDim.x, b = blockIdx.x;
+  const uint32_t flag = v.flags[b];
+  const uint64_t base = (flag & 1u) ? v.scratchBytes / 2 : 0;  // numScratchBuff = 2 (allreduce_packet.cu:60)
+  const uint8_t* in = (const uint8_t*)v.input;
+  uint8_t* out = (uint8_t*)v.output;
+  uint8_t* scr = (uint8_t*)v.scratch + base;
+  const auto rin = make_rsrc(in);
+  const auto rout = make_rsrc(out);
+  const uint64_t sliceBytes = g.wpr * 4;
+  const uint32_t bpp = G / (uint32_t)nPeers;  // blocks per peer for steps 1 and 3
+  const bool inPeerGroup = b < bpp * (uint32_t)nPeers;
+  const int peerIdx = inPeerGroup ? (int)(b / bpp) : 0;
+  const int remote = peerIdx < rank ? peerIdx : peerIdx + 1;
+  const uint32_t lb = inPeerGroup ? b % bpp : 0;
+
+  // step 1: put my copy of slice `remote` into rank `remote`'s scratch at rank*ppr packets
+  if (inPeerGroup) {
+    const auto rdst = make_rsrc((uint8_t*)v.peerScratch[remote] + base + (uint64_t)rank * g.ppr * 16);
+    const uint64_t soff = (uint64_t)remote * sliceBytes;
+    for (uint32_t j = lb * T + tid; j < g.units; j += bpp * T) {
+      const bool two = 2ull * j + 1 < g.ppr;
+      const uint64_t off = soff + (uint64_t)j * 16;
+      const u32x4 w = load_payload<kPlain>(rin, in, off, clamp_valid(g.bytes, off, two ? 16 : 8));
+      ll16_put<kSystem>(rdst, j * 32u, w, flag, two);
+    }
+  }
+
+  // step 2: reduce my slice from the n-1 incoming streams, store locally, broadcast the result
+  {
+    const auto rscr = make_rsrc(scr);
+    const uint64_t soff = (uint64_t)rank * sliceBytes;
+    for (uint32_t j = b * T + tid; j < g.units; j += G * T) {
+      const bool two = 2ull * j + 1 < g.ppr;
+      const uint64_t off = soff + (uint64_t)j * 16;
+      const uint32_t valid = clamp_valid(g.bytes, off, two ? 16 : 8);
+      u32x4 acc = load_payload<kPlain>(rin, in, off, valid);
+      u32x4 w[kMaxRanks];
+      bool ready = true;
+#pragma unroll
+      for (int p = 0; p < kMaxRanks; ++p)
+        if (p < nranks && p != rank) ready &= ll16_try(rscr, (uint32_t)(p * g.ppr * 16) + j * 32u, flag, w[p], two);
+      if (ready) {
+#pragma unroll
+        for (int p = 0; p < kMaxRanks; ++p)
+          if (p < nranks && p != rank) acc = reduce4<DT, OP>(acc, w[p]);
+      } else {
+        // slow path: wait for each stream in sum order (own first, then peers ascending)
+        for (int p = 0; p < nranks; ++p) {
+          if (p == rank) continue;
+          acc = reduce4<DT, OP>(acc, ll16_get(rscr, (uint32_t)(p * g.ppr * 16) + j * 32u, flag, two, budget, v.err));
+        }
+      }
+      store_payload<kPlain>(rout, out, off, acc, valid);
+      // broadcast: a runtime loop, so one descriptor is live at a time (SGPR budget)
+#pragma unroll 1
+      for (int q = 0; q < nranks; ++q) {
+        if (q == rank) continue;
+        const auto rq = make_rsrc((uint8_t*)v.peerScratch[q] + base + g.roff + (uint64_t)rank * g.ppr * 16);
+        ll16_put<kSystem>(rq, j * 32u, acc, flag, two);
+      }
+    }
+  }
+
+  // step 3: unpack the reduced slice of peer `remote`
+  if (inPeerGroup) {
+    const auto rres = make_rsrc(scr + g.roff + (uint64_t)remote * g.ppr * 16);
+    const uint64_t soff = (uint64_t)remote * sliceBytes;
+    for (uint32_t j = lb * T + tid; j < g.units; j += bpp * T) {
+      const bool two = 2ull * j + 1 < g.ppr;
+      const uint64_t off = soff + (uint64_t)j * 16;
+      const u32x4 w = ll16_get(rres, j * 32u, flag, two, budget, v.err);
+      store_payload<kPlain>(rout, out, off, w, clamp_valid(g.bytes, off, two ? 16 : 8));
+    }
+  }
+  bump_flags(v.flags, flag);
+}
+
+// ---- LL8 ----------------------------------------------------------------------------------------
+template <int Policy>
+__device__ __forceinline__ void ll8_put(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, u32x4 w, uint32_t flag, uint32_t npk) {
+  if (npk == 4) {
+    store16<Policy>(pk, pbyte, u32x4{w.x, flag, w.y, flag});
+    store16<Policy>(pk, pbyte + 16, u32x4{w.z, flag, w.w, flag});
+  } else {
+    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((uint32_t)i < npk) store8<Policy>(pk, pbyte + 8 * i, u32x2{d[i], flag});
+  }
+}
+__device__ __forceinline__ bool ll8_try(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, u32x4& w, uint32_t npk) {
+  if (npk == 4) {
+    u32x4 a = load16<kSystem>(pk, pbyte);
+    u32x4 c = load16<kSystem>(pk, pbyte + 16);
+    w = u32x4{a.x, a.z, c.x, c.z};
+    return a.y == flag && a.w == flag && c.y == flag && c.w == flag;
+  }
+  uint32_t d[4] = {0, 0, 0, 0};
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if ((uint32_t)i < npk) {
+      u32x2 x = load8<kSystem>(pk, pbyte + 8 * i);
+      d[i] = x.x;
+      ok &= x.y == flag;
+    }
+  }
+  w = u32x4{d[0], d[1], d[2], d[3]};
+  return ok;
+}
+__device__ __forceinline__ u32x4 ll8_get(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, uint32_t npk,
+                                         uint64_t budget, uint32_t* err) {
+  u32x4 w;
+  if (ll8_try(pk, pbyte, flag, w, npk)) return w;
+  SpinGuard g(budget);
+  while (!ll8_try(pk, pbyte, flag, w, npk)) {
+    __builtin_amdgcn_s_sleep(1);
+    if (g.expired()) {
+      report_error(err, kErrPacketTimeout);
+      return u32x4{0, 0, 0, 0};
+    }
+  }
+  return w;
+}
+
+template <int DT, int OP, int NV>
+__global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Geom g, int nranks, uint64_t budget) {
+  const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
+  const int rank = v.rank;
+  const uint32_t T = blockDim.x, G = gridDim.x;
+  const uint32_t gtid = blockIdx.x * T + threadIdx.x;
+  const uint32_t flag = v.flags[blockIdx.x];
+  const uint64_t base = (flag & 1u) ? v.scratchBytes / 2 : 0;
+  const uint8_t* in = (const uint8_t*)v.input;
+  uint8_t* out = (uint8_t*)v.output;
+  const auto rin = make_rsrc(in);
+  const auto rout = make_rsrc(out);
+  const uint64_t region = g.W * 8;  // LL8 bytes one source rank occupies in a peer's scratch half
+
+  // put my whole buffer into every peer's scratch at rank*W packets (allreduce_allpair_packet.cu:39-42)
+  for (uint32_t j = gtid; j < g.units; j += G * T) {
+    const uint32_t npk = (uint32_t)((g.W - 4ull * j) < 4 ? (g.W - 4ull * j) : 4);
+    const uint64_t off = (uint64_t)j * 16;
+    const u32x4 w = load_payload<kPlain>(rin, in, off, clamp_valid(g.bytes, off, npk * 4));
+#pragma unroll 1
+    for (int q = 0; q < nranks; ++q) {
+      if (q == rank) continue;
+      const auto rq = make_rsrc((uint8_t*)v.peerScratch[q] + base + (uint64_t)rank * region);
+      ll8_put<kSystem>(rq, j * 32u, w, flag, npk);
+    }
+  }
+  // reduce: own first, then peers ascending (:49-61).  The same lane handled unit j above, so an
+  // in-place call reads its input before overwriting it.
+  const auto rscr = make_rsrc((uint8_t*)v.scratch + base);
+  for (uint32_t j = gtid; j < g.units; j += G * T) {
+    const uint32_t npk = (uint32_t)((g.W - 4ull * j) < 4 ? (g.W - 4ull * j) : 4);
+    const uint64_t off = (uint64_t)j * 16;
+    const uint32_t valid = clamp_valid(g.bytes, off, npk * 4);
+    u32x4 acc = load_payload<kPlain>(rin, in, off, valid);
+    u32x4 w[kMaxRanks];
+    bool ready = true;
+#pragma unroll
+    for (int p = 0; p < kMaxRanks; ++p)
+      if (p < nranks && p != rank) ready &= ll8_try(rscr, (uint32_t)(p * region) + j * 32u, flag, w[p], npk);
+    if (ready) {
+#pragma unroll
+      for (int p = 0; p < kMaxRanks; ++p)
+        if (p < nranks && p != rank) acc = reduce4<DT, OP>(acc, w[p]);
+    } else {
+      for (int p = 0; p < nranks; ++p) {
+        if (p == rank) continue;
+        acc = reduce4<DT, OP>(acc, ll8_get(rscr, (uint32_t)(p * region) + j * 32u, flag, npk, budget, v.err));
+      }
+    }
+    store_payload<kPlain>(rout, out, off, acc, valid);
+  }
+  bump_flags(v.flags, flag);
+}
+
+// ---- host-side geometry + launch -------------------------------------------------------------------
+static inline bool is2byte(int dtype) { return dtype == kF16 || dtype == kBF16; }
+
+static LL16Geom ll16Geometry(int nranks, size_t bytes, int dtype) {
+  LL16Geom g{};
+  g.bytes = bytes;
+  g.W = is2byte(dtype) ? (bytes + 2) / 4 : bytes / 4;  // (count*sizeof(T)+sizeof(T))/4 for 2-byte T
+  g.wpr = g.W / (uint64_t)nranks;
+  if (g.wpr % 2) g.wpr += 1;
+  // Deviation from allreduce_packet.cu:62-63: when W % n != 0 and W / n is even the reference's
+  // slices stop short of W and its last words are never reduced.  Widen the slice by one packet
+  // pair in exactly that case; every size the reference handles correctly keeps its geometry.
+  if (g.wpr * (uint64_t)nranks < g.W) g.wpr += 2;
+  g.ppr = g.wpr / 2;
+  g.roff = 2 * (g.W / 2) * 16;  // scratchResultOffset (:74)
+  // Deviation: when the slices were rounded up (odd W / n, or the tail fix above) the last
+  // source's input packets would overlap the first reduced slice and a fast rank's broadcast could
+  // overwrite packets not yet consumed.  Start the result region after the input region then.
+  if ((uint64_t)nranks * g.ppr * 16 > g.roff) g.roff = (uint64_t)nranks * g.ppr * 16;
+  g.units = (uint32_t)((g.ppr + 1) / 2);
+  return g;
+}
+
+static LL8Geom ll8Geometry(size_t bytes, int dtype) {
+  LL8Geom g{};
+  g.bytes = bytes;
+  g.W = is2byte(dtype) ? (bytes + 2) / 4 : bytes / 4;
+  g.units = (uint32_t)((g.W + 3) / 4);
+  return g;
+}
+
+size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype) {
+  LL16Geom g = ll16Geometry(nranks, bytes, dtype);
+  if (g.W == 0) return 0;
+  uint64_t half = g.roff + (uint64_t)nranks * g.ppr * 16;
+  const uint64_t inRegion = (uint64_t)nranks * g.ppr * 16;
+  if (inRegion > half) half = inRegion;
+  half = (half + 255) & ~255ull;
+  return 2 * half;
+}
+
+size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype) {
+  LL8Geom g = ll8Geometry(bytes, dtype);
+  uint64_t half = ((uint64_t)nranks * g.W * 8 + 255) & ~255ull;
+  return 2 * half;
+}
+
+template <int DT, int OP, int NV>
+static void launchLL16T(const Views<NV>& vw, const LL16Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
+                        hipStream_t s) {
+  hipLaunchKernelGGL((allreduceLL16Kernel<DT, OP, NV>), dim3(nblocks, NV), dim3(nthreads), 0, s, vw, g, nranks, budget);
+}
+template <int DT, int OP, int NV>
+static void launchLL8T(const Views<NV>& vw, const LL8Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
+                       hipStream_t s) {
+  hipLaunchKernelGGL((allreduceLL8Kernel<DT, OP, NV>), dim3(nblocks, NV), dim3(nthreads), 0, s, vw, g, nranks, budget);
+}
+
+template <int DT, int OP>
+static void launchLL16(const mscclppAmdRankView* views, int nviews, const LL16Geom& g, int nranks, int nblocks,
+                       int nthreads, uint64_t budget, hipStream_t s) {
+  if (nviews == 1) {
+    Views<1> vw;
+    vw.v[0] = views[0];
+    launchLL16T<DT, OP, 1>(vw, g, nranks, nblocks, nthreads, budget, s);
+  } else {
+    Views<kMaxRanks> vw{};
+    for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
+    launchLL16T<DT, OP, kMaxRanks>(vw, g, nranks, nblocks, nthreads, budget, s);
+  }
+}
+template <int DT, int OP>
+static void launchLL8(const mscclppAmdRankView* views, int nviews, const LL8Geom& g, int nranks, int nblocks,
+                      int nthreads, uint64_t budget, hipStream_t s) {
+  if (nviews == 1) {
+    Views<1> vw;
+    vw.v[0] = views[0];
+    launchLL8T<DT, OP, 1>(vw, g, nranks, nblocks, nthreads, budget, s);
+  } else {
+    Views<kMaxRanks> vw{};
+    for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
+    launchLL8T<DT, OP, kMaxRanks>(vw, g, nranks, nblocks, nthreads, budget, s);
+  }
+}
+
+// Default grids.  LL16: a multiple of the peer count (allreduce_packet.cu:164, :180-212 restated
+// for 64-wide waves: the slice is split into 16-byte units, one per lane).
+static void ll16Defaults(int nranks, size_t bytes, int& nblocks, int& nthreads) {
+  const int nPeers = nranks - 1;
+  const LL16Geom g = ll16Geometry(nranks, bytes, kF16);
+  if (nthreads <= 0) nthreads = g.units >= 4096 ? 512 : (g.units >= 1024 ? 256 : 128);
+  if (nblocks <= 0) {
+    uint64_t want = (g.units + nthreads - 1) / nthreads;  // blocks to cover the slice once
+    if (want < (uint64_t)nPeers) want = nPeers;
+    if (want > 16ull * nPeers) want = 16ull * nPeers;
+    nblocks = (int)want;
+  }
+  nblocks = nblocks / nPeers * nPeers;
+  if (nblocks < nPeers) nblocks = nPeers;
+}
+
+static void ll8Defaults(int nranks, size_t bytes, int& nblocks, int& nthreads) {
+  const LL8Geom g = ll8Geometry(bytes, kF16);
+  if (nthreads <= 0) nthreads = 256;
+  if (nblocks <= 0) {
+    uint64_t want = (g.units + nthreads - 1) / nthreads;
+    if (want < 1) want = 1;
+    if (want > 64) want = 64;
+    nblocks = (int)want;
+  }
+  (void)nranks;
+}
+
+int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
+                      int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s) {
+  if (algo == MSCCLPP_AMD_ALGO_PACKET) {
+    ll16Defaults(nranks, bytes, nblocks, nthreads);
+    if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
+    const LL16Geom g = ll16Geometry(nranks, bytes, dtype);
+    if (g.W == 0) return 4;
+    for (int i = 0; i < nviews; ++i)
+      if (views[i].scratchBytes < ll16ScratchRequired(nranks, bytes, dtype)) return 5;
+    MSCCLPP_AMD_DISPATCH(dtype, op, launchLL16, views, nviews, g, nranks, nblocks, nthreads, budget, s);
+  } else {
+    ll8Defaults(nranks, bytes, nblocks, nthreads);
+    if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
+    const LL8Geom g = ll8Geometry(bytes, dtype);
+    if (g.W == 0) return 4;
+    for (int i = 0; i < nviews; ++i)
+      if (views[i].scratchBytes < ll8ScratchRequired(nranks, bytes, dtype)) return 5;
+    MSCCLPP_AMD_DISPATCH(dtype, op, launchLL8, views, nviews, g, nranks, nblocks, nthreads, budget, s);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+}  // namespace mscclpp_amd

@@ -1,0 +1,76 @@
+// Shared pieces of the mscclpp_amd kernels (not part of the public device API).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mscclpp_amd/device.hpp"
+#include "mscclpp_amd/mscclpp_amd.h"
+#include "mscclpp_amd/packet_device.hpp"
+#include "mscclpp_amd/reduce_device.hpp"
+
+namespace mscclpp_amd {
+
+// Flag slots shared by every packet kernel of a communicator (the reference keeps 128, initialised
+// to 1: src/core/algorithm.cc:251-268).  A launch of G blocks uses slots [0, G); block 0 keeps the
+// unused slots [G, kFlagSlots) equal so that a later launch with a larger grid reads the same flag
+// in every block (allreduce_packet.cu:134-140).
+constexpr int kFlagSlots = MSCCLPP_AMD_FLAG_SLOTS;
+constexpr int kMaxRanks = MSCCLPP_AMD_MAX_RANKS;
+constexpr int kMaxChannels = MSCCLPP_AMD_MAX_CHANNELS;
+
+__device__ __forceinline__ void bump_flags(uint32_t* flags, uint32_t flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) flags[blockIdx.x] = flag + 1;
+  if (blockIdx.x == 0) {
+    for (uint32_t i = gridDim.x + threadIdx.x; i < (uint32_t)kFlagSlots; i += blockDim.x) flags[i] = flag + 1;
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Kernel argument carrying NV rank views (NV = 1: one rank per process; NV = n: in-process ranks).
+template <int NV>
+struct Views {
+  mscclppAmdRankView v[NV];
+};
+
+// Payload tail helpers: a 16-byte unit of which only `valid` (< 16) bytes lie inside the buffer.
+__device__ __forceinline__ u32x4 load_tail(const uint8_t* p, uint32_t valid) {
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if ((uint32_t)i < valid) w[i / 4] |= (uint32_t)p[i] << ((i % 4) * 8);
+  return u32x4{w[0], w[1], w[2], w[3]};
+}
+__device__ __forceinline__ void store_tail(uint8_t* p, u32x4 v, uint32_t valid) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if ((uint32_t)i < valid) p[i] = (uint8_t)(w[i / 4] >> ((i % 4) * 8));
+}
+
+// Load the 16-byte payload unit at byte `off` of buffer `base` (rsrc `r` over the same base) whose
+// first `valid` bytes are in range.
+template <int Policy>
+__device__ __forceinline__ u32x4 load_payload(__amdgpu_buffer_rsrc_t r, const uint8_t* base, uint64_t off,
+                                              uint32_t valid) {
+  if (valid >= 16) return load16<Policy>(r, (uint32_t)off);
+  return load_tail(base + off, valid);
+}
+template <int Policy>
+__device__ __forceinline__ void store_payload(__amdgpu_buffer_rsrc_t r, uint8_t* base, uint64_t off, u32x4 v,
+                                              uint32_t valid) {
+  if (valid >= 16)
+    store16<Policy>(r, (uint32_t)off, v);
+  else
+    store_tail(base + off, v, valid);
+}
+
+__device__ __forceinline__ uint32_t clamp_valid(uint64_t total, uint64_t off, uint32_t cap) {
+  if (off >= total) return 0;
+  uint64_t rem = total - off;
+  return rem < cap ? (uint32_t)rem : cap;
+}
+
+}  // namespace mscclpp_amd

@@ -1,0 +1,141 @@
+"""ctypes wrapper around oracle/liboracle.so (the CPU restatement; test infrastructure only)."""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+
+F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
+SUM, MIN = 0, 1
+
+_L = None
+
+
+def L():
+    global _L
+    if _L is None:
+        if not os.path.exists(ORACLE_SO):
+            from mscclpp_amd import _build
+
+            _build.build_oracle()
+        _L = ctypes.CDLL(ORACLE_SO)
+        u16, u32, u64, sz, vp, i32 = (ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t,
+                                      ctypes.c_void_p, ctypes.c_int)
+        for n, a, r in [
+            ("oracle_f16_add", [u16, u16], u16), ("oracle_bf16_add", [u16, u16], u16),
+            ("oracle_f16_min", [u16, u16], u16), ("oracle_bf16_min", [u16, u16], u16),
+            ("oracle_f32_add", [u32, u32], u32), ("oracle_f32_min", [u32, u32], u32),
+            ("oracle_reduce_words", [i32, i32, vp, vp, sz], None),
+            ("oracle_ll16_pack", [vp, sz, u32, vp], None), ("oracle_ll16_unpack", [vp, sz, u32, vp], sz),
+            ("oracle_ll8_pack", [vp, sz, u32, vp], None), ("oracle_ll8_unpack", [vp, sz, u32, vp], sz),
+            ("oracle_self_reduce", [i32, i32, vp, vp, sz, u32, vp, vp], sz),
+            ("oracle_ll16_geometry", [i32, u64, i32, vp], None),
+            ("oracle_allreduce_packet", [i32, i32, i32, vp, u64, u32, u64, vp, vp], None),
+            ("oracle_allreduce_allpairs", [i32, i32, i32, vp, u64, u32, u64, vp, vp], None),
+            ("oracle_allreduce_sliced", [i32, i32, i32, vp, u64, u64, i32, vp], None),
+            ("oracle_trigger_encode", [u64, u32, u64, u32, u64, u64, u32, vp], None),
+            ("oracle_fifo_commit_bit", [u64, u32], u64),
+            ("oracle_lcg_fill", [i32, u64, i32, i32, vp], None),
+        ]:
+            f = getattr(_L, n)
+            f.argtypes = a
+            f.restype = r
+    return _L
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _ptr_array(arrs):
+    t = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    return t
+
+
+def reduce_words(dtype, op, acc, val):
+    acc = np.ascontiguousarray(acc, dtype=np.uint32).copy()
+    val = np.ascontiguousarray(val, dtype=np.uint32)
+    L().oracle_reduce_words(dtype, op, _p(acc), _p(val), acc.size)
+    return acc
+
+
+def ll16_pack(words, flag):
+    words = np.ascontiguousarray(words, dtype=np.uint32)
+    out = np.zeros(words.size * 2, np.uint32)
+    L().oracle_ll16_pack(_p(words), words.size // 2, flag, _p(out))
+    return out
+
+
+def ll8_pack(words, flag):
+    words = np.ascontiguousarray(words, dtype=np.uint32)
+    out = np.zeros(words.size * 2, np.uint32)
+    L().oracle_ll8_pack(_p(words), words.size, flag, _p(out))
+    return out
+
+
+def self_reduce(dtype, op, x, y, flag):
+    x = np.ascontiguousarray(x).view(np.uint32)
+    y = np.ascontiguousarray(y).view(np.uint32)
+    pk = np.zeros(x.size * 2, np.uint32)
+    out = np.zeros(x.size, np.uint32)
+    bad = L().oracle_self_reduce(dtype, op, _p(x), _p(y), x.size, flag, _p(pk), _p(out))
+    assert bad == 0
+    return pk, out
+
+
+def geometry(dtype, count, n):
+    g = np.zeros(6, np.uint64)
+    L().oracle_ll16_geometry(dtype, count, n, _p(g))
+    return [int(v) for v in g]
+
+
+def allreduce_packet(dtype, op, inputs, count, flag, half_bytes):
+    n = len(inputs)
+    W, npk, wpr, ppr, _, roff = geometry(dtype, count, n)
+    nw = max(W, n * wpr)
+    ins = [np.zeros(nw + 4, np.uint32) for _ in range(n)]
+    for r in range(n):
+        src = np.ascontiguousarray(inputs[r]).view(np.uint8)
+        ins[r].view(np.uint8)[: src.size] = src
+    scr = [np.zeros(2 * half_bytes // 4, np.uint32) for _ in range(n)]
+    outs = [np.zeros(nw + 4, np.uint32) for _ in range(n)]
+    L().oracle_allreduce_packet(dtype, op, n, _ptr_array(ins), count, flag, half_bytes, _ptr_array(scr),
+                                _ptr_array(outs))
+    return outs, scr
+
+
+def allreduce_allpairs(dtype, op, inputs, count, flag, half_bytes):
+    n = len(inputs)
+    W = (count * 2 + 2) // 4 if dtype in (F16, BF16) else count
+    ins = [np.zeros(W + 4, np.uint32) for _ in range(n)]
+    for r in range(n):
+        src = np.ascontiguousarray(inputs[r]).view(np.uint8)
+        ins[r].view(np.uint8)[: src.size] = src
+    scr = [np.zeros(2 * half_bytes // 4, np.uint32) for _ in range(n)]
+    outs = [np.zeros(W + 4, np.uint32) for _ in range(n)]
+    L().oracle_allreduce_allpairs(dtype, op, n, _ptr_array(ins), count, flag, half_bytes, _ptr_array(scr),
+                                  _ptr_array(outs))
+    return outs, scr
+
+
+def allreduce_sliced(dtype, op, inputs, nwords, slice_words, order_kind):
+    n = len(inputs)
+    ins = [np.ascontiguousarray(a).view(np.uint32) for a in inputs]
+    outs = [np.zeros(nwords, np.uint32) for _ in range(n)]
+    L().oracle_allreduce_sliced(dtype, op, n, _ptr_array(ins), nwords, slice_words, order_kind, _ptr_array(outs))
+    return outs
+
+
+def trigger_encode(typ, dst_id, dst_off, src_id, src_off, nbytes, sem):
+    out = np.zeros(2, np.uint64)
+    L().oracle_trigger_encode(typ, dst_id, dst_off, src_id, src_off, nbytes, sem, _p(out))
+    return int(out[0]), int(out[1])
+
+
+def lcg(dtype, count, rank, seq):
+    itemsize = 2 if dtype in (F16, BF16) else 4
+    out = np.zeros(count * itemsize, np.uint8)
+    L().oracle_lcg_fill(dtype, count, rank, seq, _p(out))
+    return out.view(np.uint16 if itemsize == 2 else np.uint32)

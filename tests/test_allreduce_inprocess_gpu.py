@@ -1,0 +1,158 @@
+"""GPU parity of the multi-rank AllReduce kernels, with n ranks of one collective running in one
+process on one GPU (one launch, blockIdx.y = rank; every rank has its own scratch, flags,
+semaphores).  Outputs and, for the LL paths, the whole scratch image (packet flag + data words)
+are compared bit-exactly with the CPU oracle; the bulk paths against the oracle's sliced sums in
+the reference's sum orders (fullmesh: own then ascending; rsag: ring order)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+TORCH = {O.F16: torch.float16, O.BF16: torch.bfloat16, O.F32: torch.float32, O.I32: torch.int32}
+ITEM = {O.F16: 2, O.BF16: 2, O.F32: 4, O.I32: 4}
+
+
+def _dev(arr, dt):
+    t = torch.from_numpy(arr.view(np.int16 if arr.dtype == np.uint16 else np.int32).copy())
+    return t.view(TORCH[dt]).cuda()
+
+
+def _bytes(t):
+    return t.cpu().contiguous().view(torch.uint8).numpy()
+
+
+def _inputs(dt, n, count, seq=0, special=False):
+    ins = [O.lcg(dt, count, r, seq) for r in range(n)]
+    if special:
+        rng = np.random.default_rng(11 + seq)
+        bits = 16 if ITEM[dt] == 2 else 32
+        for r in range(n):
+            m = rng.random(count) < 0.25
+            ins[r] = ins[r].copy()
+            ins[r][m] = rng.integers(0, 2**bits, m.sum(), dtype=np.uint64).astype(ins[r].dtype)
+    return ins
+
+
+def _cmp(got_bytes, exp_bytes, dt):
+    if dt == O.F32:
+        g = got_bytes.view(np.uint32)
+        e = exp_bytes.view(np.uint32)
+        nan = (e & 0x7FFFFFFF) > 0x7F800000
+        assert np.array_equal(g[~nan], e[~nan])
+        assert np.all((g[nan] & 0x7FFFFFFF) > 0x7F800000)
+    else:
+        bad = np.nonzero(got_bytes != exp_bytes)[0]
+        assert bad.size == 0, f"{bad.size} byte mismatches, first {bad[:8]}"
+
+
+LL_CASES = [
+    # (n, dt, count, special)
+    (2, O.F16, 4096, False), (4, O.F16, 8192, True), (8, O.F16, 16384, True), (8, O.BF16, 16384, True),
+    (8, O.F32, 8192, False), (8, O.I32, 8192, False), (3, O.F16, 3000, False), (8, O.F16, 1000, False),
+    (8, O.F16, 777, False), (5, O.F32, 1001, False), (8, O.F16, 262144, False),
+]
+
+
+@pytest.mark.parametrize("algo", ["packet", "allpair"])
+@pytest.mark.parametrize("n,dt,count,special", LL_CASES)
+def test_ll_allreduce_bit_exact(built, algo, n, dt, count, special):
+    import mscclpp_amd as m
+
+    algo_code = m.ALGO_PACKET if algo == "packet" else m.ALGO_ALLPAIR
+    nbytes = count * ITEM[dt]
+    if algo == "allpair" and nbytes > (256 << 10):
+        pytest.skip("one-hop LL8 is the <=16 KiB path; keep its scratch small")
+    sb = max(m.scratch_required(algo_code, n, nbytes, dt), 1 << 16)
+    ranks = m.InProcessRanks(n, sb)
+    nblocks = (n - 1) * 2 if algo == "packet" else 4
+    for call, flag in enumerate((1, 2, 3)):
+        ins = _inputs(dt, n, count, seq=call, special=special)
+        dins = [_dev(a, dt) for a in ins]
+        douts = [torch.full_like(d, 0) for d in dins]
+        ranks.all_reduce(dins, douts, algo_code, nblocks=nblocks, nthreads=256)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        if algo == "packet":
+            exp, scr = O.allreduce_packet(dt, O.SUM, ins, count, flag, sb // 2)
+        else:
+            exp, scr = O.allreduce_allpairs(dt, O.SUM, ins, count, flag, sb // 2)
+        for r in range(n):
+            _cmp(_bytes(douts[r]), exp[r].view(np.uint8)[:nbytes], dt)
+        if call == 0:
+            # packet image of the flag-1 half: flag words and data words, bit-exact
+            for r in range(n):
+                got = ranks.scratch_tensor(r, sb).cpu().numpy().view(np.uint32)
+                assert np.array_equal(got, scr[r]), f"scratch image of rank {r}"
+
+
+@pytest.mark.parametrize("algo,order", [("fullmesh", 0), ("rsag", 1)])
+@pytest.mark.parametrize("n,dt,count", [(2, O.F16, 1 << 16), (8, O.F16, 1 << 18), (8, O.F32, 100000),
+                                        (4, O.BF16, 65536 + 8), (8, O.I32, 4096), (7, O.F32, 12345)])
+def test_bulk_allreduce_bit_exact(built, algo, order, n, dt, count):
+    import mscclpp_amd as m
+
+    algo_code = m.ALGO_FULLMESH if algo == "fullmesh" else m.ALGO_RSAG
+    nbytes = count * ITEM[dt]
+    slice_bytes = ((nbytes + n - 1) // n + 15) // 16 * 16
+    ranks = m.InProcessRanks(n, 1 << 16, bulk_scratch_bytes=max(n * slice_bytes, 1 << 20))
+    for call in range(3):
+        ins = _inputs(dt, n, count, seq=call, special=(call == 1 and dt != O.F32))
+        dins = [_dev(a, dt) for a in ins]
+        douts = [torch.full_like(d, 0) for d in dins]
+        ranks.all_reduce(dins, douts, algo_code, nblocks=8, nthreads=256)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        nwords = (nbytes + 3) // 4
+        padded = []
+        for a in ins:
+            w = np.zeros(nwords, np.uint32)
+            w.view(np.uint8)[:nbytes] = a.view(np.uint8)
+            padded.append(w)
+        exp = O.allreduce_sliced(dt, O.SUM, padded, nwords, slice_bytes // 4, order)
+        for r in range(n):
+            _cmp(_bytes(douts[r]), exp[r].view(np.uint8)[:nbytes], dt)
+
+
+@pytest.mark.parametrize("algo", ["packet", "allpair", "fullmesh"])
+def test_in_place(built, algo):
+    import mscclpp_amd as m
+
+    n, dt, count = 8, O.F16, 8192
+    code = {"packet": m.ALGO_PACKET, "allpair": m.ALGO_ALLPAIR, "fullmesh": m.ALGO_FULLMESH}[algo]
+    nbytes = count * 2
+    ranks = m.InProcessRanks(n, max(m.scratch_required(code, n, nbytes, dt), 1 << 16), bulk_scratch_bytes=1 << 20)
+    ins = _inputs(dt, n, count)
+    bufs = [_dev(a, dt) for a in ins]
+    ranks.all_reduce(bufs, bufs, code, nblocks=(n - 1) * 2 if code == m.ALGO_PACKET else 8, nthreads=256)
+    torch.cuda.synchronize()
+    assert ranks.errors() == [0] * n
+    if code == m.ALGO_FULLMESH:
+        sl = ((nbytes + n - 1) // n + 15) // 16 * 16
+        exp = O.allreduce_sliced(dt, O.SUM, [a.view(np.uint32) for a in ins], nbytes // 4, sl // 4, 0)
+    elif code == m.ALGO_PACKET:
+        exp, _ = O.allreduce_packet(dt, O.SUM, ins, count, 1, 1 << 20)
+    else:
+        exp, _ = O.allreduce_allpairs(dt, O.SUM, ins, count, 1, 1 << 20)
+    for r in range(n):
+        _cmp(_bytes(bufs[r]), exp[r].view(np.uint8)[:nbytes], dt)
+
+
+def test_int32_kat(built):
+    """mscclpp-test KAT (allreduce_test.cu:1172-1183): input = rank -> n(n-1)/2 everywhere."""
+    import mscclpp_amd as m
+
+    n = 8
+    for code, nb in ((m.ALGO_ALLPAIR, 4), (m.ALGO_PACKET, 14), (m.ALGO_FULLMESH, 8), (m.ALGO_RSAG, 8)):
+        count = 1 << 14
+        ranks = m.InProcessRanks(n, max(m.scratch_required(code, n, count * 4, O.I32), 1 << 16),
+                                 bulk_scratch_bytes=1 << 20)
+        ins = [torch.full((count,), r, dtype=torch.int32, device="cuda") for r in range(n)]
+        outs = [torch.empty_like(t) for t in ins]
+        ranks.all_reduce(ins, outs, code, nblocks=nb, nthreads=256)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        for o in outs:
+            assert torch.all(o == n * (n - 1) // 2)

@@ -1,0 +1,85 @@
+"""GPU parity: the 1-GPU LL16 pack -> sum -> unpack kernel against the CPU oracle, bit-exact,
+including the packet image (flag words and data words) left in the packet buffer."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+TORCH = {O.F16: torch.float16, O.BF16: torch.bfloat16, O.F32: torch.float32, O.I32: torch.int32}
+
+
+def _inputs(dt, nbytes, special):
+    itemsize = 2 if dt in (O.F16, O.BF16) else 4
+    count = nbytes // itemsize
+    x = O.lcg(dt, count, 0, 0)
+    y = O.lcg(dt, count, 1, 0)
+    if special:
+        rng = np.random.default_rng(7)
+        bits = 16 if itemsize == 2 else 32
+        m = rng.random(count) < 0.5
+        x = x.copy()
+        y = y.copy()
+        x[m] = rng.integers(0, 2**bits, m.sum(), dtype=np.uint64).astype(x.dtype)
+        y[m] = rng.integers(0, 2**bits, m.sum(), dtype=np.uint64).astype(y.dtype)
+    return x, y
+
+
+def _to_dev(arr, dt):
+    t = torch.from_numpy(arr.view(np.int16 if arr.dtype == np.uint16 else np.int32).copy())
+    return t.view(TORCH[dt]).cuda()
+
+
+def _bits(t):
+    return t.cpu().view(torch.int16 if t.element_size() == 2 else torch.int32).numpy().view(
+        np.uint16 if t.element_size() == 2 else np.uint32)
+
+
+def _assert_equal_words(got, exp, dt):
+    got = got.view(np.uint32)
+    exp = exp.view(np.uint32)
+    if dt == O.F32:
+        nan = (exp & 0x7FFFFFFF) > 0x7F800000
+        assert np.array_equal(got[~nan], exp[~nan])
+        assert np.all((got[nan] & 0x7FFFFFFF) > 0x7F800000)
+    else:
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, f"{bad.size} mismatches, first at {bad[:4]}: {got[bad[:4]]} vs {exp[bad[:4]]}"
+
+
+@pytest.mark.parametrize("dt,op", [(O.F16, O.SUM), (O.BF16, O.SUM), (O.F32, O.SUM), (O.I32, O.SUM),
+                                   (O.F16, O.MIN), (O.BF16, O.MIN), (O.F32, O.MIN)])
+@pytest.mark.parametrize("nbytes,special", [(64 << 10, True), ((1 << 20) + 48, False), (4 << 20, True)])
+def test_self_reduce_bit_exact(built, dt, op, nbytes, special):
+    import mscclpp_amd as m
+
+    x, y = _inputs(dt, nbytes, special)
+    xd, yd = _to_dev(x, dt), _to_dev(y, dt)
+    out = torch.empty_like(xd)
+    pk = m.DeviceBuffer(2 * nbytes)
+    flags = torch.ones(m.FLAG_SLOTS, dtype=torch.int32, device="cuda")
+    err = torch.zeros(16, dtype=torch.int32, device="cuda")
+    for flag in (1, 2, 3):
+        out.zero_()
+        m.self_reduce_ll16(xd, yd, pk.ptr, out, flags, err, op=op)
+        torch.cuda.synchronize()
+        assert int(err[0].item()) == 0
+        exp_pk, exp_out = O.self_reduce(dt, op, x, y, flag)
+        _assert_equal_words(_bits(out), exp_out, dt)
+        got_pk = m.device_view(pk.ptr, 2 * nbytes).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got_pk, exp_pk)  # LL16 flag and data words, bit-exact
+        assert int(flags[0].item()) == flag + 1 and int(flags[-1].item()) == flag + 1
+    pk.free()
+
+
+def test_self_reduce_rejects_unaligned(built):
+    import mscclpp_amd as m
+
+    x = torch.zeros(9, dtype=torch.float16, device="cuda")
+    flags = torch.ones(m.FLAG_SLOTS, dtype=torch.int32, device="cuda")
+    err = torch.zeros(16, dtype=torch.int32, device="cuda")
+    with pytest.raises(m.MscclppError) as e:
+        m.self_reduce_ll16(x, x, x.data_ptr(), x, flags, err)
+    assert e.value.code == 4
