@@ -152,7 +152,7 @@ def self_reduce_ll16(x, y, pkts_ptr, out, flags, err, op=SUM, nblocks=0, budget_
     code = lib().mscclppAmdSelfReduceLL16(
         ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(pkts_ptr),
         ctypes.c_void_p(out.data_ptr()), nbytes, DTYPE_CODES[x.dtype], op, ctypes.c_void_p(flags.data_ptr()),
-        nblocks, budget_ticks or 2_000_000_000, ctypes.c_void_p(err.data_ptr()), stream_ptr(stream))
+        nblocks, budget_ticks or 200_000_000, ctypes.c_void_p(err.data_ptr()), stream_ptr(stream))
     check(code, "self_reduce_ll16")
 
 

@@ -377,6 +377,21 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
     if (dtype < 0 || dtype > MSCCLPP_AMD_U32 || op < 0 || op > MSCCLPP_AMD_MIN) return (int)ncclInvalidArgument;
     if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = mscclppAmdSelectAlgo(nranks, bytes, dtype);
     if (budgetTicks == 0) budgetTicks = spinBudgetTicks();
+    // validate every pointer the kernel will dereference before launching (a fault here would
+    // take the GPU down; a bad argument must come back as ncclInvalidArgument instead)
+    const bool bulk = algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG;
+    unsigned seen = 0;
+    for (int i = 0; i < nviews; ++i) {
+      const mscclppAmdRankView& v = views[i];
+      if (v.rank < 0 || v.rank >= nranks || (seen >> v.rank) & 1u) return (int)ncclInvalidArgument;
+      seen |= 1u << v.rank;
+      if (!v.input || !v.output || !v.scratch || !v.flags || !v.err || v.scratchBytes == 0) return (int)ncclInvalidArgument;
+      for (int q = 0; q < nranks; ++q) {
+        if (!v.peerScratch[q]) return (int)ncclInvalidArgument;
+        if (bulk && (!v.peerOutput[q] || !v.peerTokens[q])) return (int)ncclInvalidArgument;
+      }
+      if (bulk && (!v.tokens || !v.expected)) return (int)ncclInvalidArgument;
+    }
     if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR)
       return launchAllReduceLL(algo, views, nviews, nranks, bytes, dtype, op, nblocks, nthreads, budgetTicks,
                                (hipStream_t)stream);

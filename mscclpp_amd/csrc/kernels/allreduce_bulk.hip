@@ -167,9 +167,9 @@ size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom
 }
 
 template <int DT, int OP, int NV, int ORDER>
-static void launchBulkT(const Views<NV>& vw, const BulkGeom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
+static void launchBulkT(const Views<NV>& vw, int nviews, const BulkGeom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
                         hipStream_t s) {
-  hipLaunchKernelGGL((allreduceBulkKernel<DT, OP, NV, ORDER>), dim3(nblocks, NV), dim3(nthreads), 0, s, vw, g, nranks,
+  hipLaunchKernelGGL((allreduceBulkKernel<DT, OP, NV, ORDER>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks,
                      budget);
 }
 
@@ -180,16 +180,16 @@ static void launchBulk(const mscclppAmdRankView* views, int nviews, const BulkGe
     Views<1> vw;
     vw.v[0] = views[0];
     if (order == 0)
-      launchBulkT<DT, OP, 1, 0>(vw, g, nranks, nblocks, nthreads, budget, s);
+      launchBulkT<DT, OP, 1, 0>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
     else
-      launchBulkT<DT, OP, 1, 1>(vw, g, nranks, nblocks, nthreads, budget, s);
+      launchBulkT<DT, OP, 1, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   } else {
     Views<kMaxRanks> vw{};
     for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
     if (order == 0)
-      launchBulkT<DT, OP, kMaxRanks, 0>(vw, g, nranks, nblocks, nthreads, budget, s);
+      launchBulkT<DT, OP, kMaxRanks, 0>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
     else
-      launchBulkT<DT, OP, kMaxRanks, 1>(vw, g, nranks, nblocks, nthreads, budget, s);
+      launchBulkT<DT, OP, kMaxRanks, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   }
 }
 

@@ -296,14 +296,14 @@ size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype) {
 }
 
 template <int DT, int OP, int NV>
-static void launchLL16T(const Views<NV>& vw, const LL16Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
+static void launchLL16T(const Views<NV>& vw, int nviews, const LL16Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
                         hipStream_t s) {
-  hipLaunchKernelGGL((allreduceLL16Kernel<DT, OP, NV>), dim3(nblocks, NV), dim3(nthreads), 0, s, vw, g, nranks, budget);
+  hipLaunchKernelGGL((allreduceLL16Kernel<DT, OP, NV>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
 }
 template <int DT, int OP, int NV>
-static void launchLL8T(const Views<NV>& vw, const LL8Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
+static void launchLL8T(const Views<NV>& vw, int nviews, const LL8Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
                        hipStream_t s) {
-  hipLaunchKernelGGL((allreduceLL8Kernel<DT, OP, NV>), dim3(nblocks, NV), dim3(nthreads), 0, s, vw, g, nranks, budget);
+  hipLaunchKernelGGL((allreduceLL8Kernel<DT, OP, NV>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
 }
 
 template <int DT, int OP>
@@ -312,11 +312,11 @@ static void launchLL16(const mscclppAmdRankView* views, int nviews, const LL16Ge
   if (nviews == 1) {
     Views<1> vw;
     vw.v[0] = views[0];
-    launchLL16T<DT, OP, 1>(vw, g, nranks, nblocks, nthreads, budget, s);
+    launchLL16T<DT, OP, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   } else {
     Views<kMaxRanks> vw{};
     for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
-    launchLL16T<DT, OP, kMaxRanks>(vw, g, nranks, nblocks, nthreads, budget, s);
+    launchLL16T<DT, OP, kMaxRanks>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   }
 }
 template <int DT, int OP>
@@ -325,11 +325,11 @@ static void launchLL8(const mscclppAmdRankView* views, int nviews, const LL8Geom
   if (nviews == 1) {
     Views<1> vw;
     vw.v[0] = views[0];
-    launchLL8T<DT, OP, 1>(vw, g, nranks, nblocks, nthreads, budget, s);
+    launchLL8T<DT, OP, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   } else {
     Views<kMaxRanks> vw{};
     for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
-    launchLL8T<DT, OP, kMaxRanks>(vw, g, nranks, nblocks, nthreads, budget, s);
+    launchLL8T<DT, OP, kMaxRanks>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   }
 }
 

@@ -1,0 +1,101 @@
+// oracle/_ref harness -- TEST INFRASTRUCTURE ONLY.
+//
+// Runs the reference's OWN device code on the GPU, compiled where it lies under /root/reference
+// (nothing is copied): LL16Packet::write/read and LL8Packet (include/mscclpp/packet_device.hpp),
+// copyToPackets / copyFromPackets (include/mscclpp/copy_device.hpp:156-232) and the f16x2 /
+// bf16x2 / f32x2 operator+ and min with clip (include/mscclpp/gpu_data_types.hpp:315-420, 588-620).
+// reduce_kernel.hpp itself cannot be compiled here (it pulls in algorithm.hpp -> core.hpp ->
+// the build-generated mscclpp/version.hpp), so the harness calls the operators that its
+// calVectorHelper<T, Op> forwards to (reduce_kernel.hpp:28-134) directly.
+//
+// Built by oracle/build_ref.sh into oracle/_ref/libref.so; used only by tests/.
+#include <hip/hip_runtime.h>
+
+#include <mscclpp/copy_device.hpp>
+#include <mscclpp/gpu_data_types.hpp>
+#include <mscclpp/packet_device.hpp>
+
+using namespace mscclpp;
+
+// calVector<T, Op> on one 32-bit word (reduce_kernel.hpp:91-94, 112-134)
+template <int DT, int OP>
+__device__ uint32_t refWord(uint32_t a, uint32_t b) {
+  if constexpr (DT == 0) {  // __half -> f16x2
+    f16x2 x = bit_cast<f16x2, uint32_t>(a), y = bit_cast<f16x2, uint32_t>(b);
+    return bit_cast<uint32_t, f16x2>(OP == 0 ? x + y : mscclpp::min(x, y));
+  } else if constexpr (DT == 1) {  // __bfloat16 -> bf16x2
+    bf16x2 x = bit_cast<bf16x2, uint32_t>(a), y = bit_cast<bf16x2, uint32_t>(b);
+    return bit_cast<uint32_t, bf16x2>(OP == 0 ? x + y : mscclpp::min(x, y));
+  } else if constexpr (DT == 2) {  // float -> f32x2 scalar specialisation (reduce_kernel.hpp:97-109)
+    float x = bit_cast<float, uint32_t>(a), y = bit_cast<float, uint32_t>(b);
+    return bit_cast<uint32_t, float>(OP == 0 ? x + y : fminf(x, y));
+  } else {  // int
+    int x = (int)a, y = (int)b;
+    return (uint32_t)(OP == 0 ? x + y : (x < y ? x : y));
+  }
+}
+
+template <int DT, int OP>
+__global__ void refReduceKernel(uint32_t* acc, const uint32_t* val, size_t n) {
+  for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    acc[i] = refWord<DT, OP>(acc[i], val[i]);
+}
+
+__global__ void refPackLL16(void* pkts, const void* src, uint64_t bytes, uint32_t flag) {
+  copyToPackets<LL16Packet>(pkts, src, bytes, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x, flag);
+}
+__global__ void refPackLL8(void* pkts, const void* src, uint64_t bytes, uint32_t flag) {
+  copyToPackets<LL8Packet>(pkts, src, bytes, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x, flag);
+}
+
+// O = X (op) read(P, flag): the step-2 loop body of allreducePacket for one peer stream
+// (allreduce_packet.cu:93-108) with LL16Packet::read.
+template <int DT, int OP>
+__global__ void refUnpackReduceLL16(const void* pkts, const uint32_t* x, uint32_t* out, uint64_t npkts, uint32_t flag) {
+  const LL16Packet* p = reinterpret_cast<const LL16Packet*>(pkts);
+  for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < npkts; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint2 v = p[i].read(flag, 100000000);
+    out[2 * i] = refWord<DT, OP>(x[2 * i], v.x);
+    out[2 * i + 1] = refWord<DT, OP>(x[2 * i + 1], v.y);
+  }
+}
+
+#define REF_DISPATCH(dtype, op, KERNEL, ...)                                         \
+  do {                                                                               \
+    int key = (dtype) * 2 + (op);                                                    \
+    if (key == 0) hipLaunchKernelGGL((KERNEL<0, 0>), __VA_ARGS__);                   \
+    else if (key == 1) hipLaunchKernelGGL((KERNEL<0, 1>), __VA_ARGS__);              \
+    else if (key == 2) hipLaunchKernelGGL((KERNEL<1, 0>), __VA_ARGS__);              \
+    else if (key == 3) hipLaunchKernelGGL((KERNEL<1, 1>), __VA_ARGS__);              \
+    else if (key == 4) hipLaunchKernelGGL((KERNEL<2, 0>), __VA_ARGS__);              \
+    else if (key == 5) hipLaunchKernelGGL((KERNEL<2, 1>), __VA_ARGS__);              \
+    else if (key == 6) hipLaunchKernelGGL((KERNEL<3, 0>), __VA_ARGS__);              \
+    else if (key == 7) hipLaunchKernelGGL((KERNEL<3, 1>), __VA_ARGS__);              \
+    else return 4;                                                                   \
+  } while (0)
+
+extern "C" {
+
+int refReduceWords(int dtype, int op, uint32_t* acc, const uint32_t* val, size_t nwords, void* stream) {
+  REF_DISPATCH(dtype, op, refReduceKernel, dim3(256), dim3(256), 0, (hipStream_t)stream, acc, val, nwords);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int refPack(int ll8, void* pkts, const void* src, uint64_t bytes, uint32_t flag, void* stream) {
+  if (ll8)
+    hipLaunchKernelGGL(refPackLL8, dim3(256), dim3(256), 0, (hipStream_t)stream, pkts, src, bytes, flag);
+  else
+    hipLaunchKernelGGL(refPackLL16, dim3(256), dim3(256), 0, (hipStream_t)stream, pkts, src, bytes, flag);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// the 1-GPU self-reduce, reference code path: pack (kernel 1), then unpack + reduce (kernel 2)
+int refSelfReduceLL16(int dtype, int op, const void* x, const void* y, void* pkts, void* out, uint64_t bytes,
+                      uint32_t flag, void* stream) {
+  hipLaunchKernelGGL(refPackLL16, dim3(256), dim3(256), 0, (hipStream_t)stream, pkts, y, bytes, flag);
+  REF_DISPATCH(dtype, op, refUnpackReduceLL16, dim3(256), dim3(256), 0, (hipStream_t)stream, (const void*)pkts,
+               (const uint32_t*)x, (uint32_t*)out, bytes / 8, flag);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+}  // extern "C"
