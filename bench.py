@@ -154,6 +154,9 @@ def bench_multi(args):
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    ndev = torch.cuda.device_count()
+    if ndev < world:  # rehearsal on a smaller box: ranks share devices (never the case on the 8-GPU node)
+        local = local % ndev
     torch.cuda.set_device(local)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = m.Communicator.from_torch_dist()

@@ -74,6 +74,12 @@ int mscclppAmdFlagsInit(uint32_t* flags, void* stream);
 int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts, void* out, size_t bytes, int dtype, int op,
                              uint32_t* flags, int nblocks, uint64_t budgetTicks, uint32_t* err, void* stream);
 
+/* Tuning / ceiling helpers used by the benchmark (fp16 SUM): variant selects lanes-per-unit and
+ * the packet cache policies; mscclppAmdCopy is a plain streaming copy (HBM ceiling). */
+int mscclppAmdSelfReduceLL16Variant(const void* x, const void* y, void* pkts, void* out, size_t bytes, uint32_t* flags,
+                                    int nblocks, int variant, uint64_t budgetTicks, uint32_t* err, void* stream);
+int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblocks, void* stream);
+
 /* ---- explicit-view AllReduce ------------------------------------------------------------- */
 /* Launch `algo` for `nviews` ranks of an `nranks`-rank AllReduce in ONE kernel launch (views[i]
  * is handled by blockIdx.y == i).  nviews == 1 is the one-rank-per-process form; nviews ==

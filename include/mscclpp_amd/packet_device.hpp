@@ -108,9 +108,10 @@ __device__ __forceinline__ void ll16_put_unit(__amdgpu_buffer_rsrc_t pkts, uint3
 }
 
 // Poll one unit once.  Returns true and fills w when both packets carry `flag`.
+template <int LoadPolicy = kSystem>
 __device__ __forceinline__ bool ll16_try_unit(__amdgpu_buffer_rsrc_t pkts, uint32_t pbyte, uint32_t flag, u32x4& w) {
-  u32x4 a = load16<kSystem>(pkts, pbyte);
-  u32x4 b = load16<kSystem>(pkts, pbyte + 16);
+  u32x4 a = load16<LoadPolicy>(pkts, pbyte);
+  u32x4 b = load16<LoadPolicy>(pkts, pbyte + 16);
   w.x = a.x;
   w.y = a.z;
   w.z = b.x;
@@ -118,12 +119,13 @@ __device__ __forceinline__ bool ll16_try_unit(__amdgpu_buffer_rsrc_t pkts, uint3
   return LL16Packet::ready(a, flag) && LL16Packet::ready(b, flag);
 }
 
+template <int LoadPolicy = kSystem>
 __device__ __forceinline__ u32x4 ll16_get_unit(__amdgpu_buffer_rsrc_t pkts, uint32_t pbyte, uint32_t flag,
                                                uint64_t budget, uint32_t* err) {
   u32x4 w;
-  if (ll16_try_unit(pkts, pbyte, flag, w)) return w;
+  if (ll16_try_unit<LoadPolicy>(pkts, pbyte, flag, w)) return w;
   SpinGuard g(budget);
-  while (!ll16_try_unit(pkts, pbyte, flag, w)) {
+  while (!ll16_try_unit<LoadPolicy>(pkts, pbyte, flag, w)) {
     if (g.expired()) {
       report_error(err, kErrPacketTimeout);
       return u32x4{0, 0, 0, 0};

@@ -245,7 +245,7 @@ class Communicator:
     def unique_id():
         uid = UniqueId()
         check(lib().ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        return bytes(uid.internal) + b"\0" * (128 - len(bytes(uid.internal)))
+        return ctypes.string_at(ctypes.addressof(uid), 128)  # (c_char arrays stop at the first NUL)
 
     @classmethod
     def from_torch_dist(cls, group=None):

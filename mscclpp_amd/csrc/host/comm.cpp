@@ -190,6 +190,7 @@ struct ncclComm {
     size_t sz = 0;
     HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)ptr));
     HIPCHECK(hipIpcGetMemHandle(&mine.handle, base));
+    info("rank " + std::to_string(rank) + ": got ipc handle, all-gather");
     mine.base = (uint64_t)base;
     mine.offset = (uint64_t)((char*)ptr - (char*)base);
     mine.bytes = sz;
@@ -205,7 +206,9 @@ struct ncclComm {
       auto it = opened.find(key);
       void* mapped = nullptr;
       if (it == opened.end()) {
+        info("rank " + std::to_string(rank) + ": opening ipc handle of rank " + std::to_string(r));
         HIPCHECK(hipIpcOpenMemHandle(&mapped, all[r].handle, hipIpcMemLazyEnablePeerAccess));
+        info("rank " + std::to_string(rank) + ": opened");
         opened[key] = mapped;
       } else {
         mapped = it->second;
@@ -455,7 +458,9 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
     c->nranks = nranks;
     HIPCHECK(hipGetDevice(&c->device));
     const char* to = std::getenv("MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S");
+    info("rank " + std::to_string(rank) + ": bootstrap connect");
     c->boot = std::make_unique<Bootstrap>(rank, nranks, id, to ? std::atoi(to) : 600);
+    info("rank " + std::to_string(rank) + ": bootstrap connected");
     const size_t tokBytes = sizeof(uint64_t) * MSCCLPP_AMD_MAX_RANKS * MSCCLPP_AMD_MAX_CHANNELS;
     c->tokens = (uint64_t*)allocUncached(tokBytes);
     HIPCHECK(hipMalloc((void**)&c->expected, tokBytes));
@@ -468,7 +473,9 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
     HIPCHECK(hipMalloc((void**)&c->err, 256));
     HIPCHECK(hipMemset(c->err, 0, 256));
     if (nranks > 1) {
+      info("rank " + std::to_string(rank) + ": exchanging semaphore tokens");
       auto toks = c->exchange(c->tokens);
+      info("rank " + std::to_string(rank) + ": tokens mapped; allocating LL scratch");
       for (int r = 0; r < nranks; ++r) c->peerTokens[r] = (uint64_t*)toks[r];
       c->ensure(c->llScratch, c->llBytes, c->peerLL, (size_t)64 << 20);
     }

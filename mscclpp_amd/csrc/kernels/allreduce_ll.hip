@@ -26,42 +26,82 @@ struct LL16Geom {
   uint64_t wpr;     // words per rank slice, even (:62-63)
   uint64_t ppr;     // packets per rank slice
   uint64_t roff;    // byte offset of the reduced-slice region inside a scratch half (:74)
-  uint32_t units;   // 2-packet units per slice = ceil(ppr / 2)
+  uint32_t units;   // packets per slice (= ppr)
   uint32_t pad;
 };
 
 struct LL8Geom {
   uint64_t bytes;
   uint64_t W;       // words (= LL8 packets) per rank buffer (allreduce_allpair_packet.cu:20)
-  uint32_t units;   // ceil(W / 4)
+  uint32_t units;   // 2-word units = ceil(W / 2)
   uint32_t pad;
 };
 
-// ---- LL16 unit helpers (a unit is 2 packets, or 1 for the odd last packet of a slice) ----------
+// ---- packet-major units ------------------------------------------------------------------------
+// One lane owns one "unit": 8 payload bytes <-> 16 packet bytes, i.e. one LL16 packet
+// {P[2i], f, P[2i+1], f} or the two LL8 packets {P[2i], f}, {P[2i+1], f} -- the same 16-byte image.
+// Consecutive lanes own consecutive units, so every packet store / poll of a wave is one contiguous
+// 1 KiB access made of whole 64-byte lines (partial-line packet stores cost a full line each on
+// gfx950: WRITE_SIZE 5*S instead of 3*S in the self-reduce microbench), and the payload side is a
+// contiguous 512 B dwordx2 access.
 template <int Policy>
-__device__ __forceinline__ void ll16_put(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, u32x4 w, uint32_t flag, bool two) {
-  store16<Policy>(pk, pbyte, LL16Packet::make(w.x, w.y, flag));
-  if (two) store16<Policy>(pk, pbyte + 16, LL16Packet::make(w.z, w.w, flag));
+__device__ __forceinline__ void unit_put(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, u32x2 w, uint32_t flag,
+                                         bool single) {
+  if (!single)
+    store16<Policy>(pk, pbyte, u32x4{w.x, flag, w.y, flag});
+  else
+    store8<Policy>(pk, pbyte, u32x2{w.x, flag});  // lone trailing LL8 packet
 }
-__device__ __forceinline__ bool ll16_try(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, u32x4& w, bool two) {
-  u32x4 a = load16<kSystem>(pk, pbyte);
-  u32x4 c = two ? load16<kSystem>(pk, pbyte + 16) : u32x4{0, flag, 0, flag};
-  w = u32x4{a.x, a.z, c.x, c.z};
-  return LL16Packet::ready(a, flag) && LL16Packet::ready(c, flag);
+__device__ __forceinline__ bool unit_try(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, u32x2& w,
+                                         bool single) {
+  if (!single) {
+    u32x4 a = load16<kSystem>(pk, pbyte);
+    w = u32x2{a.x, a.z};
+    return a.y == flag && a.w == flag;
+  }
+  u32x2 a = load8<kSystem>(pk, pbyte);
+  w = u32x2{a.x, 0};
+  return a.y == flag;
 }
-__device__ __forceinline__ u32x4 ll16_get(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, bool two,
+__device__ __forceinline__ u32x2 unit_get(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, bool single,
                                           uint64_t budget, uint32_t* err) {
-  u32x4 w;
-  if (ll16_try(pk, pbyte, flag, w, two)) return w;
+  u32x2 w;
+  if (unit_try(pk, pbyte, flag, w, single)) return w;
   SpinGuard g(budget);
-  while (!ll16_try(pk, pbyte, flag, w, two)) {
+  while (!unit_try(pk, pbyte, flag, w, single)) {
     __builtin_amdgcn_s_sleep(1);
     if (g.expired()) {
       report_error(err, kErrPacketTimeout);
-      return u32x4{0, 0, 0, 0};
+      return u32x2{0, 0};
     }
   }
   return w;
+}
+// 8-byte payload at byte `off` of `base`, of which `valid` bytes are inside the buffer
+__device__ __forceinline__ u32x2 payload_ld(__amdgpu_buffer_rsrc_t r, const uint8_t* base, uint64_t off, uint32_t valid) {
+  if (valid >= 8) return load8<kPlain>(r, (uint32_t)off);
+  uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if ((uint32_t)i < valid) {
+      const uint32_t v = (uint32_t)base[off + i] << ((i % 4) * 8);
+      if (i < 4) w0 |= v; else w1 |= v;
+    }
+  }
+  return u32x2{w0, w1};
+}
+__device__ __forceinline__ void payload_st(__amdgpu_buffer_rsrc_t r, uint8_t* base, uint64_t off, u32x2 v, uint32_t valid) {
+  if (valid >= 8) {
+    store8<kPlain>(r, (uint32_t)off, v);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if ((uint32_t)i < valid) base[off + i] = (uint8_t)((i < 4 ? v.x : v.y) >> ((i % 4) * 8));
+}
+template <int DT, int OP>
+__device__ __forceinline__ u32x2 reduce2(u32x2 a, u32x2 b) {
+  return u32x2{reduce_word<DT, OP>(a.x, b.x), reduce_word<DT, OP>(a.y, b.y)};
 }
 
 template <int DT, int OP, int NV>
@@ -78,120 +118,69 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
   const auto rin = make_rsrc(in);
   const auto rout = make_rsrc(out);
   const uint64_t sliceBytes = g.wpr * 4;
-  const uint32_t bpp = G / (uint32_t)nPeers;  // blocks per peer for steps 1 and 3
+  const uint32_t npk = (uint32_t)g.ppr;          // packets (units) per slice
+  const uint32_t bpp = G / (uint32_t)nPeers;     // blocks per peer for steps 1 and 3
   const bool inPeerGroup = b < bpp * (uint32_t)nPeers;
   const int peerIdx = inPeerGroup ? (int)(b / bpp) : 0;
   const int remote = peerIdx < rank ? peerIdx : peerIdx + 1;
   const uint32_t lb = inPeerGroup ? b % bpp : 0;
 
-  // step 1: put my copy of slice `remote` into rank `remote`'s scratch at rank*ppr packets
+  // step 1: put my copy of slice `remote` into rank `remote`'s scratch at rank*ppr packets (:89-90)
   if (inPeerGroup) {
     const auto rdst = make_rsrc((uint8_t*)v.peerScratch[remote] + base + (uint64_t)rank * g.ppr * 16);
     const uint64_t soff = (uint64_t)remote * sliceBytes;
-    for (uint32_t j = lb * T + tid; j < g.units; j += bpp * T) {
-      const bool two = 2ull * j + 1 < g.ppr;
-      const uint64_t off = soff + (uint64_t)j * 16;
-      const u32x4 w = load_payload<kPlain>(rin, in, off, clamp_valid(g.bytes, off, two ? 16 : 8));
-      ll16_put<kSystem>(rdst, j * 32u, w, flag, two);
+    for (uint32_t j = lb * T + tid; j < npk; j += bpp * T) {
+      const uint64_t off = soff + (uint64_t)j * 8;
+      unit_put<kSystem>(rdst, j * 16u, payload_ld(rin, in, off, clamp_valid(g.bytes, off, 8)), flag, false);
     }
   }
 
-  // step 2: reduce my slice from the n-1 incoming streams, store locally, broadcast the result
+  // step 2: reduce my slice from the n-1 incoming streams (own first, then peers ascending,
+  // :93-106), store locally, broadcast the reduced packets (:111-122)
   {
     const auto rscr = make_rsrc(scr);
     const uint64_t soff = (uint64_t)rank * sliceBytes;
-    for (uint32_t j = b * T + tid; j < g.units; j += G * T) {
-      const bool two = 2ull * j + 1 < g.ppr;
-      const uint64_t off = soff + (uint64_t)j * 16;
-      const uint32_t valid = clamp_valid(g.bytes, off, two ? 16 : 8);
-      u32x4 acc = load_payload<kPlain>(rin, in, off, valid);
-      u32x4 w[kMaxRanks];
+    for (uint32_t j = b * T + tid; j < npk; j += G * T) {
+      const uint64_t off = soff + (uint64_t)j * 8;
+      const uint32_t valid = clamp_valid(g.bytes, off, 8);
+      u32x2 acc = payload_ld(rin, in, off, valid);
+      u32x2 w[kMaxRanks];
       bool ready = true;
 #pragma unroll
       for (int p = 0; p < kMaxRanks; ++p)
-        if (p < nranks && p != rank) ready &= ll16_try(rscr, (uint32_t)(p * g.ppr * 16) + j * 32u, flag, w[p], two);
+        if (p < nranks && p != rank) ready &= unit_try(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, w[p], false);
       if (ready) {
 #pragma unroll
         for (int p = 0; p < kMaxRanks; ++p)
-          if (p < nranks && p != rank) acc = reduce4<DT, OP>(acc, w[p]);
+          if (p < nranks && p != rank) acc = reduce2<DT, OP>(acc, w[p]);
       } else {
-        // slow path: wait for each stream in sum order (own first, then peers ascending)
         for (int p = 0; p < nranks; ++p) {
           if (p == rank) continue;
-          acc = reduce4<DT, OP>(acc, ll16_get(rscr, (uint32_t)(p * g.ppr * 16) + j * 32u, flag, two, budget, v.err));
+          acc = reduce2<DT, OP>(acc, unit_get(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, false, budget, v.err));
         }
       }
-      store_payload<kPlain>(rout, out, off, acc, valid);
+      payload_st(rout, out, off, acc, valid);
       // broadcast: a runtime loop, so one descriptor is live at a time (SGPR budget)
 #pragma unroll 1
       for (int q = 0; q < nranks; ++q) {
         if (q == rank) continue;
         const auto rq = make_rsrc((uint8_t*)v.peerScratch[q] + base + g.roff + (uint64_t)rank * g.ppr * 16);
-        ll16_put<kSystem>(rq, j * 32u, acc, flag, two);
+        unit_put<kSystem>(rq, j * 16u, acc, flag, false);
       }
     }
   }
 
-  // step 3: unpack the reduced slice of peer `remote`
+  // step 3: unpack the reduced slice of peer `remote` (:125-132)
   if (inPeerGroup) {
     const auto rres = make_rsrc(scr + g.roff + (uint64_t)remote * g.ppr * 16);
     const uint64_t soff = (uint64_t)remote * sliceBytes;
-    for (uint32_t j = lb * T + tid; j < g.units; j += bpp * T) {
-      const bool two = 2ull * j + 1 < g.ppr;
-      const uint64_t off = soff + (uint64_t)j * 16;
-      const u32x4 w = ll16_get(rres, j * 32u, flag, two, budget, v.err);
-      store_payload<kPlain>(rout, out, off, w, clamp_valid(g.bytes, off, two ? 16 : 8));
+    for (uint32_t j = lb * T + tid; j < npk; j += bpp * T) {
+      const uint64_t off = soff + (uint64_t)j * 8;
+      const u32x2 w = unit_get(rres, j * 16u, flag, false, budget, v.err);
+      payload_st(rout, out, off, w, clamp_valid(g.bytes, off, 8));
     }
   }
   bump_flags(v.flags, flag);
-}
-
-// ---- LL8 ----------------------------------------------------------------------------------------
-template <int Policy>
-__device__ __forceinline__ void ll8_put(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, u32x4 w, uint32_t flag, uint32_t npk) {
-  if (npk == 4) {
-    store16<Policy>(pk, pbyte, u32x4{w.x, flag, w.y, flag});
-    store16<Policy>(pk, pbyte + 16, u32x4{w.z, flag, w.w, flag});
-  } else {
-    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if ((uint32_t)i < npk) store8<Policy>(pk, pbyte + 8 * i, u32x2{d[i], flag});
-  }
-}
-__device__ __forceinline__ bool ll8_try(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, u32x4& w, uint32_t npk) {
-  if (npk == 4) {
-    u32x4 a = load16<kSystem>(pk, pbyte);
-    u32x4 c = load16<kSystem>(pk, pbyte + 16);
-    w = u32x4{a.x, a.z, c.x, c.z};
-    return a.y == flag && a.w == flag && c.y == flag && c.w == flag;
-  }
-  uint32_t d[4] = {0, 0, 0, 0};
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if ((uint32_t)i < npk) {
-      u32x2 x = load8<kSystem>(pk, pbyte + 8 * i);
-      d[i] = x.x;
-      ok &= x.y == flag;
-    }
-  }
-  w = u32x4{d[0], d[1], d[2], d[3]};
-  return ok;
-}
-__device__ __forceinline__ u32x4 ll8_get(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, uint32_t npk,
-                                         uint64_t budget, uint32_t* err) {
-  u32x4 w;
-  if (ll8_try(pk, pbyte, flag, w, npk)) return w;
-  SpinGuard g(budget);
-  while (!ll8_try(pk, pbyte, flag, w, npk)) {
-    __builtin_amdgcn_s_sleep(1);
-    if (g.expired()) {
-      report_error(err, kErrPacketTimeout);
-      return u32x4{0, 0, 0, 0};
-    }
-  }
-  return w;
 }
 
 template <int DT, int OP, int NV>
@@ -210,40 +199,40 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
 
   // put my whole buffer into every peer's scratch at rank*W packets (allreduce_allpair_packet.cu:39-42)
   for (uint32_t j = gtid; j < g.units; j += G * T) {
-    const uint32_t npk = (uint32_t)((g.W - 4ull * j) < 4 ? (g.W - 4ull * j) : 4);
-    const uint64_t off = (uint64_t)j * 16;
-    const u32x4 w = load_payload<kPlain>(rin, in, off, clamp_valid(g.bytes, off, npk * 4));
+    const bool single = 2ull * j + 1 >= g.W;
+    const uint64_t off = (uint64_t)j * 8;
+    const u32x2 w = payload_ld(rin, in, off, clamp_valid(g.bytes, off, single ? 4 : 8));
 #pragma unroll 1
     for (int q = 0; q < nranks; ++q) {
       if (q == rank) continue;
       const auto rq = make_rsrc((uint8_t*)v.peerScratch[q] + base + (uint64_t)rank * region);
-      ll8_put<kSystem>(rq, j * 32u, w, flag, npk);
+      unit_put<kSystem>(rq, j * 16u, w, flag, single);
     }
   }
   // reduce: own first, then peers ascending (:49-61).  The same lane handled unit j above, so an
   // in-place call reads its input before overwriting it.
   const auto rscr = make_rsrc((uint8_t*)v.scratch + base);
   for (uint32_t j = gtid; j < g.units; j += G * T) {
-    const uint32_t npk = (uint32_t)((g.W - 4ull * j) < 4 ? (g.W - 4ull * j) : 4);
-    const uint64_t off = (uint64_t)j * 16;
-    const uint32_t valid = clamp_valid(g.bytes, off, npk * 4);
-    u32x4 acc = load_payload<kPlain>(rin, in, off, valid);
-    u32x4 w[kMaxRanks];
+    const bool single = 2ull * j + 1 >= g.W;
+    const uint64_t off = (uint64_t)j * 8;
+    const uint32_t valid = clamp_valid(g.bytes, off, single ? 4 : 8);
+    u32x2 acc = payload_ld(rin, in, off, valid);
+    u32x2 w[kMaxRanks];
     bool ready = true;
 #pragma unroll
     for (int p = 0; p < kMaxRanks; ++p)
-      if (p < nranks && p != rank) ready &= ll8_try(rscr, (uint32_t)(p * region) + j * 32u, flag, w[p], npk);
+      if (p < nranks && p != rank) ready &= unit_try(rscr, (uint32_t)(p * region) + j * 16u, flag, w[p], single);
     if (ready) {
 #pragma unroll
       for (int p = 0; p < kMaxRanks; ++p)
-        if (p < nranks && p != rank) acc = reduce4<DT, OP>(acc, w[p]);
+        if (p < nranks && p != rank) acc = reduce2<DT, OP>(acc, w[p]);
     } else {
       for (int p = 0; p < nranks; ++p) {
         if (p == rank) continue;
-        acc = reduce4<DT, OP>(acc, ll8_get(rscr, (uint32_t)(p * region) + j * 32u, flag, npk, budget, v.err));
+        acc = reduce2<DT, OP>(acc, unit_get(rscr, (uint32_t)(p * region) + j * 16u, flag, single, budget, v.err));
       }
     }
-    store_payload<kPlain>(rout, out, off, acc, valid);
+    payload_st(rout, out, off, acc, valid);
   }
   bump_flags(v.flags, flag);
 }
@@ -267,7 +256,7 @@ static LL16Geom ll16Geometry(int nranks, size_t bytes, int dtype) {
   // source's input packets would overlap the first reduced slice and a fast rank's broadcast could
   // overwrite packets not yet consumed.  Start the result region after the input region then.
   if ((uint64_t)nranks * g.ppr * 16 > g.roff) g.roff = (uint64_t)nranks * g.ppr * 16;
-  g.units = (uint32_t)((g.ppr + 1) / 2);
+  g.units = (uint32_t)g.ppr;
   return g;
 }
 
@@ -275,7 +264,7 @@ static LL8Geom ll8Geometry(size_t bytes, int dtype) {
   LL8Geom g{};
   g.bytes = bytes;
   g.W = is2byte(dtype) ? (bytes + 2) / 4 : bytes / 4;
-  g.units = (uint32_t)((g.W + 3) / 4);
+  g.units = (uint32_t)((g.W + 1) / 2);
   return g;
 }
 

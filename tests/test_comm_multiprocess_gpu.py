@@ -1,0 +1,95 @@
+"""Two processes, one rank each, both on cuda:0, through the NCCL ABI (ncclGetUniqueId ->
+ncclCommInitRank -> ncclAllReduce): exercises the TCP bootstrap, hipIpc handle exchange of
+scratch / semaphores / output buffers between processes, and every algorithm, checked bit-exactly
+against the CPU oracle (same LCG inputs as test/torch/correctness_test.py:44-56)."""
+import multiprocessing as mp
+import os
+import queue
+import traceback
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # (algo, dtype code, count)
+    ("allpair", 0, 4096), ("packet", 0, 1 << 18), ("fullmesh", 0, 1 << 20), ("rsag", 2, 100000),
+    ("packet", 1, 30000), ("auto", 0, 48 << 19), ("auto", 2, 1000), ("fullmesh", 1, 12345),
+]
+
+
+def _worker(rank, n, uid, q):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "5000")
+        import torch
+
+        import mscclpp_amd as m
+        import oracle_lib as O
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        tdt = {0: torch.float16, 1: torch.bfloat16, 2: torch.float32}
+        results = []
+        for algo, dt, count in CASES:
+            ins = [O.lcg(dt, count, r, 3) for r in range(n)]
+            x = torch.from_numpy(ins[rank].view(np.int16 if dt < 2 else np.int32).copy()).view(tdt[dt]).cuda()
+            out = torch.zeros_like(x)
+            for _ in range(3):  # repeated calls: flag / semaphore lifecycle, registration cache
+                comm.all_reduce(x, out, algo=None if algo == "auto" else algo)
+            torch.cuda.synchronize()
+            errc = comm.device_error()
+            nbytes = count * (2 if dt < 2 else 4)
+            sel = algo
+            if algo == "auto":
+                sel = {1: "packet", 2: "allpair", 3: "fullmesh"}[m.lib().mscclppAmdSelectAlgo(n, nbytes, dt)]
+            if sel == "packet":
+                exp, _ = O.allreduce_packet(dt, O.SUM, ins, count, 1, 1 << 22)
+                e = exp[rank].view(np.uint8)[:nbytes]
+            elif sel == "allpair":
+                exp, _ = O.allreduce_allpairs(dt, O.SUM, ins, count, 1, 1 << 22)
+                e = exp[rank].view(np.uint8)[:nbytes]
+            else:
+                sl = ((nbytes + n - 1) // n + 15) // 16 * 16
+                nw = (nbytes + 3) // 4
+                pad = []
+                for a in ins:
+                    w = np.zeros(nw, np.uint32)
+                    w.view(np.uint8)[:nbytes] = a.view(np.uint8)
+                    pad.append(w)
+                e = O.allreduce_sliced(dt, O.SUM, pad, nw, sl // 4, 1 if sel == "rsag" else 0)[rank].view(np.uint8)[:nbytes]
+            got = out.cpu().contiguous().view(torch.uint8).numpy()
+            results.append((algo, dt, count, errc, int(np.count_nonzero(got != e))))
+        comm.barrier()
+        comm.destroy()
+        q.put((rank, results, None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_two_process_ncclallreduce(built):
+    import mscclpp_amd as m
+
+    uid = m.Communicator.unique_id()  # root thread lives in this (parent) process
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    n = 2
+    procs = [ctx.Process(target=_worker, args=(r, n, uid, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=240)
+            assert err is None, err
+            got[rank] = res
+    except queue.Empty:
+        pytest.fail("multi-process AllReduce timed out")
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        for algo, dt, count, errc, bad in got[rank]:
+            assert errc == 0, (rank, algo, dt, count, errc)
+            assert bad == 0, (rank, algo, dt, count, bad)
