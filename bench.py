@@ -79,6 +79,18 @@ def cpu_baseline_allreduce(nbytes, n, budget_s):
             "sample": f"{iters} x oracle {n}-rank fullmesh-order fp16 sum of {sample >> 20} MiB (scalar C, 1 thread)"}
 
 
+def committed_traffic(S):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/<tag>_self_reduce_pmc.json:
+    2*FETCH_SIZE + WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md §HBM), or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_self_reduce_pmc.json")))
+    if not files or S != 48 << 20:
+        return None
+    d = json.load(open(files[-1]))
+    return d.get("hbm_bytes_per_launch_corrected")
+
+
 def bench_single(args):
     import mscclpp_amd as m
 
@@ -136,8 +148,8 @@ def bench_single(args):
         "config": {"workload": "ll16_self_reduce_fp16_48MiB (BASELINE configs[1]: pack+sum+unpack, 1 GPU)",
                    "bytes": S, "parallelism": "single-gpu"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "selfReduceLL16Kernel", "kernel_us": round(kern_ms * 1e3, 2),
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": committed_traffic(S),
+                     "kernel": "selfReduceLL16PmKernel", "kernel_us": round(kern_ms * 1e3, 2),
                      "algorithmic_bytes_per_launch": 7 * S},
     }
     if not args.no_cpu_baseline:
