@@ -37,6 +37,7 @@ def parse():
     p.add_argument("--algo", default=None, help="force an AllReduce algorithm (N>1): packet|allpair|fullmesh|rsag")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extras", action="store_true", help="N>1: skip the LL latency sweep and the fp32 1 GiB run")
     return p.parse_args()
 
 
@@ -158,6 +159,16 @@ def bench_single(args):
     return res
 
 
+def _time_calls(fn, reps):
+    """Mean per-call time (s) of `reps` back-to-back calls, synchronised on both sides."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps
+
+
 def bench_multi(args):
     import torch.distributed as dist
 
@@ -172,6 +183,7 @@ def bench_multi(args):
     torch.cuda.set_device(local)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = m.Communicator.from_torch_dist()
+    n = world
     S = args.bytes
     count = S // 2
     dev = torch.device("cuda", local)
@@ -179,8 +191,31 @@ def bench_multi(args):
     x = torch.rand(count, generator=g).to(torch.float16).to(dev)
     out = torch.empty_like(x)
 
+    def tmax(v):
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    # ---- pick the launch shape (untimed; every rank tries the same candidates in the same order)
+    algo = args.algo or {1: "packet", 2: "allpair", 3: "fullmesh", 4: "rsag"}[m.lib().mscclppAmdSelectAlgo(n, S, 0)]
+    if algo in ("fullmesh", "rsag"):
+        cands = [(64, 512), (32, 512), (128, 512), (64, 256), (128, 256)]
+    else:
+        cands = [(0, 0)]
+    tune = {}
+    for nb, nt in cands:
+        try:
+            for _ in range(2):
+                comm.all_reduce(x, out, algo=algo, nblocks=nb, nthreads=nt)
+            tune[(nb, nt)] = tmax(_time_calls(lambda: comm.all_reduce(x, out, algo=algo, nblocks=nb, nthreads=nt), 5))
+        except Exception as e:  # a rejected shape is simply skipped
+            tune[(nb, nt)] = float("inf")
+            if rank == 0:
+                print(f"tune {nb}x{nt}: {e}", file=sys.stderr)
+    nb, nt = min(tune, key=tune.get)
+
     def step():
-        comm.all_reduce(x, out, algo=args.algo)
+        comm.all_reduce(x, out, algo=algo, nblocks=nb, nthreads=nt)
 
     for _ in range(args.warmup):
         step()
@@ -191,7 +226,8 @@ def bench_multi(args):
         step()
         b.record()
     torch.cuda.synchronize()
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kern_ms = tmax(float(np.mean([a.elapsed_time(b) for a, b in evs])))
+    # ---- timed region: exactly K steps, barrier + synchronize on both sides, max over ranks
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -200,17 +236,18 @@ def bench_multi(args):
     torch.cuda.synchronize()
     t_local = (time.perf_counter() - t0) / args.steps
     dist.barrier()
-    tt = torch.tensor([t_local, kern_ms], dtype=torch.float64)
-    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t, kern_ms = float(tt[0]), float(tt[1])
+    t = tmax(t_local)
     errc = comm.device_error()
-    # correctness: compare with a gloo all-reduce of the same inputs in fp32 (tolerance check)
+    # correctness of the timed call: fp32 gloo reference of the same inputs (tolerance of
+    # python/mscclpp_benchmark/correctness.py:257-258)
     ref = x.float().cpu()
     dist.all_reduce(ref)
-    ok = torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=5e-4 * world)
+    ok = bool(torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=5e-4 * n)) and errc == 0
     algbw = S / t / 1e9
-    n = world
     ceiling = n * XGMI_LINK_GBS / 2  # all-pairs algbw ceiling
+    # HBM bytes one rank's bulk AllReduce moves (reads S input + (n-1)/n S scratch; writes S/n own
+    # output + (n-1)/n S incoming scratch + (n-1)/n S incoming output)
+    hbm = S * (1 + 3 * (n - 1) / n + 1 / n)
     res = {
         "metric": "device-resident AllReduce algbw GB/s fp16 at 1/2/4/8 MI355X; % xGMI roofline",
         "value": round(algbw, 2),
@@ -225,22 +262,57 @@ def bench_multi(args):
         "dtype": "f16",
         "data": "synthetic",
         "config": {"workload": f"allreduce_fp16_{S >> 20}MiB (BASELINE configs[2]: 2048x12288 fp16 bucket per rank)",
-                   "bytes": S, "parallelism": f"allreduce{world}", "algo": args.algo or "auto"},
+                   "bytes": S, "parallelism": f"allreduce{world}", "algo": algo, "nblocks": nb, "nthreads": nt},
         "busbw": round(algbw * 2 * (n - 1) / n, 2),
         "xgmi": {"allpairs_algbw_ceiling": round(ceiling, 1), "frac": round(algbw / ceiling, 4),
-                 "link_GBs": XGMI_LINK_GBS},
-        "roofline": {"bound": "hbm", "achieved": round(S * (2 + 2 * (n - 1) / n) / (kern_ms * 1e-3) / 1e9, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None, "kernel": "allreduce (per launch)",
-                     "kernel_us": round(kern_ms * 1e3, 2)},
-        "correct": bool(ok and errc == 0),
+                 "link_GBs_assumed": XGMI_LINK_GBS, "wire_bytes_per_rank": int(2 * (n - 1) * S / n)},
+        "roofline": {"bound": "hbm", "achieved": round(hbm / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "traffic": None, "kernel": f"allreduceBulkKernel ({algo})",
+                     "kernel_us": round(kern_ms * 1e3, 2), "algorithmic_bytes_per_launch": int(hbm)},
+        "tune_ms": {f"{k[0]}x{k[1]}": round(v * 1e3, 4) for k, v in tune.items()},
+        "correct": ok,
     }
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if not args.no_extras:
+        res["extras"] = bench_extras(args, comm, n, dev, tmax)
     if rank == 0 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_allreduce(S, n, args.cpu_seconds)
     comm.destroy()
     dist.barrier()
     dist.destroy_process_group()
     return res if rank == 0 else None
+
+
+def bench_extras(args, comm, n, dev, tmax):
+    """BASELINE configs[3] (LL latency sweep, fp16 1 KiB..1 MiB) and configs[4] (fp32 1 GiB
+    RS+AG in ring order), timed the same way; failures are recorded, not raised."""
+    extras = {}
+    try:
+        lat = {}
+        for kb in (1, 4, 16, 64, 256, 1024):
+            cnt = kb * 512
+            xs = torch.rand(cnt, device=dev).half()
+            os_ = torch.empty_like(xs)
+            for _ in range(5):
+                comm.all_reduce(xs, os_)
+            lat[f"{kb}KiB"] = round(tmax(_time_calls(lambda: comm.all_reduce(xs, os_), 50)) * 1e6, 2)
+        extras["ll_latency_us"] = lat
+    except Exception as e:
+        extras["ll_latency_error"] = str(e)
+    try:
+        S = 1 << 30
+        xs = torch.rand(S // 4, device=dev)
+        os_ = torch.empty_like(xs)
+        for _ in range(2):
+            comm.all_reduce(xs, os_, algo="rsag")
+        t = tmax(_time_calls(lambda: comm.all_reduce(xs, os_, algo="rsag"), 5))
+        extras["fp32_1GiB_rsag"] = {"ms": round(t * 1e3, 3), "algbw_GBs": round(S / t / 1e9, 2),
+                                    "busbw_GBs": round(S / t / 1e9 * 2 * (n - 1) / n, 2)}
+        del xs, os_
+    except Exception as e:
+        extras["fp32_1GiB_rsag_error"] = str(e)
+    extras["device_error"] = comm.device_error()
+    return extras
 
 
 def main():

@@ -28,7 +28,7 @@ extern "C" {
 
 #define MSCCLPP_AMD_MAX_RANKS 8
 #define MSCCLPP_AMD_FLAG_SLOTS 1024
-#define MSCCLPP_AMD_MAX_CHANNELS 64
+#define MSCCLPP_AMD_MAX_CHANNELS 128
 
 /* dtype / op codes of the extension API (ncclDataType_t / ncclRedOp_t are mapped onto these) */
 enum { MSCCLPP_AMD_F16 = 0, MSCCLPP_AMD_BF16 = 1, MSCCLPP_AMD_F32 = 2, MSCCLPP_AMD_I32 = 3, MSCCLPP_AMD_U32 = 4 };
@@ -100,6 +100,13 @@ int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes);
 int mscclppAmdCommFlags(ncclComm_t comm, uint32_t** flags);
 /* Bootstrap all-gather of `bytes` per rank (host memory), for harnesses. */
 int mscclppAmdCommAllGatherHost(ncclComm_t comm, const void* sendbuf, void* recvbuf, size_t bytes);
+
+/* ---- bootstrap (TcpBootstrap, src/core/bootstrap/bootstrap.cc:169-611) -------------------------
+ * Host-only setup plane; uniqueId is the 128-byte ncclUniqueId from ncclGetUniqueId. */
+int mscclppAmdBootstrapCreate(int rank, int nranks, const void* uniqueId, void** handle);
+int mscclppAmdBootstrapAllGather(void* handle, const void* sendbuf, void* recvbuf, size_t bytes);
+int mscclppAmdBootstrapBarrier(void* handle);
+int mscclppAmdBootstrapDestroy(void* handle);
 
 #ifdef __cplusplus
 }

@@ -22,7 +22,7 @@ ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG = 0, 1, 2, 3, 4
 ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4}
 MAX_RANKS = 8
 FLAG_SLOTS = 1024
-MAX_CHANNELS = 64
+MAX_CHANNELS = 128
 
 # ncclDataType_t / ncclRedOp_t (include/mscclpp_amd/nccl.h, values of the reference nccl.h:217-253)
 NCCL_DTYPES = {torch.float16: 6, torch.bfloat16: 9, torch.float32: 7, torch.int32: 2}

@@ -673,4 +673,37 @@ int mscclppAmdCommAllGatherHost(ncclComm_t comm, const void* sendbuf, void* recv
   });
 }
 
+// ---- bootstrap (setup plane only; host code, usable without a GPU) -------------------------
+int mscclppAmdBootstrapCreate(int rank, int nranks, const void* uniqueId, void** handle) {
+  return guarded([&] {
+    if (!uniqueId || !handle || nranks <= 0 || rank < 0 || rank >= nranks) return (int)ncclInvalidArgument;
+    BootstrapId id;
+    std::memcpy(&id, uniqueId, sizeof(id));
+    if (!bootstrapIdValid(id)) return (int)ncclInvalidArgument;
+    *handle = new Bootstrap(rank, nranks, id, 120);
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdBootstrapAllGather(void* handle, const void* sendbuf, void* recvbuf, size_t bytes) {
+  return guarded([&] {
+    if (!handle) return (int)ncclInvalidArgument;
+    static_cast<Bootstrap*>(handle)->allGather(sendbuf, recvbuf, bytes);
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdBootstrapBarrier(void* handle) {
+  return guarded([&] {
+    if (!handle) return (int)ncclInvalidArgument;
+    static_cast<Bootstrap*>(handle)->barrier();
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdBootstrapDestroy(void* handle) {
+  delete static_cast<Bootstrap*>(handle);
+  return ncclSuccess;
+}
+
 }  // extern "C"
