@@ -92,9 +92,46 @@ def committed_traffic(S):
     return d.get("hbm_bytes_per_launch_corrected")
 
 
+def host_proxy_baseline():
+    """BASELINE config 1 (host-proxy path, 2 ranks, 4 KiB) -- spawned before this process touches the GPU."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import host_proxy_baseline as H
+
+        return H.run(2, 4096, timeout=240)
+    except Exception as e:  # recorded, never fatal for the headline line
+        return {"error": str(e)[-400:]}
+
+
+def staged_rate(m, S, x, y, out, pk, flags, err, reps=10):
+    """IB/proxy staging: buckets start and end in host-pinned memory, so time H2D(x, y) + kernel + D2H(out)."""
+    hx = torch.empty(x.numel(), dtype=x.dtype).pin_memory()
+    hy = torch.empty_like(hx).pin_memory()
+    ho = torch.empty_like(hx).pin_memory()
+    hx.copy_(x.cpu())
+    hy.copy_(y.cpu())
+
+    def step():
+        x.copy_(hx, non_blocking=True)
+        y.copy_(hy, non_blocking=True)
+        m.self_reduce_ll16(x, y, pk.ptr, out, flags, err)
+        ho.copy_(out, non_blocking=True)
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    return {"value": round(S / t / 1e9, 2), "unit": "GB/s", "ms_per_step": round(t * 1e3, 3),
+            "note": "S / (H2D 2S + pack+sum+unpack + D2H S) with host-pinned buffers (PCIe-inclusive)"}
+
+
 def bench_single(args):
     import mscclpp_amd as m
 
+    hp = None if args.no_cpu_baseline else host_proxy_baseline()
     S = args.bytes
     count = S // 2
     dev = torch.device("cuda", 0)
@@ -153,8 +190,10 @@ def bench_single(args):
                      "kernel": "selfReduceLL16PmKernel", "kernel_us": round(kern_ms * 1e3, 2),
                      "algorithmic_bytes_per_launch": 7 * S},
     }
+    res["staged_pcie_inclusive"] = staged_rate(m, S, x, y, out, pk, flags, err)
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_self_reduce(S, args.cpu_seconds)
+        res["host_proxy_baseline"] = hp
     pk.free()
     return res
 

@@ -101,6 +101,19 @@ int mscclppAmdCommFlags(ncclComm_t comm, uint32_t** flags);
 /* Bootstrap all-gather of `bytes` per rank (host memory), for harnesses. */
 int mscclppAmdCommAllGatherHost(ncclComm_t comm, const void* sendbuf, void* recvbuf, size_t bytes);
 
+/* ---- host-proxy path (PortChannel / FIFO / proxy thread) ------------------------------------
+ * Config-1 harness: test/allgather_test_host_offloading.cu on this library.  out[0] = us per
+ * kernel (no graph), out[1] = us per kernel (graph of graphIters x 2 kernels), out[2] = 1 if the
+ * gathered data is correct, out[3] = NUMA node the proxy thread was bound to (-1 if none). */
+int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, int iters, int graphIters, double* out);
+/* PortChannel all-to-all through the proxy (mode 0: put+signal, 1: putWithSignal,
+ * 2: putWithSignalAndFlush).  out[0] = us per iteration, out[1] = 1 if correct, out[2] = NUMA node. */
+int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int mode, int iters, double* out);
+int mscclppAmdLaunchHostOffloadKernel(int rank, int nranks, const void* fifoHandle, void* semHandles, int handleIndex,
+                                      uint64_t budget, uint32_t* err, void* stream);
+int mscclppAmdLaunchPortChannelPut(void* chans, int nchans, const uint64_t* dstOffs, const uint64_t* srcOffs,
+                                   uint64_t chunk, int mode, void* stream);
+
 /* ---- bootstrap (TcpBootstrap, src/core/bootstrap/bootstrap.cc:169-611) -------------------------
  * Host-only setup plane; uniqueId is the 128-byte ncclUniqueId from ncclGetUniqueId. */
 int mscclppAmdBootstrapCreate(int rank, int nranks, const void* uniqueId, void** handle);

@@ -7,332 +7,7 @@
 //  * ncclComm + NCCL ABI    -- nccl.cc:187-905: bootstrap, IPC-mapped scratch and semaphores,
 //                             per-buffer registration cache (algorithm.cc:42-68 context cache)
 // Every C entry point catches C++ exceptions and returns an ncclResult_t (SURVEY §8b "Errors").
-#include <hip/hip_runtime.h>
-
-#include <array>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <map>
-#include <memory>
-#include <mutex>
-#include <stdexcept>
-#include <string>
-#include <vector>
-
-#include "bootstrap.hpp"
-#include "mscclpp_amd/mscclpp_amd.h"
-#include "mscclpp_amd/nccl.h"
-
-namespace mscclpp_amd {
-int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
-                      int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
-int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
-                        int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
-size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype);
-size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype);
-struct BulkGeom;
-size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks);
-}  // namespace mscclpp_amd
-
-using namespace mscclpp_amd;
-
-namespace {
-
-struct HipError : std::runtime_error {
-  hipError_t code;
-  HipError(hipError_t c, const char* what) : std::runtime_error(what), code(c) {}
-};
-
-#define HIPCHECK(cmd)                                                                               \
-  do {                                                                                              \
-    hipError_t e_ = (cmd);                                                                          \
-    if (e_ != hipSuccess) {                                                                         \
-      char buf_[256];                                                                               \
-      snprintf(buf_, sizeof(buf_), "%s:%d %s -> %s", __FILE__, __LINE__, #cmd, hipGetErrorString(e_)); \
-      throw HipError(e_, buf_);                                                                     \
-    }                                                                                               \
-  } while (0)
-
-thread_local std::string gLastError;
-
-int logLevel() {
-  static int lvl = [] {
-    const char* e = std::getenv("MSCCLPP_LOG_LEVEL");
-    if (!e) return 1;
-    std::string s(e);
-    if (s == "DEBUG" || s == "TRACE") return 3;
-    if (s == "INFO") return 2;
-    if (s == "WARN") return 1;
-    return 0;
-  }();
-  return lvl;
-}
-
-void warn(const std::string& m) {
-  gLastError = m;
-  if (logLevel() >= 1) fprintf(stderr, "[mscclpp_amd WARN] %s\n", m.c_str());
-}
-void info(const std::string& m) {
-  if (logLevel() >= 2) fprintf(stderr, "[mscclpp_amd INFO] %s\n", m.c_str());
-}
-
-template <typename F>
-int guarded(F&& f) {
-  try {
-    return f();
-  } catch (const HipError& e) {
-    warn(e.what());
-    return ncclUnhandledCudaError;
-  } catch (const std::exception& e) {
-    warn(e.what());
-    return ncclInternalError;
-  } catch (...) {
-    warn("unknown exception");
-    return ncclInternalError;
-  }
-}
-
-uint64_t spinBudgetTicks() {
-  static uint64_t t = [] {
-    const char* e = std::getenv("MSCCLPP_AMD_SPIN_TIMEOUT_MS");
-    uint64_t ms = e ? std::strtoull(e, nullptr, 10) : 20000;
-    if (ms == 0) ms = 20000;
-    return ms * 100000ull;  // s_memrealtime ticks at 100 MHz
-  }();
-  return t;
-}
-
-void* allocUncached(size_t bytes) {
-  void* p = nullptr;
-  HIPCHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
-  HIPCHECK(hipMemset(p, 0, bytes));
-  return p;
-}
-
-int dtypeFromNccl(ncclDataType_t t) {
-  switch (t) {
-    case ncclFloat16: return MSCCLPP_AMD_F16;
-    case ncclBfloat16: return MSCCLPP_AMD_BF16;
-    case ncclFloat32: return MSCCLPP_AMD_F32;
-    case ncclInt32: return MSCCLPP_AMD_I32;
-    case ncclUint32: return MSCCLPP_AMD_U32;
-    default: return -1;
-  }
-}
-size_t ncclTypeBytes(ncclDataType_t t) {
-  switch (t) {
-    case ncclInt8: case ncclUint8: case ncclFloat8e4m3: case ncclFloat8e5m2: return 1;
-    case ncclFloat16: case ncclBfloat16: return 2;
-    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
-    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
-    default: return 0;
-  }
-}
-int opFromNccl(ncclRedOp_t op) {
-  if (op == ncclSum) return MSCCLPP_AMD_SUM;
-  if (op == ncclMin) return MSCCLPP_AMD_MIN;
-  return -1;
-}
-
-int envAlgo() {
-  const char* e = std::getenv("MSCCLPP_AMD_ALGO");
-  if (!e) return MSCCLPP_AMD_ALGO_AUTO;
-  std::string s(e);
-  if (s == "packet") return MSCCLPP_AMD_ALGO_PACKET;
-  if (s == "allpair" || s == "allpair_packet") return MSCCLPP_AMD_ALGO_ALLPAIR;
-  if (s == "fullmesh") return MSCCLPP_AMD_ALGO_FULLMESH;
-  if (s == "rsag") return MSCCLPP_AMD_ALGO_RSAG;
-  return MSCCLPP_AMD_ALGO_AUTO;
-}
-
-}  // namespace
-
-// =============================================================================================
-// ncclComm
-// =============================================================================================
-struct IpcBlob {
-  hipIpcMemHandle_t handle;
-  uint64_t base;    // allocation base in the owner's address space (cache key)
-  uint64_t offset;  // pointer - base
-  uint64_t bytes;
-};
-
-struct ncclComm {
-  std::unique_ptr<Bootstrap> boot;
-  int rank = 0, nranks = 1, device = 0;
-  // LL scratch (two halves, packets), bulk scratch, semaphores, flags, error word
-  void* llScratch = nullptr;
-  size_t llBytes = 0;
-  void* bulkScratch = nullptr;
-  size_t bulkBytes = 0;
-  uint64_t* tokens = nullptr;
-  uint64_t* expected = nullptr;
-  uint32_t* flags = nullptr;
-  uint32_t* err = nullptr;
-  std::array<void*, MSCCLPP_AMD_MAX_RANKS> peerLL{}, peerBulk{};
-  std::array<uint64_t*, MSCCLPP_AMD_MAX_RANKS> peerTokens{};
-  // peer mappings opened through IPC: (peer, peer allocation base) -> mapped base here
-  std::map<std::pair<int, uint64_t>, void*> opened;
-  // registered output buffers: local allocation base -> per-peer mapped pointers of that buffer
-  struct Reg {
-    uint64_t bytes;
-    std::array<uint64_t, MSCCLPP_AMD_MAX_RANKS> peerBase;  // mapped peer allocation bases
-    std::array<uint64_t, MSCCLPP_AMD_MAX_RANKS> peerOffsetBase;
-  };
-  std::map<std::pair<uint64_t, uint64_t>, std::array<void*, MSCCLPP_AMD_MAX_RANKS>> outRegs;
-  std::mutex mu;
-
-  // Exchange an IPC handle for [ptr, ptr+bytes) and return every rank's pointer as mapped here.
-  std::array<void*, MSCCLPP_AMD_MAX_RANKS> exchange(void* ptr) {
-    IpcBlob mine{};
-    void* base = nullptr;
-    size_t sz = 0;
-    HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)ptr));
-    HIPCHECK(hipIpcGetMemHandle(&mine.handle, base));
-    info("rank " + std::to_string(rank) + ": got ipc handle, all-gather");
-    mine.base = (uint64_t)base;
-    mine.offset = (uint64_t)((char*)ptr - (char*)base);
-    mine.bytes = sz;
-    std::vector<IpcBlob> all(nranks);
-    boot->allGather(&mine, all.data(), sizeof(IpcBlob));
-    std::array<void*, MSCCLPP_AMD_MAX_RANKS> res{};
-    for (int r = 0; r < nranks; ++r) {
-      if (r == rank) {
-        res[r] = ptr;
-        continue;
-      }
-      auto key = std::make_pair(r, all[r].base);
-      auto it = opened.find(key);
-      void* mapped = nullptr;
-      if (it == opened.end()) {
-        info("rank " + std::to_string(rank) + ": opening ipc handle of rank " + std::to_string(r));
-        HIPCHECK(hipIpcOpenMemHandle(&mapped, all[r].handle, hipIpcMemLazyEnablePeerAccess));
-        info("rank " + std::to_string(rank) + ": opened");
-        opened[key] = mapped;
-      } else {
-        mapped = it->second;
-      }
-      res[r] = (char*)mapped + all[r].offset;
-    }
-    return res;
-  }
-
-  void forgetMapping(int peer, void* mappedBase) {
-    for (auto it = opened.begin(); it != opened.end(); ++it) {
-      if (it->first.first == peer && it->second == mappedBase) {
-        (void)hipIpcCloseMemHandle(it->second);
-        opened.erase(it);
-        return;
-      }
-    }
-  }
-
-  // Grow a scratch region collectively (every rank calls with the same size at the same call).
-  void ensure(void*& buf, size_t& have, std::array<void*, MSCCLPP_AMD_MAX_RANKS>& peers, size_t need) {
-    if (need <= have) return;
-    size_t want = have ? have : (size_t)64 << 20;
-    while (want < need) want *= 2;
-    HIPCHECK(hipDeviceSynchronize());
-    boot->barrier();  // every rank has drained its previous use of the old buffers
-    for (int r = 0; r < nranks; ++r)
-      if (r != rank && peers[r]) forgetMapping(r, peers[r]);
-    if (buf) HIPCHECK(hipFree(buf));
-    buf = allocUncached(want);
-    have = want;
-    peers = exchange(buf);
-    boot->barrier();
-    info("rank " + std::to_string(rank) + " scratch grown to " + std::to_string(want));
-  }
-
-  std::array<void*, MSCCLPP_AMD_MAX_RANKS> registerOutput(void* out) {
-    void* base = nullptr;
-    size_t sz = 0;
-    HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)out));
-    auto key = std::make_pair((uint64_t)base, (uint64_t)sz);
-    auto it = outRegs.find(key);
-    std::array<void*, MSCCLPP_AMD_MAX_RANKS> peersOfBase;
-    if (it == outRegs.end()) {
-      peersOfBase = exchange(base);  // collective: every rank registers its matching buffer now
-      outRegs[key] = peersOfBase;
-    } else {
-      peersOfBase = it->second;
-    }
-    // The offset of `out` inside its allocation must be the same on every rank for the cached
-    // mapping to be reused; exchange offsets (cheap) to check and build exact pointers.
-    uint64_t off = (uint64_t)((char*)out - (char*)base);
-    std::vector<uint64_t> offs(nranks);
-    boot->allGather(&off, offs.data(), sizeof(off));
-    std::array<void*, MSCCLPP_AMD_MAX_RANKS> res{};
-    for (int r = 0; r < nranks; ++r) res[r] = (r == rank) ? out : (char*)peersOfBase[r] + offs[r];
-    return res;
-  }
-
-  mscclppAmdRankView baseView(const void* in, void* out) {
-    mscclppAmdRankView v{};
-    v.input = in;
-    v.output = out;
-    v.tokens = tokens;
-    v.expected = expected;
-    v.flags = flags;
-    v.err = err;
-    v.rank = rank;
-    for (int r = 0; r < nranks; ++r) v.peerTokens[r] = peerTokens[r];
-    return v;
-  }
-
-  int allReduce(const void* in, void* out, size_t bytes, int dtype, int op, int algo, int nblocks, int nthreads,
-                hipStream_t stream) {
-    std::lock_guard<std::mutex> lk(mu);
-    if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = envAlgo();
-    if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = mscclppAmdSelectAlgo(nranks, bytes, dtype);
-    mscclppAmdRankView v = baseView(in, out);
-    if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR) {
-      const size_t need = algo == MSCCLPP_AMD_ALGO_PACKET ? ll16ScratchRequired(nranks, bytes, dtype)
-                                                          : ll8ScratchRequired(nranks, bytes, dtype);
-      ensure(llScratch, llBytes, peerLL, need);
-      v.scratch = llScratch;
-      v.scratchBytes = llBytes;
-      for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerLL[r];
-      return launchAllReduceLL(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
-    }
-    if (algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG) {
-      // a bucket up to 1 GiB fits in one pass with the default 1 GiB bulk scratch
-      size_t need = bytes + 16 * (size_t)nranks * 64;
-      const size_t cap = (size_t)1 << 30;
-      if (need > cap) need = cap;
-      ensure(bulkScratch, bulkBytes, peerBulk, need);
-      v.scratch = bulkScratch;
-      v.scratchBytes = bulkBytes;
-      for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
-      auto outs = registerOutput(out);
-      for (int r = 0; r < nranks; ++r) v.peerOutput[r] = outs[r];
-      return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
-    }
-    return ncclInvalidArgument;
-  }
-
-  void destroy() {
-    (void)hipDeviceSynchronize();
-    if (boot) {
-      try {
-        boot->barrier();
-      } catch (...) {
-      }
-    }
-    for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
-    opened.clear();
-    if (llScratch) (void)hipFree(llScratch);
-    if (bulkScratch) (void)hipFree(bulkScratch);
-    if (tokens) (void)hipFree(tokens);
-    if (expected) (void)hipFree(expected);
-    if (flags) (void)hipFree(flags);
-    if (err) (void)hipFree(err);
-    llScratch = bulkScratch = nullptr;
-    tokens = expected = nullptr;
-    flags = err = nullptr;
-  }
-};
+#include "comm_internal.hpp"
 
 // =============================================================================================
 // C ABI: memory, microbench, launcher, selector

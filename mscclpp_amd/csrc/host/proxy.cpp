@@ -1,0 +1,461 @@
+// Host-proxy transport: trigger FIFO (host side), proxy thread, ProxyService and the two harnesses
+// built on them (the config-1 host-offload AllGather and a PortChannel all-to-all).
+//
+// Reference behaviour:
+//   Fifo::poll / pop                 src/core/fifo.cc:58-78 (commit bit = lap parity, cleared on read)
+//   Proxy::start loop                src/core/proxy.cc:42-100 (busy poll, handler, pop; NUMA bind :23-33)
+//   ProxyService::handleTrigger      src/core/port_channel.cc:117-154 (Data -> write, Flag -> signal,
+//                                    Sync -> flush then publish flushDonePos)
+//   CudaIpcConnection::write/flush   src/core/connection.cc:138-195 (hipMemcpyAsync on a per-connection
+//                                    stream; updateAndSync = H2D copy of the outbound token)
+//   MyProxyService / main timing     test/allgather_test_host_offloading.cu:81-330
+#include <sched.h>
+
+#include <atomic>
+#include <chrono>
+#include <fstream>
+#include <functional>
+#include <sstream>
+#include <thread>
+
+#include "comm_internal.hpp"
+#include "mscclpp_amd/port_channel_device.hpp"
+
+extern "C" int mscclppAmdLaunchHostOffloadKernel(int rank, int nranks, const void* fifoHandle, void* semHandles,
+                                                 int handleIndex, uint64_t budget, uint32_t* err, void* stream);
+extern "C" int mscclppAmdLaunchPortChannelPut(void* chans, int nchans, const uint64_t* dstOffs, const uint64_t* srcOffs,
+                                              uint64_t chunk, int mode, void* stream);
+
+namespace mscclpp_amd {
+namespace host {
+
+// ---- NUMA: pin the proxy thread to the CPUs of the GPU's NUMA node (proxy.cc:23-33) ----------
+static int deviceNumaNode(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return -1;
+  std::string id(bus);
+  for (auto& ch : id) ch = (char)std::tolower(ch);
+  std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
+  int node = -1;
+  if (f) f >> node;
+  return node;
+}
+
+static int bindToNumaNode(int node) {
+  if (node < 0) return -1;
+  std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+  std::string list;
+  if (!f || !std::getline(f, list)) return -1;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  int count = 0;
+  std::stringstream ss(list);
+  std::string part;
+  while (std::getline(ss, part, ',')) {
+    int a = 0, b = 0;
+    if (sscanf(part.c_str(), "%d-%d", &a, &b) == 2) {
+      for (int c = a; c <= b; ++c, ++count) CPU_SET(c, &set);
+    } else if (sscanf(part.c_str(), "%d", &a) == 1) {
+      CPU_SET(a, &set);
+      ++count;
+    }
+  }
+  if (count == 0) return -1;
+  return sched_setaffinity(0, sizeof(set), &set) == 0 ? node : -1;
+}
+
+// ---- FIFO (host side) --------------------------------------------------------------------------
+class Fifo {
+ public:
+  explicit Fifo(int size) : size_(size) {
+    if (size <= 0 || (size & (size - 1))) throw std::invalid_argument("FIFO size must be a power of two");
+    while ((1 << shift_) < size) ++shift_;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    HIPCHECK(hipHostMalloc((void**)&triggers_, sizeof(ProxyTrigger) * size, fl));
+    std::memset((void*)triggers_, 0, sizeof(ProxyTrigger) * size);
+    HIPCHECK(hipHostMalloc((void**)&tail_, 64, fl));
+    std::memset((void*)tail_, 0, 64);
+    HIPCHECK(hipHostGetDevicePointer((void**)&dTriggers_, (void*)triggers_, 0));
+    HIPCHECK(hipHostGetDevicePointer((void**)&dTail_, (void*)tail_, 0));
+    HIPCHECK(hipMalloc((void**)&head_, 64));
+    HIPCHECK(hipMemset(head_, 0, 64));
+    HIPCHECK(hipMalloc((void**)&tailCache_, 64));
+    HIPCHECK(hipMemset(tailCache_, 0, 64));
+  }
+  ~Fifo() {
+    (void)hipHostFree((void*)triggers_);
+    (void)hipHostFree((void*)tail_);
+    (void)hipFree(head_);
+    (void)hipFree(tailCache_);
+  }
+  // fifo.cc:58-73: accept the slot only when its commit bit carries this lap's parity.
+  bool poll(ProxyTrigger& t) {
+    const uint64_t cur = *tail_;
+    ProxyTrigger* slot = &triggers_[cur & (uint64_t)(size_ - 1)];
+    const uint64_t snd = __atomic_load_n(&slot->snd, __ATOMIC_ACQUIRE);
+    const uint64_t parity = ((cur >> shift_) & 1ull) ^ 1ull;
+    if ((snd >> 63) != parity) return false;
+    t.snd = snd & ~(1ull << 63);
+    t.fst = __atomic_load_n(&slot->fst, __ATOMIC_RELAXED);
+    return true;
+  }
+  void pop() { __atomic_store_n(tail_, *tail_ + 1, __ATOMIC_RELEASE); }  // fifo.cc:75-78
+  uint64_t tail() const { return *tail_; }
+  FifoDeviceHandle deviceHandle() const {
+    FifoDeviceHandle h{};
+    h.triggers = dTriggers_;
+    h.head = head_;
+    h.tail = dTail_;
+    h.tailCache = tailCache_;
+    h.size = size_;
+    h.sizeMask = (uint64_t)size_ - 1;
+    h.sizeShift = (uint64_t)shift_;
+    return h;
+  }
+
+ private:
+  int size_;
+  int shift_ = 0;
+  ProxyTrigger* triggers_ = nullptr;
+  ProxyTrigger* dTriggers_ = nullptr;
+  uint64_t* tail_ = nullptr;
+  uint64_t* dTail_ = nullptr;
+  uint64_t* head_ = nullptr;
+  uint64_t* tailCache_ = nullptr;
+};
+
+// ---- proxy thread ------------------------------------------------------------------------------
+class Proxy {
+ public:
+  using Handler = std::function<bool(const ProxyTrigger&, uint64_t pos)>;  // true = stop
+  Proxy(int device, int fifoSize, Handler h) : device_(device), fifo_(fifoSize), handler_(std::move(h)) {}
+  ~Proxy() { stop(); }
+  void start() {
+    running_.store(true, std::memory_order_release);
+    th_ = std::thread([this] {
+      (void)hipSetDevice(device_);
+      numaNode_ = bindToNumaNode(deviceNumaNode(device_));
+      hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+      (void)hipThreadExchangeStreamCaptureMode(&mode);  // never capture in a proxy thread
+      started_.store(true, std::memory_order_release);
+      ProxyTrigger t;
+      int runCnt = 4096;
+      for (;;) {
+        if (runCnt-- == 0) {
+          runCnt = 4096;
+          if (!running_.load(std::memory_order_acquire)) break;
+        }
+        if (!fifo_.poll(t)) continue;
+        const bool stop = handler_(t, fifo_.tail());
+        fifo_.pop();
+        if (stop) break;
+      }
+    });
+    while (!started_.load(std::memory_order_acquire)) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  void stop() {
+    if (th_.joinable()) {
+      running_.store(false, std::memory_order_release);
+      th_.join();
+    }
+  }
+  Fifo& fifo() { return fifo_; }
+  int numaNode() const { return numaNode_; }
+
+ private:
+  int device_;
+  Fifo fifo_;
+  Handler handler_;
+  std::thread th_;
+  std::atomic<bool> running_{false};
+  std::atomic<bool> started_{false};
+  int numaNode_ = -1;
+};
+
+static double nowSec() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Per-peer host-driven connection: a non-blocking stream (CudaIpcStream, context.cc:16-46).
+struct Conn {
+  hipStream_t stream = nullptr;
+};
+
+}  // namespace host
+}  // namespace mscclpp_amd
+
+// =============================================================================================
+// Harness 1: test/allgather_test_host_offloading.cu on the C ABI (BASELINE config 1)
+// =============================================================================================
+extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, int iters, int graphIters,
+                                             double* out) {
+  return guarded([&] {
+    if (!comm || !out || dataSize == 0) return (int)ncclInvalidArgument;
+    const int n = comm->nranks, rank = comm->rank;
+    if (n < 2 || dataSize % (4 * (size_t)n)) return (int)ncclInvalidArgument;
+    const size_t perRank = dataSize / n;
+    const size_t nelems = dataSize / 4;
+    // data: element i = i+1 in my part, 0 elsewhere (:64-79)
+    int* data = nullptr;
+    HIPCHECK(hipMalloc((void**)&data, dataSize));
+    std::vector<int> h(nelems, 0);
+    for (size_t i = 0; i < nelems; ++i)
+      if (i / (perRank / 4) == (size_t)rank) h[i] = (int)(i + 1);
+    HIPCHECK(hipMemcpy(data, h.data(), dataSize, hipMemcpyHostToDevice));
+    auto peers = comm->exchange(data);
+    // two Host2Device semaphore sets per peer (:86-87): inbound tokens [2][n], expected [2][n]
+    uint64_t* tok = nullptr;
+    uint64_t* expct = nullptr;
+    HIPCHECK(hipMalloc((void**)&tok, 2 * n * 8));
+    HIPCHECK(hipMemset(tok, 0, 2 * n * 8));
+    HIPCHECK(hipMalloc((void**)&expct, 2 * n * 8));
+    HIPCHECK(hipMemset(expct, 0, 2 * n * 8));
+    auto peerTok = comm->exchange(tok);
+    uint64_t* hcnt = nullptr;
+    HIPCHECK(hipHostMalloc((void**)&hcnt, 2 * n * 8, hipHostMallocDefault));
+    std::memset(hcnt, 0, 2 * n * 8);
+    std::vector<Host2DeviceSemaphoreDeviceHandle> hh(2 * n);
+    for (int s = 0; s < 2; ++s)
+      for (int r = 0; r < n; ++r) hh[s * n + r] = {tok + s * n + r, expct + s * n + r};
+    Host2DeviceSemaphoreDeviceHandle* dh = nullptr;
+    HIPCHECK(hipMalloc((void**)&dh, hh.size() * sizeof(hh[0])));
+    HIPCHECK(hipMemcpy(dh, hh.data(), hh.size() * sizeof(hh[0]), hipMemcpyHostToDevice));
+    std::vector<Conn> conns(n);
+    for (int r = 0; r < n; ++r)
+      if (r != rank) HIPCHECK(hipStreamCreateWithFlags(&conns[r].stream, hipStreamNonBlocking));
+    uint32_t* err = nullptr;
+    HIPCHECK(hipMalloc((void**)&err, 64));
+    HIPCHECK(hipMemset(err, 0, 64));
+    // MyProxyService::handleTrigger (:135-155)
+    Proxy proxy(comm->device, 512, [&](const ProxyTrigger& t, uint64_t) {
+      if (t.fst > 0) {
+        const int set = t.fst == 1 ? 0 : 1;
+        for (int k = 1; k < n; ++k) {
+          const int nghr = (rank + k) % n;
+          (void)hipMemcpyAsync((char*)peers[nghr] + rank * perRank, (char*)data + rank * perRank, perRank,
+                               hipMemcpyDeviceToDevice, conns[nghr].stream);
+          uint64_t* c = &hcnt[set * n + nghr];
+          __atomic_store_n(c, *c + 1, __ATOMIC_RELAXED);
+          (void)hipMemcpyAsync((uint64_t*)peerTok[nghr] + set * n + rank, c, 8, hipMemcpyHostToDevice,
+                               conns[nghr].stream);
+        }
+      }
+      return false;
+    });
+    proxy.start();
+    FifoDeviceHandle fh = proxy.fifo().deviceHandle();
+    hipStream_t st;
+    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const uint64_t budget = spinBudgetTicks();
+    auto k = [&](int set) {
+      int rc = mscclppAmdLaunchHostOffloadKernel(rank, n, &fh, dh + (set - 1) * n, set, budget, err, st);
+      if (rc) throw std::runtime_error("host offload kernel launch failed");
+    };
+    // correctness (:258-271)
+    k(1);
+    HIPCHECK(hipStreamSynchronize(st));
+    std::vector<int> back(nelems);
+    HIPCHECK(hipMemcpy(back.data(), data, dataSize, hipMemcpyDeviceToHost));
+    bool ok = true;
+    for (size_t i = 0; i < nelems; ++i) ok &= back[i] == (int)(i + 1);
+    comm->boot->barrier();
+    // no-graph timing (:275-292)
+    HIPCHECK(hipStreamSynchronize(st));
+    comm->boot->barrier();
+    double t0 = nowSec();
+    for (int i = 0; i < iters; ++i) {
+      k(1);
+      k(2);
+    }
+    HIPCHECK(hipStreamSynchronize(st));
+    comm->boot->barrier();
+    double t1 = nowSec();
+    out[0] = (t1 - t0) * 1e6 / iters / 2;
+    // graph timing (:294-330): graphIters x (2 kernels) captured, 10 warmup replays, 10 timed
+    hipGraph_t graph;
+    hipGraphExec_t inst;
+    HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    for (int i = 0; i < graphIters; ++i) {
+      k(1);
+      k(2);
+    }
+    HIPCHECK(hipStreamEndCapture(st, &graph));
+    HIPCHECK(hipGraphInstantiate(&inst, graph, nullptr, nullptr, 0));
+    for (int i = 0; i < 10; ++i) HIPCHECK(hipGraphLaunch(inst, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    comm->boot->barrier();
+    t0 = nowSec();
+    for (int i = 0; i < 10; ++i) HIPCHECK(hipGraphLaunch(inst, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    t1 = nowSec();
+    out[1] = (t1 - t0) * 1e6 / 10 / graphIters / 2;
+    comm->boot->barrier();
+    uint32_t e = 0;
+    HIPCHECK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost));
+    out[2] = (ok && e == 0) ? 1.0 : 0.0;
+    out[3] = (double)proxy.numaNode();
+    proxy.stop();
+    for (int r = 0; r < n; ++r)
+      if (conns[r].stream) {
+        (void)hipStreamSynchronize(conns[r].stream);
+        (void)hipStreamDestroy(conns[r].stream);
+      }
+    (void)hipGraphExecDestroy(inst);
+    (void)hipGraphDestroy(graph);
+    (void)hipStreamDestroy(st);
+    comm->boot->barrier();  // peers no longer touch my data / tokens
+    for (int r = 0; r < n; ++r)
+      if (r != rank) {  // peers free these buffers now: drop the cached mappings
+        comm->forgetMapping(r, peers[r]);
+        comm->forgetMapping(r, peerTok[r]);
+      }
+    (void)hipFree(err);
+    (void)hipFree(dh);
+    (void)hipHostFree(hcnt);
+    (void)hipFree(tok);
+    (void)hipFree(expct);
+    (void)hipFree(data);
+    return (int)ncclSuccess;
+  });
+}
+
+// =============================================================================================
+// Harness 2: PortChannel all-to-all through ProxyService (port_channel.cc:117-178)
+// =============================================================================================
+extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int mode, int iters, double* out) {
+  return guarded([&] {
+    if (!comm || !out || chunk == 0 || chunk % 4 || mode < 0 || mode > 2) return (int)ncclInvalidArgument;
+    const int n = comm->nranks, rank = comm->rank;
+    if (n < 2) return (int)ncclInvalidArgument;
+    const size_t bytes = chunk * n;
+    uint32_t *src = nullptr, *dst = nullptr;
+    HIPCHECK(hipMalloc((void**)&src, bytes));
+    HIPCHECK(hipMalloc((void**)&dst, bytes));
+    HIPCHECK(hipMemset(dst, 0, bytes));
+    std::vector<uint32_t> h(bytes / 4);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = (uint32_t)(rank * 0x01000000u + i);  // src chunk q for peer q
+    HIPCHECK(hipMemcpy(src, h.data(), bytes, hipMemcpyHostToDevice));
+    auto peerDst = comm->exchange(dst);
+    // MemoryId 0 = my src; 1 + q = peer q's dst.  One semaphore (and channel) per peer.
+    std::vector<void*> mem(1 + n);
+    mem[0] = src;
+    for (int q = 0; q < n; ++q) mem[1 + q] = peerDst[q];
+    uint64_t *tok = nullptr, *expct = nullptr, *hcnt = nullptr, *flushDone = nullptr, *dFlushDone = nullptr;
+    HIPCHECK(hipMalloc((void**)&tok, n * 8));
+    HIPCHECK(hipMemset(tok, 0, n * 8));
+    HIPCHECK(hipMalloc((void**)&expct, n * 8));
+    HIPCHECK(hipMemset(expct, 0, n * 8));
+    auto peerTok = comm->exchange(tok);
+    HIPCHECK(hipHostMalloc((void**)&hcnt, n * 8, hipHostMallocDefault));
+    std::memset(hcnt, 0, n * 8);
+    HIPCHECK(hipHostMalloc((void**)&flushDone, n * 64, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(flushDone, 0, n * 64);
+    HIPCHECK(hipHostGetDevicePointer((void**)&dFlushDone, flushDone, 0));
+    std::vector<Conn> conns(n);
+    for (int q = 0; q < n; ++q)
+      if (q != rank) HIPCHECK(hipStreamCreateWithFlags(&conns[q].stream, hipStreamNonBlocking));
+    uint32_t* err = nullptr;
+    HIPCHECK(hipMalloc((void**)&err, 64));
+    HIPCHECK(hipMemset(err, 0, 64));
+    // semaphoreId = peer index
+    Proxy proxy(comm->device, 512, [&](const ProxyTrigger& t, uint64_t pos) {
+      const int q = (int)t.fields.semaphoreId;
+      if (q < 0 || q >= n || q == rank) return false;
+      if (t.fields.type & kTriggerData)
+        (void)hipMemcpyAsync((char*)mem[t.fields.dstMemoryId] + t.fields.dstOffset,
+                             (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
+                             hipMemcpyDeviceToDevice, conns[q].stream);
+      if (t.fields.type & kTriggerFlag) {
+        uint64_t* c = &hcnt[q];
+        __atomic_store_n(c, *c + 1, __ATOMIC_RELAXED);
+        // remote token slot of peer q for source `rank`
+        (void)hipMemcpyAsync((uint64_t*)peerTok[q] + rank, c, 8, hipMemcpyHostToDevice, conns[q].stream);
+      }
+      if (t.fields.type & kTriggerSync) {
+        (void)hipStreamSynchronize(conns[q].stream);
+        __atomic_store_n(&flushDone[q * 8], pos + 1, __ATOMIC_RELEASE);
+      }
+      return false;
+    });
+    proxy.start();
+    std::vector<PortChannelDeviceHandle> ch;
+    for (int q = 0; q < n; ++q) {
+      if (q == rank) continue;
+      PortChannelDeviceHandle c{};
+      c.semaphoreId = (uint32_t)q;
+      c.dst = (uint32_t)(1 + q);
+      c.src = 0;
+      c.semaphore = {tok + q, expct + q};
+      c.fifo = proxy.fifo().deviceHandle();
+      c.flushDonePos = dFlushDone + q * 8;
+      c.budget = spinBudgetTicks();
+      c.err = err;
+      ch.push_back(c);
+    }
+    // channel c (peer q) moves my src chunk q to offset rank*chunk of q's dst
+    std::vector<uint64_t> offs;
+    for (int q = 0; q < n; ++q)
+      if (q != rank) offs.push_back((uint64_t)rank * chunk);
+    for (int q = 0; q < n; ++q)
+      if (q != rank) offs.push_back((uint64_t)q * chunk);
+    uint64_t* dOffs = nullptr;
+    HIPCHECK(hipMalloc((void**)&dOffs, offs.size() * 8));
+    HIPCHECK(hipMemcpy(dOffs, offs.data(), offs.size() * 8, hipMemcpyHostToDevice));
+    PortChannelDeviceHandle* dch = nullptr;
+    HIPCHECK(hipMalloc((void**)&dch, ch.size() * sizeof(ch[0])));
+    HIPCHECK(hipMemcpy(dch, ch.data(), ch.size() * sizeof(ch[0]), hipMemcpyHostToDevice));
+    hipStream_t st;
+    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    comm->boot->barrier();
+    double t0 = nowSec();
+    for (int i = 0; i < iters; ++i) {
+      if (mscclppAmdLaunchPortChannelPut(dch, (int)ch.size(), dOffs, dOffs + ch.size(), chunk, mode, st))
+        throw std::runtime_error("launch");
+    }
+    HIPCHECK(hipStreamSynchronize(st));
+    double t1 = nowSec();
+    comm->boot->barrier();
+    out[0] = (t1 - t0) * 1e6 / iters;
+    // check: peer p's chunk addressed to me (its src chunk `rank`) sits at offset p*chunk of my dst
+    std::vector<uint32_t> back(bytes / 4);
+    HIPCHECK(hipMemcpy(back.data(), dst, bytes, hipMemcpyDeviceToHost));
+    bool ok = true;
+    for (int p = 0; p < n && ok; ++p) {
+      if (p == rank) continue;
+      for (size_t i = 0; i < chunk / 4; ++i) {
+        const size_t srcElem = (size_t)rank * (chunk / 4) + i;
+        if (back[(size_t)p * (chunk / 4) + i] != (uint32_t)(p * 0x01000000u + srcElem)) {
+          ok = false;
+          break;
+        }
+      }
+    }
+    uint32_t e = 0;
+    HIPCHECK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost));
+    out[1] = (ok && e == 0) ? 1.0 : 0.0;
+    out[2] = (double)proxy.numaNode();
+    proxy.stop();
+    for (int q = 0; q < n; ++q)
+      if (conns[q].stream) {
+        (void)hipStreamSynchronize(conns[q].stream);
+        (void)hipStreamDestroy(conns[q].stream);
+      }
+    (void)hipStreamDestroy(st);
+    comm->boot->barrier();
+    for (int q = 0; q < n; ++q)
+      if (q != rank) {
+        comm->forgetMapping(q, peerDst[q]);
+        comm->forgetMapping(q, peerTok[q]);
+      }
+    (void)hipFree(dOffs);
+    (void)hipFree(dch);
+    (void)hipFree(err);
+    (void)hipHostFree(flushDone);
+    (void)hipHostFree(hcnt);
+    (void)hipFree(tok);
+    (void)hipFree(expct);
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    return (int)ncclSuccess;
+  });
+}

@@ -93,3 +93,18 @@ def test_two_process_ncclallreduce(built):
         for algo, dt, count, errc, bad in got[rank]:
             assert errc == 0, (rank, algo, dt, count, errc)
             assert bad == 0, (rank, algo, dt, count, bad)
+
+
+def test_host_proxy_paths(built):
+    """Config 1 (host-offload AllGather through the FIFO + proxy thread) and the PortChannel
+    put / putWithSignal / putWithSignalAndFlush surface, 2 processes on cuda:0."""
+    import sys as _s
+
+    _s.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import host_proxy_baseline as H
+
+    res = H.run(2, 4096, timeout=200)
+    assert res["correct"], res
+    assert res["us_per_kernel_graph"] > 0
+    for mode, r in res["portchannel_alltoall_1MiB"].items():
+        assert r["correct"], (mode, r)

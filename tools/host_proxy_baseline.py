@@ -1,0 +1,76 @@
+"""BASELINE config 1: the host-proxy path of test/allgather_test_host_offloading.cu (2 ranks,
+4 KiB, CPU proxy thread per rank moves the bytes with hipMemcpyAsync), run on this library.
+
+Prints one JSON object: us per kernel without / with graph, algbw, correctness, cores used.
+Ranks are processes (spawn); on a 1-GPU box both use cuda:0 (loopback), as the config describes."""
+import ctypes
+import json
+import multiprocessing as mp
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def worker(rank, n, uid, size, q):
+    try:
+        import torch
+
+        import mscclpp_amd as m
+
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(rank % ndev)
+        L = m.lib()
+        L.mscclppAmdHostOffloadAllGather.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.POINTER(ctypes.c_double)]
+        L.mscclppAmdPortChannelAllToAll.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.POINTER(ctypes.c_double)]
+        comm = m.Communicator(rank, n, uid)
+        out = (ctypes.c_double * 4)()
+        m.check(L.mscclppAmdHostOffloadAllGather(comm.comm, size, 10, 10, out), "host offload")
+        res = {"us_per_kernel_nograph": out[0], "us_per_kernel_graph": out[1], "correct": out[2] == 1.0,
+               "proxy_numa_node": int(out[3])}
+        pc = {}
+        for mode in (0, 1, 2):
+            o = (ctypes.c_double * 3)()
+            m.check(L.mscclppAmdPortChannelAllToAll(comm.comm, 1 << 20, mode, 5, o), "portchannel")
+            pc[["put+signal", "putWithSignal", "putWithSignalAndFlush"][mode]] = {"us": round(o[0], 2),
+                                                                                  "correct": o[1] == 1.0}
+        res["portchannel_alltoall_1MiB"] = pc
+        comm.destroy()
+        q.put((rank, res, None))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def run(n=2, size=4096, timeout=180):
+    import mscclpp_amd as m
+
+    uid = m.Communicator.unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=worker, args=(r, n, uid, size, q)) for r in range(n)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(n):
+        rank, res, err = q.get(timeout=timeout)
+        if err:
+            raise RuntimeError(err)
+        got[rank] = res
+    for p in ps:
+        p.join(timeout=30)
+    r0 = got[0]
+    us = r0["us_per_kernel_graph"]
+    return {"value": round(size / (us * 1e-6) / 1e9, 4), "unit": "GB/s", "us_per_kernel_graph": round(us, 2),
+            "us_per_kernel_nograph": round(r0["us_per_kernel_nograph"], 2), "bytes": size, "ranks": n,
+            "correct": all(g["correct"] for g in got.values()),
+            "cores": 2 * n, "cores_note": "per rank: 1 busy-poll proxy thread + 1 launching thread",
+            "proxy_numa_node": r0["proxy_numa_node"], "portchannel_alltoall_1MiB": r0["portchannel_alltoall_1MiB"],
+            "path": "test/allgather_test_host_offloading.cu restated on libmscclpp_amd (FIFO + proxy + hipMemcpyAsync)"}
+
+
+if __name__ == "__main__":
+    print(json.dumps(run(int(sys.argv[1]) if len(sys.argv) > 1 else 2)), flush=True)
