@@ -114,6 +114,10 @@ int mscclppAmdLaunchHostOffloadKernel(int rank, int nranks, const void* fifoHand
 int mscclppAmdLaunchPortChannelPut(void* chans, int nchans, const uint64_t* dstOffs, const uint64_t* srcOffs,
                                    uint64_t chunk, int mode, void* stream);
 
+/* MemoryChannel device-surface self-test on one GPU (two in-process ranks): mode 0 LL16 packet
+ * ping-pong, 1 LL8 ping-pong, 2 put + signal/wait round trip.  *failures = mismatching words. */
+int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int* failures, uint32_t* devErr);
+
 /* ---- bootstrap (TcpBootstrap, src/core/bootstrap/bootstrap.cc:169-611) -------------------------
  * Host-only setup plane; uniqueId is the 128-byte ncclUniqueId from ncclGetUniqueId. */
 int mscclppAmdBootstrapCreate(int rank, int nranks, const void* uniqueId, void** handle);

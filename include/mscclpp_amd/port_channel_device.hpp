@@ -119,6 +119,7 @@ struct Host2DeviceSemaphoreDeviceHandle {
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
     return true;
   }
 #endif

@@ -56,6 +56,7 @@ __device__ __forceinline__ void block_handshake(const mscclppAmdRankView& v, int
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
   }
   __syncthreads();
 }

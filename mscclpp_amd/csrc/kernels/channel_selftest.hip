@@ -1,0 +1,134 @@
+// Self-tests of the MemoryChannel device surface on one GPU: two in-process "ranks" (blocks 0 and 1
+// of one launch), each with its own buffer, packet buffer and semaphore tokens, connected by
+// MemoryChannelDeviceHandles whose dst_ points at the other rank's memory.
+//
+//  mode 0: LL16 packet ping-pong  (test/mp_unit/memory_channel_tests.cu:286-338)
+//  mode 1: LL8 packet ping-pong   (memory_channel_tests.cu:246-284)
+//  mode 2: put + signal / wait + get round trip (memory_channel_tests.cu put/get/signal tests)
+#include "common.hpp"
+#include "mscclpp_amd/memory_channel_device.hpp"
+
+namespace mscclpp_amd {
+
+__global__ void memChanSelfTestKernel(MemoryChannelDeviceHandle* chans, int* b0, int* b1, int nElem, int nTries,
+                                      int mode, int* ret) {
+  const int rank = blockIdx.x;
+  MemoryChannelDeviceHandle& ch = chans[rank];
+  int* sendBuff = rank == 0 ? b0 : b1;
+  const int putOffset = rank == 0 ? 0 : 10000000;
+  const int getOffset = rank == 0 ? 10000000 : 0;
+  if (mode <= 1) {
+    for (int i = 0; i < nTries; ++i) {
+      const uint32_t flag = (uint32_t)i + 1;
+      if ((rank ^ (i & 1)) == 0) {
+        for (int j = threadIdx.x; j < nElem; j += blockDim.x) sendBuff[j] = putOffset + i + j;
+        __syncthreads();
+        if (mode == 0)
+          ch.putPackets<LL16Packet>(0, 0, nElem * sizeof(int), threadIdx.x, blockDim.x, flag);
+        else
+          ch.putPackets<LL8Packet>(0, 0, nElem * sizeof(int), threadIdx.x, blockDim.x, flag);
+      } else {
+        if (mode == 0)
+          ch.unpackPackets<LL16Packet>(0, 0, nElem * sizeof(int), threadIdx.x, blockDim.x, flag);
+        else
+          ch.unpackPackets<LL8Packet>(0, 0, nElem * sizeof(int), threadIdx.x, blockDim.x, flag);
+        __syncthreads();
+        for (int j = threadIdx.x; j < nElem; j += blockDim.x)
+          if (sendBuff[j] != getOffset + i + j) atomicAdd(ret, 1);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  // mode 2: each rank writes its half into the peer's buffer, signals, waits for the peer's
+  // signal, checks the half it received, then gets the peer's own half back and checks it.
+  const int half = nElem / 2;
+  for (int i = 0; i < nTries; ++i) {
+    for (int j = threadIdx.x; j < half; j += blockDim.x) sendBuff[rank * half + j] = putOffset + i + j;
+    __syncthreads();
+    ch.put((uint64_t)rank * half * 4, (uint64_t)half * 4, threadIdx.x, blockDim.x);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      ch.signal();
+      ch.wait();
+    }
+    __syncthreads();
+    const int peer = 1 - rank;
+    for (int j = threadIdx.x; j < half; j += blockDim.x)
+      if (sendBuff[peer * half + j] != getOffset + i + j) atomicAdd(ret, 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // both ranks are done reading before the next round overwrites
+      ch.signal();
+      ch.wait();
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace mscclpp_amd
+
+using namespace mscclpp_amd;
+
+// Returns 0 on success, the mismatch count in *failures, any device error code in *devErr.
+extern "C" int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int* failures, uint32_t* devErr) {
+  if (!failures || !devErr || nElem <= 0 || nElem % 2 || mode < 0 || mode > 2) return 4;
+  const size_t bytes = (size_t)nElem * 4;
+  int *b[2] = {nullptr, nullptr}, *ret = nullptr;
+  void* pk[2] = {nullptr, nullptr};
+  uint64_t *tok = nullptr, *exp = nullptr;
+  uint32_t* err = nullptr;
+  MemoryChannelDeviceHandle* dch = nullptr;
+  int rc = 0;
+#define CK(x)                   \
+  if ((x) != hipSuccess) {      \
+    rc = 1;                     \
+    goto done;                  \
+  }
+  for (int r = 0; r < 2; ++r) {
+    CK(hipMalloc((void**)&b[r], bytes));
+    CK(hipMemset(b[r], 0, bytes));
+    CK(hipExtMallocWithFlags(&pk[r], bytes * 4, hipDeviceMallocUncached));
+    CK(hipMemset(pk[r], 0, bytes * 4));
+  }
+  CK(hipExtMallocWithFlags((void**)&tok, 64, hipDeviceMallocUncached));
+  CK(hipMemset(tok, 0, 64));
+  CK(hipMalloc((void**)&exp, 64));
+  CK(hipMemset(exp, 0, 64));
+  CK(hipMalloc((void**)&ret, 4));
+  CK(hipMemset(ret, 0, 4));
+  CK(hipMalloc((void**)&err, 4));
+  CK(hipMemset(err, 0, 4));
+  {
+    MemoryChannelDeviceHandle h[2];
+    for (int r = 0; r < 2; ++r) {
+      const int p = 1 - r;
+      h[r].semaphore_ = {tok + r, tok + p, exp + r};
+      // packet modes: dst_ = peer's packet buffer; mode 2: dst_ = peer's data buffer
+      h[r].dst_ = mode <= 1 ? pk[p] : (void*)b[p];
+      h[r].src_ = b[r];
+      h[r].packetBuffer_ = pk[r];
+      h[r].budget_ = 200000000ull;  // 2 s
+      h[r].err_ = err;
+    }
+    CK(hipMalloc((void**)&dch, sizeof(h)));
+    CK(hipMemcpy(dch, h, sizeof(h), hipMemcpyHostToDevice));
+  }
+  hipLaunchKernelGGL(memChanSelfTestKernel, dim3(2), dim3(256), 0, 0, dch, b[0], b[1], nElem, nTries, mode, ret);
+  CK(hipGetLastError());
+  CK(hipDeviceSynchronize());
+  CK(hipMemcpy(failures, ret, 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(devErr, err, 4, hipMemcpyDeviceToHost));
+done:
+#undef CK
+  for (int r = 0; r < 2; ++r) {
+    if (b[r]) (void)hipFree(b[r]);
+    if (pk[r]) (void)hipFree(pk[r]);
+  }
+  if (tok) (void)hipFree(tok);
+  if (exp) (void)hipFree(exp);
+  if (ret) (void)hipFree(ret);
+  if (err) (void)hipFree(err);
+  if (dch) (void)hipFree(dch);
+  return rc;
+}
