@@ -86,6 +86,11 @@ int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblocks, void* 
  * nranks runs every rank of the collective inside this process. */
 int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes,
                               int dtype, int op, int nblocks, int nthreads, uint64_t budgetTicks, void* stream);
+/* coll 0 AllReduce (bytes = buffer), 1 ReduceScatter / 2 AllGather (bytes = nranks * block, block %
+ * 16 == 0) through the bulk all-pairs kernel (reduce-scatter / all-gather halves of fullmesh). */
+int mscclppAmdCollectiveLaunch(int coll, int algo, const mscclppAmdRankView* views, int nviews, int nranks,
+                               size_t bytes, int dtype, int op, int nblocks, int nthreads, uint64_t budgetTicks,
+                               void* stream);
 /* Scratch bytes per rank (both halves) that `algo` needs for `bytes` (0 if unsupported). */
 size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype);
 /* Algorithm the selector picks (algorithm_selector.cc:91-139 restated for gfx950). */

@@ -81,6 +81,9 @@ def lib():
         "mscclppAmdSelfReduceLL16": [vp, vp, vp, vp, sz, i32, i32, vp, i32, u64, vp, vp],
         "mscclppAmdAllReduceLaunch": [i32, ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, i32, u64, vp],
         "mscclppAmdSelectAlgo": [i32, sz, i32],
+        "mscclppAmdCollectiveLaunch": [i32, i32, ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, i32, u64, vp],
+        "ncclReduceScatter": [vp, vp, sz, i32, i32, vp, vp],
+        "ncclAllGather": [vp, vp, sz, i32, vp, vp],
         "ncclGetUniqueId": [ctypes.POINTER(UniqueId)],
         "ncclCommInitRank": [ctypes.POINTER(vp), i32, UniqueId, i32],
         "ncclCommDestroy": [vp],
@@ -211,6 +214,17 @@ class InProcessRanks:
                                                budget_ticks, stream_ptr(stream))
         check(code, "in-process all_reduce")
 
+    def collective(self, coll, inputs, outputs, algo=ALGO_FULLMESH, op=SUM, nblocks=8, nthreads=256,
+                   budget_ticks=500_000_000, stream=None):
+        """coll 1 = ReduceScatter (inputs n*block, outputs block), 2 = AllGather (inputs block, outputs n*block)."""
+        dt = DTYPE_CODES[inputs[0].dtype]
+        big = inputs[0] if coll == 1 else outputs[0]
+        nbytes = big.numel() * big.element_size()
+        arr = self.views(inputs, outputs, bulk=True)
+        code = lib().mscclppAmdCollectiveLaunch(coll, algo, arr, self.n, self.n, nbytes, dt, op, nblocks, nthreads,
+                                                budget_ticks, stream_ptr(stream))
+        check(code, "in-process collective")
+
     def errors(self):
         return [int(e[0].item()) for e in self.err]
 
@@ -269,6 +283,19 @@ class Communicator:
                                                  ALGO_NAMES.get(algo, algo) if isinstance(algo, str) else algo,
                                                  nblocks, nthreads, stream_ptr(stream))
         check(code, "ncclAllReduce")
+        return recv
+
+    def reduce_scatter(self, send, recv, op="sum", stream=None):
+        """ncclReduceScatter(send, recv, recvcount, dtype, op, comm, stream)."""
+        check(lib().ncclReduceScatter(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(recv.data_ptr()), recv.numel(),
+                                      NCCL_DTYPES[send.dtype], NCCL_OPS[op], self.comm, stream_ptr(stream)),
+              "ncclReduceScatter")
+        return recv
+
+    def all_gather(self, send, recv, stream=None):
+        """ncclAllGather(send, recv, sendcount, dtype, comm, stream)."""
+        check(lib().ncclAllGather(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(recv.data_ptr()), send.numel(),
+                                  NCCL_DTYPES[send.dtype], self.comm, stream_ptr(stream)), "ncclAllGather")
         return recv
 
     def barrier(self):

@@ -80,6 +80,27 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
   });
 }
 
+int mscclppAmdCollectiveLaunch(int coll, int algo, const mscclppAmdRankView* views, int nviews, int nranks,
+                               size_t bytes, int dtype, int op, int nblocks, int nthreads, uint64_t budgetTicks,
+                               void* stream) {
+  if (coll == 0)
+    return mscclppAmdAllReduceLaunch(algo, views, nviews, nranks, bytes, dtype, op, nblocks, nthreads, budgetTicks,
+                                     stream);
+  return guarded([&] {
+    if (!views || nviews < 1 || nranks < 2 || nranks > MSCCLPP_AMD_MAX_RANKS || bytes == 0) return (int)ncclInvalidArgument;
+    if (nviews != 1 && nviews != nranks) return (int)ncclInvalidArgument;
+    if (coll != 1 && coll != 2) return (int)ncclInvalidArgument;
+    for (int i = 0; i < nviews; ++i) {
+      const mscclppAmdRankView& v = views[i];
+      if (!v.input || !v.output || !v.scratch || !v.tokens || !v.expected || !v.err) return (int)ncclInvalidArgument;
+      for (int q = 0; q < nranks; ++q)
+        if (!v.peerScratch[q] || !v.peerTokens[q] || !v.peerOutput[q]) return (int)ncclInvalidArgument;
+    }
+    return launchCollectiveBulk(coll, algo, views, nviews, nranks, bytes, dtype, op, nblocks, nthreads,
+                                budgetTicks ? budgetTicks : spinBudgetTicks(), (hipStream_t)stream);
+  });
+}
+
 size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype) {
   if (algo == MSCCLPP_AMD_ALGO_PACKET) return ll16ScratchRequired(nranks, bytes, dtype);
   if (algo == MSCCLPP_AMD_ALGO_ALLPAIR) return ll8ScratchRequired(nranks, bytes, dtype);
@@ -262,14 +283,41 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
   });
 }
 
-ncclResult_t ncclReduceScatter(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, void*) {
-  warn("ncclReduceScatter: not on the AllReduce hot path yet (SURVEY §8f row 2)");
-  return ncclInvalidUsage;
+ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recvcount, ncclDataType_t datatype,
+                               ncclRedOp_t op, ncclComm_t comm, void* stream) {
+  return (ncclResult_t)guarded([&] {
+    if (!comm) return (int)ncclInvalidArgument;
+    const size_t tb = ncclTypeBytes(datatype);
+    const size_t bytes = recvcount * tb;
+    if (comm->nranks == 1) {  // nccl.cc:662-672
+      if (sendbuff != recvbuff && bytes)
+        HIPCHECK(hipMemcpyAsync(recvbuff, sendbuff, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+      return (int)ncclSuccess;
+    }
+    if (!sendbuff || !recvbuff || recvcount == 0 || tb == 0) return (int)ncclInvalidArgument;
+    const int dt = dtypeFromNccl(datatype), o = opFromNccl(op);
+    if (dt < 0 || o < 0) return (int)ncclInvalidArgument;
+    return comm->bulkCollective(1, sendbuff, recvbuff, bytes, dt, o, MSCCLPP_AMD_ALGO_AUTO, 0, 0, (hipStream_t)stream);
+  });
 }
 
-ncclResult_t ncclAllGather(const void*, void*, size_t, ncclDataType_t, ncclComm_t, void*) {
-  warn("ncclAllGather: not on the AllReduce hot path yet (SURVEY §8f row 2)");
-  return ncclInvalidUsage;
+ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcount, ncclDataType_t datatype,
+                           ncclComm_t comm, void* stream) {
+  return (ncclResult_t)guarded([&] {
+    if (!comm) return (int)ncclInvalidArgument;
+    const size_t tb = ncclTypeBytes(datatype);
+    const size_t bytes = sendcount * tb;
+    if (comm->nranks == 1) {
+      if (sendbuff != recvbuff && bytes)
+        HIPCHECK(hipMemcpyAsync(recvbuff, sendbuff, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+      return (int)ncclSuccess;
+    }
+    if (!sendbuff || !recvbuff || sendcount == 0 || tb == 0) return (int)ncclInvalidArgument;
+    const int dt = (tb == 2) ? MSCCLPP_AMD_F16 : MSCCLPP_AMD_F32;  // bytes are moved, not summed
+    if (tb != 2 && tb != 4 && tb != 1 && tb != 8) return (int)ncclInvalidArgument;
+    return comm->bulkCollective(2, sendbuff, recvbuff, bytes, dt, MSCCLPP_AMD_SUM, MSCCLPP_AMD_ALGO_AUTO, 0, 0,
+                                (hipStream_t)stream);
+  });
 }
 
 ncclResult_t ncclGroupStart(void) { return ncclSuccess; }

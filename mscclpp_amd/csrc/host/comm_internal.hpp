@@ -21,6 +21,8 @@
 namespace mscclpp_amd {
 int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
                       int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
+int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes,
+                         int dtype, int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
 int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
                         int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
 size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype);
@@ -304,6 +306,35 @@ struct ncclComm {
       return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
     }
     return ncclInvalidArgument;
+  }
+
+  // ReduceScatter (mode 1) / AllGather (mode 2) through the bulk all-pairs kernel; `bytes` is the
+  // per-rank block (recvcount / sendcount bytes).
+  int bulkCollective(int mode, const void* in, void* out, size_t blockBytes, int dtype, int op, int algo, int nblocks,
+                     int nthreads, hipStream_t stream) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (blockBytes % 16) {
+      warn("ReduceScatter/AllGather blocks must be a multiple of 16 bytes on this path");
+      return ncclInvalidUsage;
+    }
+    const size_t total = blockBytes * nranks;
+    mscclppAmdRankView v = baseView(in, out);
+    size_t need = total + 16 * (size_t)nranks * 64;
+    const size_t cap = (size_t)1 << 30;
+    if (need > cap) need = cap;
+    ensure(bulkScratch, bulkBytes, peerBulk, need);
+    v.scratch = bulkScratch;
+    v.scratchBytes = bulkBytes;
+    for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
+    if (mode == 2) {
+      auto outs = registerOutput(out);
+      for (int r = 0; r < nranks; ++r) v.peerOutput[r] = outs[r];
+    } else {
+      for (int r = 0; r < nranks; ++r) v.peerOutput[r] = out;  // unused by ReduceScatter
+    }
+    if (algo != MSCCLPP_AMD_ALGO_RSAG) algo = MSCCLPP_AMD_ALGO_FULLMESH;
+    return launchCollectiveBulk(mode, algo, &v, 1, nranks, total, dtype, op, nblocks, nthreads, spinBudgetTicks(),
+                                stream);
   }
 
   void destroy() {

@@ -61,11 +61,13 @@ __device__ __forceinline__ void block_handshake(const mscclppAmdRankView& v, int
   __syncthreads();
 }
 
-template <int DT, int OP, int NV, int ORDER>
+// MODE 0: AllReduce.  MODE 1: ReduceScatter (input n*slice, output = my reduced slice; no
+// all-gather).  MODE 2: AllGather (input = my slice, output n*slice; no reduce-scatter, no sum).
+template <int DT, int OP, int NV, int ORDER, int MODE>
 __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, BulkGeom g, int nranks, uint64_t budget) {
   const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
   const int rank = v.rank;
-  const uint32_t T = blockDim.x, tid = threadIdx.x, b = blockIdx.x, G = gridDim.x;
+  const uint32_t T = blockDim.x, tid = threadIdx.x, b = blockIdx.x;
   const uint8_t* in = (const uint8_t*)v.input;
   uint8_t* out = (uint8_t*)v.output;
   uint8_t* scr = (uint8_t*)v.scratch;
@@ -82,72 +84,79 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
     }
     const uint32_t nUnits = (uint32_t)((bLen + 15) / 16);
 
-    // ---- reduce-scatter: put my copy of every peer's slice sub-range into that peer's scratch
-    if (nUnits) {
+    if constexpr (MODE != 2) {
+      // ---- reduce-scatter: put my copy of every peer's slice sub-range into that peer's scratch
+      if (nUnits) {
 #pragma unroll 1
-      for (int i = 0; i < nranks - 1; ++i) {
-        // rotate the first peer by block index so concurrent blocks start on different links
-        const int k = (i + (int)b) % (nranks - 1);
-        const int q = k < rank ? k : k + 1;
-        const uint64_t srcOff = (uint64_t)q * g.slice + bOff;
-        const auto rsrc = make_rsrc(in + srcOff);
-        const uint64_t valid = g.bytes > srcOff ? g.bytes - srcOff : 0;
-        for (uint32_t u0 = tid; u0 < nUnits; u0 += T * U) {
-          u32x4 w[U];
-#pragma unroll
-          for (int k2 = 0; k2 < U; ++k2) {
-            const uint32_t u = u0 + k2 * T;
-            if (u < nUnits) w[k2] = load_payload<kNonTemporal>(rsrc, in + srcOff, (uint64_t)u * 16, clamp_valid(valid, (uint64_t)u * 16, 16));
-          }
-          // remote scratch of peer q: region of source `rank`
+        for (int i = 0; i < nranks - 1; ++i) {
+          // rotate the first peer by block index so concurrent blocks start on different links
+          const int k = (i + (int)b) % (nranks - 1);
+          const int q = k < rank ? k : k + 1;
+          const uint64_t srcOff = (uint64_t)q * g.slice + bOff;
+          const auto rsrc = make_rsrc(in + srcOff);
+          const uint64_t valid = g.bytes > srcOff ? g.bytes - srcOff : 0;
           const auto rq = make_rsrc((uint8_t*)v.peerScratch[q] + (uint64_t)rank * g.pass + (bOff - pOff));
+          for (uint32_t u0 = tid; u0 < nUnits; u0 += T * U) {
+            u32x4 w[U];
 #pragma unroll
-          for (int k2 = 0; k2 < U; ++k2) {
-            const uint32_t u = u0 + k2 * T;
-            if (u < nUnits) store16<kSystem>(rq, u * 16u, w[k2]);
+            for (int k2 = 0; k2 < U; ++k2) {
+              const uint32_t u = u0 + k2 * T;
+              if (u < nUnits)
+                w[k2] = load_payload<kNonTemporal>(rsrc, in + srcOff, (uint64_t)u * 16, clamp_valid(valid, (uint64_t)u * 16, 16));
+            }
+#pragma unroll
+            for (int k2 = 0; k2 < U; ++k2) {
+              const uint32_t u = u0 + k2 * T;
+              if (u < nUnits) store16<kSystem>(rq, u * 16u, w[k2]);
+            }
           }
         }
       }
+      block_handshake(v, nranks, rank, b, budget);
     }
-    block_handshake(v, nranks, rank, b, budget);
 
-    // ---- reduce my slice sub-range; write it locally and into every peer's output (all-gather)
+    // ---- my slice sub-range: reduce (AR, RS), write locally, and (AR, AG) into every peer's output
     if (nUnits) {
       const uint64_t myOff = (uint64_t)rank * g.slice + bOff;
-      const uint64_t valid = g.bytes > myOff ? g.bytes - myOff : 0;
-      const auto rin = make_rsrc(in + myOff);
-      const auto rout = make_rsrc(out + myOff);
+      const uint8_t* myIn = MODE == 2 ? in + bOff : in + myOff;
+      uint8_t* myOut = MODE == 1 ? out + bOff : out + myOff;
+      const uint64_t valid = MODE == 2 ? g.slice - bOff : (g.bytes > myOff ? g.bytes - myOff : 0);
+      const auto rin = make_rsrc(myIn);
+      const auto rout = make_rsrc(myOut);
       const auto rscr = make_rsrc(scr + (bOff - pOff));
       for (uint32_t u = tid; u < nUnits; u += T) {
         const uint32_t vb = clamp_valid(valid, (uint64_t)u * 16, 16);
-        u32x4 acc = load_payload<kNonTemporal>(rin, in + myOff, (uint64_t)u * 16, vb);
-        u32x4 w[kMaxRanks];
+        u32x4 acc = load_payload<kNonTemporal>(rin, myIn, (uint64_t)u * 16, vb);
+        if constexpr (MODE != 2) {
+          u32x4 w[kMaxRanks];
 #pragma unroll
-        for (int k = 1; k < kMaxRanks; ++k) {
-          if (k < nranks) {
-            const int src = ORDER == 0 ? (k - 1 < rank ? k - 1 : k) : (rank + k) % nranks;
-            w[k] = load16<kSystem>(rscr, (uint32_t)((uint64_t)src * g.pass) + u * 16u);
+          for (int k = 1; k < kMaxRanks; ++k) {
+            if (k < nranks) {
+              const int src = ORDER == 0 ? (k - 1 < rank ? k - 1 : k) : (rank + k) % nranks;
+              w[k] = load16<kSystem>(rscr, (uint32_t)((uint64_t)src * g.pass) + u * 16u);
+            }
           }
-        }
 #pragma unroll
-        for (int k = 1; k < kMaxRanks; ++k)
-          if (k < nranks) acc = reduce4<DT, OP>(acc, w[k]);
-        store_payload<kPlain>(rout, out + myOff, (uint64_t)u * 16, acc, vb);
+          for (int k = 1; k < kMaxRanks; ++k)
+            if (k < nranks) acc = reduce4<DT, OP>(acc, w[k]);
+        }
+        store_payload<kPlain>(rout, myOut, (uint64_t)u * 16, acc, vb);
+        if constexpr (MODE != 1) {
 #pragma unroll 1
-        for (int i = 0; i < nranks - 1; ++i) {
-          const int k = (i + (int)b) % (nranks - 1);
-          const int q = k < rank ? k : k + 1;
-          uint8_t* po = (uint8_t*)v.peerOutput[q] + myOff;
-          if (vb >= 16)
-            store16<kSystem>(make_rsrc(po), u * 16u, acc);
-          else
-            store_tail(po + (uint64_t)u * 16, acc, vb);
+          for (int i = 0; i < nranks - 1; ++i) {
+            const int k = (i + (int)b) % (nranks - 1);
+            const int q = k < rank ? k : k + 1;
+            uint8_t* po = (uint8_t*)v.peerOutput[q] + myOff;
+            if (vb >= 16)
+              store16<kSystem>(make_rsrc(po), u * 16u, acc);
+            else
+              store_tail(po + (uint64_t)u * 16, acc, vb);
+          }
         }
       }
     }
     block_handshake(v, nranks, rank, b, budget);
   }
-  (void)G;
 }
 
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks) {
@@ -169,41 +178,60 @@ size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom
 
 template <int DT, int OP, int NV, int ORDER>
 static void launchBulkT(const Views<NV>& vw, int nviews, const BulkGeom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
-                        hipStream_t s) {
-  hipLaunchKernelGGL((allreduceBulkKernel<DT, OP, NV, ORDER>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks,
-                     budget);
+                        hipStream_t s, int mode) {
+  if (mode == 0)
+    hipLaunchKernelGGL((allreduceBulkKernel<DT, OP, NV, ORDER, 0>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g,
+                       nranks, budget);
+  else if (mode == 1)
+    hipLaunchKernelGGL((allreduceBulkKernel<DT, OP, NV, ORDER, 1>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g,
+                       nranks, budget);
+  else if constexpr (ORDER == 0 && OP == kSum && (DT == kF16 || DT == kF32))
+    // AllGather moves bytes only: one instantiation per element width is enough
+    hipLaunchKernelGGL((allreduceBulkKernel<DT, OP, NV, ORDER, 2>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g,
+                       nranks, budget);
 }
 
 template <int DT, int OP>
 static void launchBulk(const mscclppAmdRankView* views, int nviews, const BulkGeom& g, int nranks, int nblocks,
-                       int nthreads, uint64_t budget, hipStream_t s, int order) {
+                       int nthreads, uint64_t budget, hipStream_t s, int order, int mode) {
   if (nviews == 1) {
     Views<1> vw;
     vw.v[0] = views[0];
     if (order == 0)
-      launchBulkT<DT, OP, 1, 0>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+      launchBulkT<DT, OP, 1, 0>(vw, nviews, g, nranks, nblocks, nthreads, budget, s, mode);
     else
-      launchBulkT<DT, OP, 1, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+      launchBulkT<DT, OP, 1, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s, mode);
   } else {
     Views<kMaxRanks> vw{};
     for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
     if (order == 0)
-      launchBulkT<DT, OP, kMaxRanks, 0>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+      launchBulkT<DT, OP, kMaxRanks, 0>(vw, nviews, g, nranks, nblocks, nthreads, budget, s, mode);
     else
-      launchBulkT<DT, OP, kMaxRanks, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+      launchBulkT<DT, OP, kMaxRanks, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s, mode);
   }
+}
+
+// mode 0 AllReduce (bytes = whole buffer), 1 ReduceScatter / 2 AllGather (bytes = n * block, block % 16 == 0)
+int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes,
+                         int dtype, int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s) {
+  if (nblocks <= 0) nblocks = 64;
+  if (nthreads <= 0) nthreads = 512;
+  if (nblocks > kMaxChannels || nthreads > 512 || nthreads % 64 || nthreads < 64) return 4;
+  if (mode != 0 && (bytes % ((size_t)16 * nranks))) return 5;
+  BulkGeom g{};
+  if (!bulkScratchRequired(nranks, bytes, views[0].scratchBytes, &g, nblocks)) return 5;
+  const int order = (algo == MSCCLPP_AMD_ALGO_RSAG && mode != 2) ? 1 : 0;
+  if (mode == 2) {  // byte movement only: map to the f16 or f32 instantiation by element width
+    dtype = (dtype == kF16 || dtype == kBF16) ? kF16 : kF32;
+    op = kSum;
+  }
+  MSCCLPP_AMD_DISPATCH(dtype, op, launchBulk, views, nviews, g, nranks, nblocks, nthreads, budget, s, order, mode);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
 int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
                         int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s) {
-  if (nblocks <= 0) nblocks = 64;
-  if (nthreads <= 0) nthreads = 512;
-  if (nblocks > kMaxChannels || nthreads > 512 || nthreads % 64 || nthreads < 64) return 4;
-  BulkGeom g{};
-  if (!bulkScratchRequired(nranks, bytes, views[0].scratchBytes, &g, nblocks)) return 5;
-  const int order = algo == MSCCLPP_AMD_ALGO_RSAG ? 1 : 0;
-  MSCCLPP_AMD_DISPATCH(dtype, op, launchBulk, views, nviews, g, nranks, nblocks, nthreads, budget, s, order);
-  return hipGetLastError() == hipSuccess ? 0 : 1;
+  return launchCollectiveBulk(0, algo, views, nviews, nranks, bytes, dtype, op, nblocks, nthreads, budget, s);
 }
 
 }  // namespace mscclpp_amd

@@ -156,3 +156,32 @@ def test_int32_kat(built):
         assert ranks.errors() == [0] * n
         for o in outs:
             assert torch.all(o == n * (n - 1) // 2)
+
+
+@pytest.mark.parametrize("n,dt,block", [(2, O.F16, 4096), (8, O.F16, 65536), (8, O.F32, 12288), (4, O.BF16, 2048),
+                                        (8, O.I32, 1024)])
+def test_reduce_scatter_and_all_gather(built, n, dt, block):
+    """ncclReduceScatter / ncclAllGather halves of the bulk path (nccl.cc:662-772), in-process ranks."""
+    import mscclpp_amd as m
+
+    item = ITEM[dt]
+    count = block * n
+    ranks = m.InProcessRanks(n, 1 << 16, bulk_scratch_bytes=max(count * item, 1 << 20))
+    for call in range(2):
+        ins = _inputs(dt, n, count, seq=call)
+        dins = [_dev(a, dt) for a in ins]
+        douts = [torch.zeros(block, dtype=TORCH[dt], device="cuda") for _ in range(n)]
+        ranks.collective(1, dins, douts)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        nw = count * item // 4
+        exp = O.allreduce_sliced(dt, O.SUM, [a.view(np.uint32) for a in ins], nw, nw // n, 0)[0]
+        for r in range(n):
+            _cmp(_bytes(douts[r]), exp.view(np.uint8)[r * block * item:(r + 1) * block * item], dt)
+        # all-gather of the reduced blocks reconstructs the AllReduce result on every rank
+        gathered = [torch.zeros(count, dtype=TORCH[dt], device="cuda") for _ in range(n)]
+        ranks.collective(2, douts, gathered)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        for r in range(n):
+            _cmp(_bytes(gathered[r]), exp.view(np.uint8)[: count * item], dt)

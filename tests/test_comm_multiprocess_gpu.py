@@ -59,6 +59,20 @@ def _worker(rank, n, uid, q):
                 e = O.allreduce_sliced(dt, O.SUM, pad, nw, sl // 4, 1 if sel == "rsag" else 0)[rank].view(np.uint8)[:nbytes]
             got = out.cpu().contiguous().view(torch.uint8).numpy()
             results.append((algo, dt, count, errc, int(np.count_nonzero(got != e))))
+        # ncclReduceScatter + ncclAllGather reconstruct the AllReduce (fp32, block 8192)
+        block = 8192
+        ins = [O.lcg(2, block * n, r, 9) for r in range(n)]
+        x = torch.from_numpy(ins[rank].view(np.int32).copy()).view(torch.float32).cuda()
+        rs = torch.zeros(block, dtype=torch.float32, device="cuda")
+        ag = torch.zeros(block * n, dtype=torch.float32, device="cuda")
+        for _ in range(2):
+            comm.reduce_scatter(x, rs)
+            comm.all_gather(rs, ag)
+        torch.cuda.synchronize()
+        nw = block * n
+        e = O.allreduce_sliced(2, O.SUM, [a.view(np.uint32) for a in ins], nw, block, 0)[0]
+        got = ag.cpu().numpy().view(np.uint32)
+        results.append(("rs+ag", 2, nw, comm.device_error(), int(np.count_nonzero(got != e))))
         comm.barrier()
         comm.destroy()
         q.put((rank, results, None))
