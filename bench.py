@@ -191,6 +191,17 @@ def bench_single(args):
                      "algorithmic_bytes_per_launch": 7 * S},
     }
     res["staged_pcie_inclusive"] = staged_rate(m, S, x, y, out, pk, flags, err)
+    # BASELINE configs[1] sweep, 64 KiB .. 48 MiB: per-launch time with 20 launches captured in one
+    # HIP graph (device time, not host launch rate)
+    sweep = {}
+    for sz in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 48 << 20):
+        if sz > S:
+            break
+        xs, ys, os_ = x[: sz // 2], y[: sz // 2], out[: sz // 2]
+        us = graph_time_per_call(lambda: m.self_reduce_ll16(xs, ys, pk.ptr, os_, flags, err)) * 1e6
+        sweep[f"{sz >> 10}KiB"] = {"kernel_us": round(us, 2), "algbw_GBs": round(sz / us / 1e3, 1),
+                                   "hbm_7S_TBs": round(7 * sz / us / 1e6, 3)}
+    res["sweep"] = sweep
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_self_reduce(S, args.cpu_seconds)
         res["host_proxy_baseline"] = hp
@@ -322,6 +333,24 @@ def bench_multi(args):
     return res if rank == 0 else None
 
 
+def graph_time_per_call(fn, calls=20, replays=10):
+    """Per-call time with `calls` calls captured in one HIP graph (mscclpp-test common.cc:202-227)."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(calls):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    return _time_calls(g.replay, replays) / calls
+
+
 def bench_extras(args, comm, n, dev, tmax):
     """BASELINE configs[3] (LL latency sweep, fp16 1 KiB..1 MiB) and configs[4] (fp32 1 GiB
     RS+AG in ring order), timed the same way; failures are recorded, not raised."""
@@ -336,6 +365,16 @@ def bench_extras(args, comm, n, dev, tmax):
                 comm.all_reduce(xs, os_)
             lat[f"{kb}KiB"] = round(tmax(_time_calls(lambda: comm.all_reduce(xs, os_), 50)) * 1e6, 2)
         extras["ll_latency_us"] = lat
+    except Exception as e:
+        extras["ll_latency_error"] = str(e)
+    try:
+        glat = {}
+        for kb in (1, 4, 16, 64, 256, 1024):
+            cnt = kb * 512
+            xs = torch.rand(cnt, device=dev).half()
+            os_ = torch.empty_like(xs)
+            glat[f"{kb}KiB"] = round(tmax(graph_time_per_call(lambda: comm.all_reduce(xs, os_))) * 1e6, 2)
+        extras["ll_latency_graph_us"] = glat
     except Exception as e:
         extras["ll_latency_error"] = str(e)
     try:
