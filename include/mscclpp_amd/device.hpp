@@ -92,6 +92,19 @@ __device__ __forceinline__ void report_error(uint32_t* err, uint32_t code) {
   }
 }
 
+// As report_error; the first reporter also records three diagnostic words in err[1..3] (the error
+// word must then point at >= 16 bytes).
+__device__ __forceinline__ void report_error_detail(uint32_t* err, uint32_t code, uint32_t a, uint32_t b, uint32_t c) {
+  if (!err) return;
+  uint32_t expected = kErrNone;
+  if (__hip_atomic_compare_exchange_strong(err, &expected, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM)) {
+    err[1] = a;
+    err[2] = b;
+    err[3] = c;
+  }
+}
+
 // Relaxed system-scope 64-bit load / store / add (global_* sc0 sc1), used for tokens and flags.
 __device__ __forceinline__ uint64_t ld_relaxed_sys(const uint64_t* p) {
   return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -83,7 +83,9 @@ int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblocks, void* 
 /* ---- explicit-view AllReduce ------------------------------------------------------------- */
 /* Launch `algo` for `nviews` ranks of an `nranks`-rank AllReduce in ONE kernel launch (views[i]
  * is handled by blockIdx.y == i).  nviews == 1 is the one-rank-per-process form; nviews ==
- * nranks runs every rank of the collective inside this process. */
+ * nranks runs every rank of the collective inside this process.  Every workgroup waits on other
+ * ranks' workgroups, so nblocks * nviews workgroups must be resident at once; a grid that is not
+ * returns ncclInvalidUsage (5) without launching. */
 int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes,
                               int dtype, int op, int nblocks, int nthreads, uint64_t budgetTicks, void* stream);
 /* coll 0 AllReduce (bytes = buffer), 1 ReduceScatter / 2 AllGather (bytes = nranks * block, block %

@@ -228,6 +228,9 @@ class InProcessRanks:
     def errors(self):
         return [int(e[0].item()) for e in self.err]
 
+    def error_details(self):
+        return [[int(v) for v in e[:4].tolist()] for e in self.err]
+
     def scratch_tensor(self, r, nbytes=None, bulk=False):
         """Zero-copy uint8 view of rank r's scratch (for packet-image checks)."""
         buf = (self.bulk if bulk else self.scratch)[r]

@@ -45,13 +45,16 @@ __device__ __forceinline__ void block_handshake(const mscclppAmdRankView& v, int
     add_release_sys(remote, 1);
     uint64_t* mine = v.tokens + (uint64_t)p * kMaxChannels + ch;
     uint64_t* exp = v.expected + (uint64_t)p * kMaxChannels + ch;
-    const uint64_t want = *exp + 1;
-    *exp = want;
+    // the counter lives in ordinary device memory and is touched once per handshake: agent-scope
+    // atomics keep it out of any XCD's stale L2 line whichever XCD this block lands on next launch
+    const uint64_t want = __hip_atomic_fetch_add(exp, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
     SpinGuard g(budget);
     while (ld_relaxed_sys(mine) < want) {
       __builtin_amdgcn_s_sleep(2);
       if (g.expired()) {
-        report_error(v.err, kErrSemaphoreTimeout);
+        // detail: channel | peer << 16, rank, tokens seen (low 16 bits) | wanted (low 16 bits) << 16
+        report_error_detail(v.err, kErrSemaphoreTimeout, ch | ((uint32_t)p << 16), (uint32_t)rank,
+                            ((uint32_t)ld_relaxed_sys(mine) & 0xffffu) | ((uint32_t)want << 16));
         break;
       }
     }
@@ -71,7 +74,7 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
   const uint8_t* in = (const uint8_t*)v.input;
   uint8_t* out = (uint8_t*)v.output;
   uint8_t* scr = (uint8_t*)v.scratch;
-  constexpr int U = 2;  // units per lane per step
+  constexpr int U = 8;  // units per lane per step (128 B in flight per lane in the put phase)
 
   for (uint32_t ps = 0; ps < g.npasses; ++ps) {
     const uint64_t pOff = (uint64_t)ps * g.pass;          // offset inside a slice
@@ -159,6 +162,8 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
   }
 }
 
+static thread_local int g_launch_status = 0;
+
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks) {
   BulkGeom g{};
   g.bytes = bytes;
@@ -179,6 +184,10 @@ size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom
 template <int DT, int OP, int NV, int ORDER>
 static void launchBulkT(const Views<NV>& vw, int nviews, const BulkGeom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
                         hipStream_t s, int mode) {
+  if (!grid_coresident(allreduceBulkKernel<DT, OP, NV, ORDER, 0>, nthreads, (long)nblocks * nviews)) {
+    g_launch_status = 5;  // ncclInvalidUsage: the grid cannot be resident at once: its handshakes would deadlock
+    return;
+  }
   if (mode == 0)
     hipLaunchKernelGGL((allreduceBulkKernel<DT, OP, NV, ORDER, 0>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g,
                        nranks, budget);
@@ -225,7 +234,9 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
     dtype = (dtype == kF16 || dtype == kBF16) ? kF16 : kF32;
     op = kSum;
   }
+  g_launch_status = 0;
   MSCCLPP_AMD_DISPATCH(dtype, op, launchBulk, views, nviews, g, nranks, nblocks, nthreads, budget, s, order, mode);
+  if (g_launch_status) return g_launch_status;
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -284,14 +284,24 @@ size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype) {
   return 2 * half;
 }
 
+static thread_local int g_ll_launch_status = 0;
+
 template <int DT, int OP, int NV>
 static void launchLL16T(const Views<NV>& vw, int nviews, const LL16Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
                         hipStream_t s) {
+  if (!grid_coresident(allreduceLL16Kernel<DT, OP, NV>, nthreads, (long)nblocks * nviews)) {
+    g_ll_launch_status = 5;  // ncclInvalidUsage: the grid cannot be resident at once: its packet waits would deadlock
+    return;
+  }
   hipLaunchKernelGGL((allreduceLL16Kernel<DT, OP, NV>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
 }
 template <int DT, int OP, int NV>
 static void launchLL8T(const Views<NV>& vw, int nviews, const LL8Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
                        hipStream_t s) {
+  if (!grid_coresident(allreduceLL8Kernel<DT, OP, NV>, nthreads, (long)nblocks * nviews)) {
+    g_ll_launch_status = 5;  // ncclInvalidUsage: the grid cannot be resident at once: its packet waits would deadlock
+    return;
+  }
   hipLaunchKernelGGL((allreduceLL8Kernel<DT, OP, NV>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
 }
 
@@ -352,6 +362,7 @@ static void ll8Defaults(int nranks, size_t bytes, int& nblocks, int& nthreads) {
 
 int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
                       int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s) {
+  g_ll_launch_status = 0;
   if (algo == MSCCLPP_AMD_ALGO_PACKET) {
     ll16Defaults(nranks, bytes, nblocks, nthreads);
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
@@ -369,6 +380,7 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
       if (views[i].scratchBytes < ll8ScratchRequired(nranks, bytes, dtype)) return 5;
     MSCCLPP_AMD_DISPATCH(dtype, op, launchLL8, views, nviews, g, nranks, nblocks, nthreads, budget, s);
   }
+  if (g_ll_launch_status) return g_ll_launch_status;
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -19,6 +19,29 @@ constexpr int kFlagSlots = MSCCLPP_AMD_FLAG_SLOTS;
 constexpr int kMaxRanks = MSCCLPP_AMD_MAX_RANKS;
 constexpr int kMaxChannels = MSCCLPP_AMD_MAX_CHANNELS;
 
+// Every workgroup of a collective kernel spins on workgroups of other ranks (and, with in-process
+// ranks, of the same launch), so the whole grid must be resident at once.  Host side: true when
+// `blocks` workgroups of `kernel` at `threads` lanes fit on the current device together.
+// The answer is cached per kernel instantiation, device and block size (launches stay cheap).
+template <typename Kernel>
+inline bool grid_coresident(Kernel kernel, int threads, long blocks) {
+  static thread_local Kernel cKernel = nullptr;
+  static thread_local int cDev = -1, cThreads = -1;
+  static thread_local long cCap = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (kernel != cKernel || dev != cDev || threads != cThreads) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess) return false;
+    cKernel = kernel;
+    cDev = dev;
+    cThreads = threads;
+    cCap = (long)per * cus;
+  }
+  return cCap >= blocks;
+}
+
 __device__ __forceinline__ void bump_flags(uint32_t* flags, uint32_t flag) {
   __syncthreads();
   if (threadIdx.x == 0) flags[blockIdx.x] = flag + 1;

@@ -171,9 +171,12 @@ def test_reduce_scatter_and_all_gather(built, n, dt, block):
         ins = _inputs(dt, n, count, seq=call)
         dins = [_dev(a, dt) for a in ins]
         douts = [torch.zeros(block, dtype=TORCH[dt], device="cuda") for _ in range(n)]
+        torch.cuda.synchronize()
+        pre = [int(e.abs().max().item()) for e in ranks.expected]
         ranks.collective(1, dins, douts)
         torch.cuda.synchronize()
-        assert ranks.errors() == [0] * n
+        assert ranks.errors() == [0] * n, ("reduce-scatter", call, pre, ranks.error_details(),
+                                           [int(e.abs().max().item()) for e in ranks.expected])
         nw = count * item // 4
         exp = O.allreduce_sliced(dt, O.SUM, [a.view(np.uint32) for a in ins], nw, nw // n, 0)[0]
         for r in range(n):
@@ -182,6 +185,6 @@ def test_reduce_scatter_and_all_gather(built, n, dt, block):
         gathered = [torch.zeros(count, dtype=TORCH[dt], device="cuda") for _ in range(n)]
         ranks.collective(2, douts, gathered)
         torch.cuda.synchronize()
-        assert ranks.errors() == [0] * n
+        assert ranks.errors() == [0] * n, ("all-gather", call, ranks.error_details())
         for r in range(n):
             _cmp(_bytes(gathered[r]), exp.view(np.uint8)[: count * item], dt)
