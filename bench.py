@@ -324,7 +324,7 @@ def bench_multi(args):
     }
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
     if not args.no_extras:
-        res["extras"] = bench_extras(args, comm, n, dev, tmax)
+        res["extras"] = bench_extras(args, comm, n, dev, tmax, dist.barrier)
     if rank == 0 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_allreduce(S, n, args.cpu_seconds)
     comm.destroy()
@@ -333,8 +333,10 @@ def bench_multi(args):
     return res if rank == 0 else None
 
 
-def graph_time_per_call(fn, calls=20, replays=10):
-    """Per-call time with `calls` calls captured in one HIP graph (mscclpp-test common.cc:202-227)."""
+def graph_time_per_call(fn, calls=20, replays=10, sync=None):
+    """Per-call time with `calls` calls captured in one HIP graph (mscclpp-test common.cc:202-227).
+    `sync` (a host barrier across ranks) lines the ranks up before the timed replays, so the first
+    replay does not absorb another rank's late start."""
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -348,10 +350,12 @@ def graph_time_per_call(fn, calls=20, replays=10):
             fn()
     g.replay()
     torch.cuda.synchronize()
+    if sync is not None:
+        sync()
     return _time_calls(g.replay, replays) / calls
 
 
-def bench_extras(args, comm, n, dev, tmax):
+def bench_extras(args, comm, n, dev, tmax, barrier):
     """BASELINE configs[3] (LL latency sweep, fp16 1 KiB..1 MiB) and configs[4] (fp32 1 GiB
     RS+AG in ring order), timed the same way; failures are recorded, not raised."""
     extras = {}
@@ -363,6 +367,8 @@ def bench_extras(args, comm, n, dev, tmax):
             os_ = torch.empty_like(xs)
             for _ in range(5):
                 comm.all_reduce(xs, os_)
+            torch.cuda.synchronize()
+            barrier()
             lat[f"{kb}KiB"] = round(tmax(_time_calls(lambda: comm.all_reduce(xs, os_), 50)) * 1e6, 2)
         extras["ll_latency_us"] = lat
     except Exception as e:
@@ -373,7 +379,7 @@ def bench_extras(args, comm, n, dev, tmax):
             cnt = kb * 512
             xs = torch.rand(cnt, device=dev).half()
             os_ = torch.empty_like(xs)
-            glat[f"{kb}KiB"] = round(tmax(graph_time_per_call(lambda: comm.all_reduce(xs, os_))) * 1e6, 2)
+            glat[f"{kb}KiB"] = round(tmax(graph_time_per_call(lambda: comm.all_reduce(xs, os_), sync=barrier)) * 1e6, 2)
         extras["ll_latency_graph_us"] = glat
     except Exception as e:
         extras["ll_latency_error"] = str(e)

@@ -2,6 +2,7 @@
 
 Everything is built in-tree so the shared objects travel to the GPU box with the repo snapshot:
     mscclpp_amd/lib/libmscclpp_amd.so   product library (C ABI: include/mscclpp_amd/*.h)
+    mscclpp_amd/lib/libmscclpp_amd_audit.so  LD_AUDIT redirect of librccl/libnccl to the above
     oracle/liboracle.so                 CPU restatement used only by tests / smoke / bench baseline
     oracle/proxy_baseline               host-proxy CPU path (config 1 baseline), see oracle/
 No cmake/ninja: plain hipcc / gcc invocations, parallel, incremental by mtime.
@@ -22,6 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 LIB = os.path.join(LIBDIR, "libmscclpp_amd.so")
 ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+AUDIT_LIB = os.path.join(LIBDIR, "libmscclpp_amd_audit.so")
 
 
 def _headers():
@@ -82,9 +84,18 @@ def build_oracle():
     return ORACLE_LIB
 
 
+def build_audit():
+    src = os.path.join(CSRC, "audit", "audit_nccl.c")
+    os.makedirs(LIBDIR, exist_ok=True)
+    if _newer(AUDIT_LIB, [src]):
+        _run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-fvisibility=hidden", "-o", AUDIT_LIB, src, "-ldl"])
+    return AUDIT_LIB
+
+
 def build_all(verbose=False):
     build_oracle()
     build_library(verbose=verbose)
+    build_audit()
     ref = os.path.join(ROOT, "oracle", "build_ref.sh")
     if os.path.isdir("/root/reference") and os.path.exists(ref):
         # the reference-header harness (oracle/_ref) can only be built where /root/reference exists

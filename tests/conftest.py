@@ -22,4 +22,5 @@ def built():
 
     _build.build_oracle()
     _build.build_library()
+    _build.build_audit()
     return True
