@@ -99,6 +99,15 @@ def lib():
         "mscclppAmdCommScratch": [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)],
         "mscclppAmdCommFlags": [vp, ctypes.POINTER(vp)],
         "mscclppAmdCommAllGatherHost": [vp, vp, vp, sz],
+        "mscclppAmdExecutionPlanCreate": [ctypes.c_char_p, i32, ctypes.POINTER(vp)],
+        "mscclppAmdExecutionPlanDestroy": [vp],
+        "mscclppAmdExecutionPlanIsInPlace": [vp],
+        "mscclppAmdExecutionPlanDescribe": [vp, sz, sz, ctypes.c_char_p, sz, ctypes.POINTER(sz)],
+        "mscclppAmdExecutorCreate": [vp, ctypes.POINTER(vp)],
+        "mscclppAmdExecutorExecute": [vp, i32, vp, vp, sz, sz, i32, vp, vp, i32],
+        "mscclppAmdExecutorReset": [vp],
+        "mscclppAmdExecutorDestroy": [vp],
+        "mscclppAmdExecutorGetDeviceError": [vp, ctypes.POINTER(ctypes.c_uint32), i32],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -106,6 +115,12 @@ def lib():
         f.restype = ctypes.c_int
     L.mscclppAmdScratchRequired.argtypes = [i32, i32, sz, i32]
     L.mscclppAmdScratchRequired.restype = sz
+    for name in ("mscclppAmdExecutionPlanName", "mscclppAmdExecutionPlanCollective"):
+        getattr(L, name).argtypes = [vp]
+        getattr(L, name).restype = ctypes.c_char_p
+    for name in ("mscclppAmdExecutionPlanMinMessageSize", "mscclppAmdExecutionPlanMaxMessageSize"):
+        getattr(L, name).argtypes = [vp]
+        getattr(L, name).restype = sz
     L.ncclGetErrorString.argtypes = [i32]
     L.ncclGetErrorString.restype = ctypes.c_char_p
     _lib = L
@@ -313,3 +328,95 @@ class Communicator:
         if self.comm:
             check(lib().ncclCommDestroy(self.comm), "ncclCommDestroy")
             self.comm = None
+
+
+# ---- execution plans / executor (include/mscclpp_amd/executor.h; reference executor.hpp) ----------
+
+class DataType:
+    """mscclpp.DataType values (gpu_data_types.hpp:169-183)."""
+    int32, uint32, float16, float32, bfloat16 = 0, 1, 2, 3, 4
+
+
+EXEC_DTYPES = {torch.int32: DataType.int32, torch.float16: DataType.float16, torch.float32: DataType.float32,
+               torch.bfloat16: DataType.bfloat16}
+
+
+class PacketType:
+    """mscclpp.PacketType (executor.hpp:15-18)."""
+    LL8, LL16 = 0, 1
+
+
+class ExecutionPlan:
+    """mscclpp.ExecutionPlan(plan_path, rank): a JSON plan resolved for one rank."""
+
+    def __init__(self, plan_path, rank):
+        p = ctypes.c_void_p()
+        check(lib().mscclppAmdExecutionPlanCreate(os.fsencode(plan_path), rank, ctypes.byref(p)),
+              f"ExecutionPlan({plan_path})")
+        self.handle, self.rank, self.path = p, rank, plan_path
+
+    def name(self):
+        return lib().mscclppAmdExecutionPlanName(self.handle).decode()
+
+    def collective(self):
+        return lib().mscclppAmdExecutionPlanCollective(self.handle).decode()
+
+    def min_message_size(self):
+        return lib().mscclppAmdExecutionPlanMinMessageSize(self.handle)
+
+    def max_message_size(self):
+        return lib().mscclppAmdExecutionPlanMaxMessageSize(self.handle)
+
+    def is_in_place(self):
+        return bool(lib().mscclppAmdExecutionPlanIsInPlace(self.handle))
+
+    def describe(self, input_bytes, output_bytes):
+        """The plan lowered for this rank at these message sizes (host only), as a dict."""
+        import json
+
+        need = ctypes.c_size_t()
+        check(lib().mscclppAmdExecutionPlanDescribe(self.handle, input_bytes, output_bytes, None, 0, ctypes.byref(need)),
+              "ExecutionPlan.describe")
+        buf = ctypes.create_string_buffer(need.value)
+        check(lib().mscclppAmdExecutionPlanDescribe(self.handle, input_bytes, output_bytes, buf, need.value,
+                                                    ctypes.byref(need)), "ExecutionPlan.describe")
+        return json.loads(buf.value.decode())
+
+    def __del__(self):
+        try:
+            if self.handle:
+                lib().mscclppAmdExecutionPlanDestroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+class Executor:
+    """mscclpp.Executor(comm): runs execution plans on a Communicator (collective setup)."""
+
+    def __init__(self, comm):
+        e = ctypes.c_void_p()
+        check(lib().mscclppAmdExecutorCreate(comm.comm, ctypes.byref(e)), "Executor")
+        self.handle, self.comm = e, comm
+
+    def execute(self, rank, send_ptr, recv_ptr, send_size, recv_size, dtype, plan, stream=None,
+                packet_type=PacketType.LL16):
+        """Executor::execute (executor.hpp:85-86); pointers are device addresses, dtype a DataType."""
+        sp = stream if isinstance(stream, (int, ctypes.c_void_p)) else stream_ptr(stream)
+        check(lib().mscclppAmdExecutorExecute(self.handle, rank, ctypes.c_void_p(send_ptr), ctypes.c_void_p(recv_ptr),
+                                              send_size, recv_size, dtype, plan.handle,
+                                              sp if isinstance(sp, ctypes.c_void_p) else ctypes.c_void_p(sp),
+                                              packet_type), "Executor.execute")
+
+    def reset(self):
+        check(lib().mscclppAmdExecutorReset(self.handle), "Executor.reset")
+
+    def device_error(self, clear=True):
+        w = (ctypes.c_uint32 * 4)()
+        check(lib().mscclppAmdExecutorGetDeviceError(self.handle, w, 1 if clear else 0), "Executor.device_error")
+        return list(w)
+
+    def destroy(self):
+        if self.handle:
+            check(lib().mscclppAmdExecutorDestroy(self.handle), "Executor.destroy")
+            self.handle = None

@@ -1,0 +1,136 @@
+"""GPU parity of the DSL executor: n processes (one rank each) on cuda:0 run a JSON execution plan
+through mscclppAmdExecutorExecute, call after call; every rank's buffers are compared bit-exactly
+with the CPU oracle's simulation of the same plan on the same inputs (oracle/executor_oracle.py,
+whose integer results are pinned to exact sums by tests/test_executor_plan.py).  Mirrors the
+reference's test_executor (python/test/test_mscclpp.py:657-700): in-place AllReduce of fp16 data,
+here with LCG inputs and bit-exact checks instead of a tolerance."""
+import json
+import multiprocessing as mp
+import os
+import queue
+import sys
+import traceback
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PLANS = os.path.join(ROOT, "tests", "golden", "plans")
+
+# (plan, nranks, dtype name, elements per rank, packet type, calls)
+CASES_2 = [
+    ("allreduce_pkt_n2.json", "f16", 1 << 19, "LL16", 3),
+    ("allreduce_pkt_n2.json", "bf16", 1 << 14, "LL8", 2),
+    ("allreduce_pkt_n2.json", "f32", 4096, "LL16", 2),
+    ("allreduce_rres_n2.json", "f16", 1 << 19, "LL16", 3),
+    ("allreduce_put_n2.json", "f32", 1 << 16, "LL16", 3),
+]
+CASES_4 = [
+    ("allreduce_pkt_n4.json", "f16", 1 << 16, "LL16", 3),
+    ("allreduce_rres_n4.json", "f32", 1 << 15, "LL16", 2),
+    ("allreduce_put_n4.json", "f16", 1 << 14, "LL16", 2),
+]
+DT = {"f16": 0, "bf16": 1, "f32": 2}
+
+
+def _worker(rank, n, uid, cases, q):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "5000")
+        import torch
+
+        import mscclpp_amd as m
+        import oracle_lib as O
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        ex = m.Executor(comm)
+        tdt = {"f16": torch.float16, "bf16": torch.bfloat16, "f32": torch.float32}
+        results = []
+        for ci, (fname, dt, count, pkt, calls) in enumerate(cases):
+            plan = m.ExecutionPlan(os.path.join(PLANS, fname), rank)
+            outs = []
+            for call in range(calls):
+                a = O.lcg(DT[dt], count, rank, 10 * ci + call)
+                x = torch.from_numpy(a.view(np.int16 if dt != "f32" else np.int32).copy()).view(tdt[dt]).cuda()
+                y = x if plan.is_in_place() else torch.zeros_like(x)
+                stream = torch.cuda.current_stream()
+                ex.execute(rank, x.data_ptr(), y.data_ptr(), x.numel() * x.element_size(), y.numel() * y.element_size(),
+                           m.EXEC_DTYPES[tdt[dt]], plan, stream,
+                           m.PacketType.LL16 if pkt == "LL16" else m.PacketType.LL8)
+                torch.cuda.synchronize()
+                outs.append(y.cpu().contiguous().view(torch.uint8).numpy().copy())
+            err = ex.device_error()
+            results.append((fname, dt, outs, err))
+            comm.barrier()
+        ex.destroy()
+        comm.barrier()
+        comm.destroy()
+        q.put((rank, results, None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def _run(n, cases):
+    import mscclpp_amd as m
+
+    uid = m.Communicator.unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, n, uid, cases, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=300)
+            assert err is None, err
+            got[rank] = res
+    except queue.Empty:
+        pytest.fail("executor processes timed out")
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return got
+
+
+def _oracle(n, cases):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import executor_oracle as E
+    import oracle_lib as O
+
+    exp = []
+    for ci, (fname, dt, count, pkt, calls) in enumerate(cases):
+        with open(os.path.join(PLANS, fname)) as f:
+            doc = json.load(f)
+        eo = E.ExecutorOracle(doc, n)
+        per_call = []
+        for call in range(calls):
+            ins = [O.lcg(DT[dt], count, r, 10 * ci + call).view(np.uint8).copy() for r in range(n)]
+            outs = ins if doc["inplace"] else [np.zeros_like(a) for a in ins]
+            res = eo.execute(ins, outs, dt, packet=pkt)
+            per_call.append([res[r][0 if doc["inplace"] else 1].copy() for r in range(n)])
+        exp.append(per_call)
+    return exp
+
+
+def _compare(n, cases, got):
+    exp = _oracle(n, cases)
+    for rank in range(n):
+        for ci, (fname, dt, outs, err) in enumerate(got[rank]):
+            assert err == [0, 0, 0, 0], (rank, fname, dt, err)
+            for call, o in enumerate(outs):
+                e = exp[ci][call][rank]
+                bad = np.nonzero(o != e)[0]
+                assert bad.size == 0, (rank, fname, dt, call, bad.size, bad[:8])
+
+
+def test_executor_two_ranks(built):
+    _compare(2, CASES_2, _run(2, CASES_2))
+
+
+def test_executor_four_ranks(built):
+    _compare(4, CASES_4, _run(4, CASES_4))

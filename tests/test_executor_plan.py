@@ -1,0 +1,150 @@
+"""Execution plans on the CPU: the C++ lowering (mscclppAmdExecutionPlanDescribe) against the
+oracle's independent restatement of execution_plan.cc, for every rank of every plan at several
+message sizes; the oracle's simulated execution against exact integer sums (a known answer); and
+the error paths (unsupported channels / operations, misaligned sizes, missing files)."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PLANS = os.path.join(ROOT, "tests", "golden", "plans")
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import executor_oracle as E  # noqa: E402
+
+GENERATED = sorted(f for f in os.listdir(PLANS) if f.endswith(".json"))
+REF_PLANS = "/root/reference/test/execution-files"
+
+
+def _nranks(doc):
+    return len(doc["gpus"])
+
+
+def _sizes(doc):
+    g = doc["gpus"][0]
+    c = max(g["input_chunks"], g["output_chunks"]) * doc.get("buffer_alignment", 16)
+    return [c, c * 4, c * 1024, c * 1000 + c * 7]
+
+
+def _check_plan(built, path):
+    import mscclpp_amd as m
+
+    with open(path) as f:
+        doc = json.load(f)
+    for rank in range(_nranks(doc)):
+        plan = m.ExecutionPlan(path, rank)
+        assert plan.name() == doc["name"] and plan.collective() == doc["collective"]
+        assert plan.is_in_place() == doc["inplace"]
+        for size in _sizes(doc):
+            got = plan.describe(size, size)
+            exp = E.RankPlan(doc, rank, size, size).describe()
+            assert got == json.loads(json.dumps(exp)), (path, rank, size)
+
+
+@pytest.mark.parametrize("fname", GENERATED)
+def test_lowering_matches_oracle(built, fname):
+    _check_plan(built, os.path.join(PLANS, fname))
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_PLANS), reason="reference plans only exist in the build container")
+@pytest.mark.parametrize("fname", ["allreduce_packet.json", "allreduce.json"])
+def test_lowering_of_reference_plans(built, fname):
+    """The reference's own plan files, read where they lie (never copied into this repo)."""
+    _check_plan(built, os.path.join(REF_PLANS, fname))
+
+
+@pytest.mark.parametrize("fname", GENERATED)
+@pytest.mark.parametrize("dtype", ["i32", "u32"])
+def test_oracle_known_answer(fname, dtype):
+    """Integer sums are exact whatever the order: every rank must end with the plain sum."""
+    with open(os.path.join(PLANS, fname)) as f:
+        doc = json.load(f)
+    n = _nranks(doc)
+    eo = E.ExecutorOracle(doc, n)
+    nbytes = _sizes(doc)[1] * 8
+    rng = np.random.default_rng(5)
+    npdt = np.int32 if dtype == "i32" else np.uint32
+    for _ in range(3):
+        ins = [rng.integers(0, 1 << 20, nbytes // 4).astype(npdt).view(np.uint8).copy() for _ in range(n)]
+        exp = sum(a.view(npdt).astype(np.int64) for a in ins).astype(npdt)
+        outs = ins if doc["inplace"] else [np.zeros_like(a) for a in ins]
+        res = eo.execute(ins, outs, dtype)
+        for r in range(n):
+            got = res[r][0 if doc["inplace"] else 1].view(npdt)
+            assert np.array_equal(got, exp)
+
+
+def test_oracle_flag_and_double_scratch():
+    """Consecutive calls alternate scratch halves (flag parity) and carry flag = call number."""
+    with open(os.path.join(PLANS, "allreduce_pkt_n2.json")) as f:
+        doc = json.load(f)
+    eo = E.ExecutorOracle(doc, 2)
+    ins = [np.arange(1024, dtype=np.int32).view(np.uint8).copy() for _ in range(2)]
+    res1 = eo.execute([a.copy() for a in ins], [a.copy() for a in ins], "i32")
+    half = res1[0][2].size // 2
+    flags1 = res1[0][2][:half].view(np.uint32).reshape(-1, 4)[:, 1]
+    assert set(np.unique(flags1)) <= {0, 1} and 1 in flags1
+    res2 = eo.execute([a.copy() for a in ins], [a.copy() for a in ins], "i32")
+    flags2 = res2[0][2][half:].view(np.uint32).reshape(-1, 4)[:, 1]
+    assert 2 in flags2
+
+
+def _write(tmp_path, doc, name="p.json"):
+    p = tmp_path / name
+    p.write_text(json.dumps(doc))
+    return str(p)
+
+
+def test_rejects_port_and_switch_channels(built, tmp_path):
+    import mscclpp_amd as m
+
+    with open(os.path.join(PLANS, "allreduce_rres_n2.json")) as f:
+        doc = json.load(f)
+    doc["gpus"][0]["channels"][0]["channel_type"] = "port"
+    plan = m.ExecutionPlan(_write(tmp_path, doc), 0)
+    with pytest.raises(m.MscclppError):
+        plan.describe(4096, 4096)
+    doc["gpus"][0]["channels"][0]["channel_type"] = "switch"
+    plan = m.ExecutionPlan(_write(tmp_path, doc, "q.json"), 0)
+    with pytest.raises(m.MscclppError):
+        plan.describe(4096, 4096)
+
+
+def test_rejects_multimem_ops(built, tmp_path):
+    import mscclpp_amd as m
+
+    with open(os.path.join(PLANS, "allreduce_rres_n2.json")) as f:
+        doc = json.load(f)
+    doc["gpus"][0]["threadblocks"][0]["ops"][3]["name"] = "glres"
+    plan = m.ExecutionPlan(_write(tmp_path, doc), 0)
+    with pytest.raises(m.MscclppError):
+        plan.describe(4096, 4096)
+
+
+def test_rejects_misaligned_and_out_of_range(built, tmp_path):
+    import mscclpp_amd as m
+
+    with open(os.path.join(PLANS, "allreduce_pkt_n2.json")) as f:
+        doc = json.load(f)
+    path = _write(tmp_path, doc)
+    plan = m.ExecutionPlan(path, 0)
+    with pytest.raises(m.MscclppError):
+        plan.describe(1000, 1000)  # not a multiple of alignment * chunks
+    doc["max_message_size"] = 4096
+    plan = m.ExecutionPlan(_write(tmp_path, doc, "small.json"), 0)
+    plan.describe(4096, 4096)
+    with pytest.raises(m.MscclppError):
+        plan.describe(8192, 8192)
+
+
+def test_missing_or_malformed_file(built, tmp_path):
+    import mscclpp_amd as m
+
+    with pytest.raises(m.MscclppError):
+        m.ExecutionPlan(str(tmp_path / "nope.json"), 0)
+    bad = tmp_path / "bad.json"
+    bad.write_text("{\"name\": \"x\", ")
+    with pytest.raises(m.MscclppError):
+        m.ExecutionPlan(str(bad), 0)
