@@ -190,6 +190,9 @@ def bench_single(args):
                      "kernel": "selfReduceLL16PmKernel", "kernel_us": round(kern_ms * 1e3, 2),
                      "algorithmic_bytes_per_launch": 7 * S},
     }
+    if args.no_extras:  # profiling runs: only the headline launches, so per-kernel stats are of one size
+        pk.free()
+        return res
     res["staged_pcie_inclusive"] = staged_rate(m, S, x, y, out, pk, flags, err)
     # BASELINE configs[1] sweep, 64 KiB .. 48 MiB: per-launch time with 20 launches captured in one
     # HIP graph (device time, not host launch rate)

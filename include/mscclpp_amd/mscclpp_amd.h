@@ -32,6 +32,19 @@ extern "C" {
 
 /* dtype / op codes of the extension API (ncclDataType_t / ncclRedOp_t are mapped onto these) */
 enum { MSCCLPP_AMD_F16 = 0, MSCCLPP_AMD_BF16 = 1, MSCCLPP_AMD_F32 = 2, MSCCLPP_AMD_I32 = 3, MSCCLPP_AMD_U32 = 4 };
+/* OCP FP8 (gfx950 hardware formats; the reference's DataType::FLOAT8_E4M3FN / FLOAT8_E5M2,
+ * gpu_data_types.hpp:170-183).  The code also names the accumulation type of
+ * Algorithm::execute(..., accumDtype) (algorithm.hpp:108-113, common.hpp:89-100): the element
+ * type itself (AUTO), half or float. */
+enum {
+  MSCCLPP_AMD_E4M3 = 5,
+  MSCCLPP_AMD_E5M2 = 6,
+  MSCCLPP_AMD_E4M3_ACC_F16 = 7,
+  MSCCLPP_AMD_E5M2_ACC_F16 = 8,
+  MSCCLPP_AMD_E4M3_ACC_F32 = 9,
+  MSCCLPP_AMD_E5M2_ACC_F32 = 10,
+  MSCCLPP_AMD_NUM_DTYPES = 11
+};
 enum { MSCCLPP_AMD_SUM = 0, MSCCLPP_AMD_MIN = 1 };
 
 /* AllReduce algorithms (names follow the reference's AlgorithmCollection keys) */
@@ -101,6 +114,12 @@ int mscclppAmdSelectAlgo(int nranks, size_t bytes, int dtype);
 /* ---- communicator extensions -------------------------------------------------------------- */
 int mscclppAmdCommAllReduce(ncclComm_t comm, const void* sendbuff, void* recvbuff, size_t count, int ncclDtype,
                             int ncclOp, int algo, int nblocks, int nthreads, void* stream);
+/* As above with the accumulation type of Algorithm::execute (accumNcclDtype: -1 = AUTO, i.e. the
+ * element type; ncclFloat16 / ncclFloat32 for FP8 buffers). */
+int mscclppAmdCommAllReduceAccum(ncclComm_t comm, const void* sendbuff, void* recvbuff, size_t count, int ncclDtype,
+                                 int ncclOp, int accumNcclDtype, int algo, int nblocks, int nthreads, void* stream);
+/* Reduce-type code (MSCCLPP_AMD_*) for an ncclDataType_t and accumulation type (-1 = AUTO), or -1. */
+int mscclppAmdReduceType(int ncclDtype, int accumNcclDtype);
 int mscclppAmdCommBarrier(ncclComm_t comm);
 int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear);
 int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes);

@@ -17,6 +17,8 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmscclpp_amd.so")
 
 # dtype / op / algorithm codes (include/mscclpp_amd/mscclpp_amd.h)
 F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
+# OCP fp8 reduce types: element type x accumulation type (Algorithm::execute accumDtype)
+E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32 = 5, 6, 7, 8, 9, 10
 SUM, MIN = 0, 1
 ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG = 0, 1, 2, 3, 4
 ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4}
@@ -25,9 +27,21 @@ FLAG_SLOTS = 1024
 MAX_CHANNELS = 128
 
 # ncclDataType_t / ncclRedOp_t (include/mscclpp_amd/nccl.h, values of the reference nccl.h:217-253)
-NCCL_DTYPES = {torch.float16: 6, torch.bfloat16: 9, torch.float32: 7, torch.int32: 2}
+NCCL_DTYPES = {torch.float16: 6, torch.bfloat16: 9, torch.float32: 7, torch.int32: 2,
+               torch.float8_e4m3fn: 10, torch.float8_e5m2: 11}
 NCCL_OPS = {"sum": 0, "min": 3}
-DTYPE_CODES = {torch.float16: F16, torch.bfloat16: BF16, torch.float32: F32, torch.int32: I32}
+DTYPE_CODES = {torch.float16: F16, torch.bfloat16: BF16, torch.float32: F32, torch.int32: I32,
+               torch.float8_e4m3fn: E4M3, torch.float8_e5m2: E5M2}
+# accumulation dtype (ncclDataType_t) -> reduce-type code, for fp8 buffers
+ACCUM_CODES = {(torch.float8_e4m3fn, torch.float16): E4M3_ACC_F16, (torch.float8_e5m2, torch.float16): E5M2_ACC_F16,
+               (torch.float8_e4m3fn, torch.float32): E4M3_ACC_F32, (torch.float8_e5m2, torch.float32): E5M2_ACC_F32}
+
+
+def reduce_code(dtype, accum=None):
+    """Reduce-type code of a buffer dtype accumulated in `accum` (None: the element type)."""
+    if accum is None or accum == dtype:
+        return DTYPE_CODES[dtype]
+    return ACCUM_CODES[(dtype, accum)]
 
 ERRORS = {0: "ncclSuccess", 1: "ncclUnhandledCudaError", 2: "ncclSystemError", 3: "ncclInternalError",
           4: "ncclInvalidArgument", 5: "ncclInvalidUsage", 6: "ncclRemoteError", 7: "ncclInProgress"}
@@ -94,6 +108,8 @@ def lib():
         "ncclCommGetAsyncError": [vp, ctypes.POINTER(i32)],
         "ncclGetVersion": [ctypes.POINTER(i32)],
         "mscclppAmdCommAllReduce": [vp, vp, vp, sz, i32, i32, i32, i32, i32, vp],
+        "mscclppAmdCommAllReduceAccum": [vp, vp, vp, sz, i32, i32, i32, i32, i32, i32, vp],
+        "mscclppAmdReduceType": [i32, i32],
         "mscclppAmdCommBarrier": [vp],
         "mscclppAmdCommGetDeviceError": [vp, ctypes.POINTER(ctypes.c_uint32), i32],
         "mscclppAmdCommScratch": [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)],
@@ -163,13 +179,13 @@ def flags_init(flags_tensor, stream=None):
     check(lib().mscclppAmdFlagsInit(ctypes.c_void_p(flags_tensor.data_ptr()), stream_ptr(stream)), "flags init")
 
 
-def self_reduce_ll16(x, y, pkts_ptr, out, flags, err, op=SUM, nblocks=0, budget_ticks=0, stream=None):
+def self_reduce_ll16(x, y, pkts_ptr, out, flags, err, op=SUM, nblocks=0, budget_ticks=0, stream=None, accum=None):
     """out = x (op) unpack(pack(y)) -- the 1-GPU LL16 hot path (BASELINE config 2)."""
     assert x.dtype == y.dtype == out.dtype and x.numel() == y.numel() == out.numel()
     nbytes = x.numel() * x.element_size()
     code = lib().mscclppAmdSelfReduceLL16(
         ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(pkts_ptr),
-        ctypes.c_void_p(out.data_ptr()), nbytes, DTYPE_CODES[x.dtype], op, ctypes.c_void_p(flags.data_ptr()),
+        ctypes.c_void_p(out.data_ptr()), nbytes, reduce_code(x.dtype, accum), op, ctypes.c_void_p(flags.data_ptr()),
         nblocks, budget_ticks or 200_000_000, ctypes.c_void_p(err.data_ptr()), stream_ptr(stream))
     check(code, "self_reduce_ll16")
 
@@ -220,8 +236,9 @@ class InProcessRanks:
             v.rank = r
         return arr
 
-    def all_reduce(self, inputs, outputs, algo, op=SUM, nblocks=0, nthreads=0, budget_ticks=500_000_000, stream=None):
-        dt = DTYPE_CODES[inputs[0].dtype]
+    def all_reduce(self, inputs, outputs, algo, op=SUM, nblocks=0, nthreads=0, budget_ticks=500_000_000, stream=None,
+                   accum=None):
+        dt = reduce_code(inputs[0].dtype, accum)
         nbytes = inputs[0].numel() * inputs[0].element_size()
         bulk = algo in (ALGO_FULLMESH, ALGO_RSAG)
         arr = self.views(inputs, outputs, bulk=bulk)
@@ -230,9 +247,9 @@ class InProcessRanks:
         check(code, "in-process all_reduce")
 
     def collective(self, coll, inputs, outputs, algo=ALGO_FULLMESH, op=SUM, nblocks=8, nthreads=256,
-                   budget_ticks=500_000_000, stream=None):
+                   budget_ticks=500_000_000, stream=None, accum=None):
         """coll 1 = ReduceScatter (inputs n*block, outputs block), 2 = AllGather (inputs block, outputs n*block)."""
-        dt = DTYPE_CODES[inputs[0].dtype]
+        dt = reduce_code(inputs[0].dtype, accum)
         big = inputs[0] if coll == 1 else outputs[0]
         nbytes = big.numel() * big.element_size()
         arr = self.views(inputs, outputs, bulk=True)
@@ -288,11 +305,18 @@ class Communicator:
         dist.broadcast_object_list(obj, src=0, group=group)
         return cls(rank, n, obj[0])
 
-    def all_reduce(self, send, recv=None, op="sum", algo=None, nblocks=0, nthreads=0, stream=None):
-        """ncclAllReduce(send, recv, count, dtype, op, comm, stream); algo forces an algorithm."""
+    def all_reduce(self, send, recv=None, op="sum", algo=None, nblocks=0, nthreads=0, stream=None, accum=None):
+        """ncclAllReduce(send, recv, count, dtype, op, comm, stream); algo forces an algorithm, accum
+        the accumulation dtype of Algorithm::execute (fp8 buffers: torch.float16 / torch.float32)."""
         recv = send if recv is None else recv
         dt = NCCL_DTYPES[send.dtype]
-        if algo is None:
+        if accum is not None:
+            code = lib().mscclppAmdCommAllReduceAccum(self.comm, ctypes.c_void_p(send.data_ptr()),
+                                                      ctypes.c_void_p(recv.data_ptr()), send.numel(), dt,
+                                                      NCCL_OPS[op], NCCL_DTYPES[accum],
+                                                      ALGO_NAMES.get(algo or "auto", algo) if isinstance(algo, str) or algo is None else algo,
+                                                      nblocks, nthreads, stream_ptr(stream))
+        elif algo is None:
             code = lib().ncclAllReduce(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(recv.data_ptr()),
                                        send.numel(), dt, NCCL_OPS[op], self.comm, stream_ptr(stream))
         else:

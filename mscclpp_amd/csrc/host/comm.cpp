@@ -52,7 +52,7 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
   return guarded([&] {
     if (!views || nviews < 1 || nranks < 2 || nranks > MSCCLPP_AMD_MAX_RANKS || bytes == 0) return (int)ncclInvalidArgument;
     if (nviews != 1 && nviews != nranks) return (int)ncclInvalidArgument;
-    if (dtype < 0 || dtype > MSCCLPP_AMD_U32 || op < 0 || op > MSCCLPP_AMD_MIN) return (int)ncclInvalidArgument;
+    if (dtype < 0 || dtype >= MSCCLPP_AMD_NUM_DTYPES || op < 0 || op > MSCCLPP_AMD_MIN) return (int)ncclInvalidArgument;
     if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = mscclppAmdSelectAlgo(nranks, bytes, dtype);
     if (budgetTicks == 0) budgetTicks = spinBudgetTicks();
     // validate every pointer the kernel will dereference before launching (a fault here would
@@ -276,7 +276,7 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     const int dt = dtypeFromNccl(datatype);
     const int o = opFromNccl(op);
     if (dt < 0 || o < 0) {
-      warn("unsupported dtype/op for AllReduce (supported: fp16, bf16, fp32, int32, uint32 x sum, min)");
+      warn("unsupported dtype/op for AllReduce (supported: fp16, bf16, fp32, int32, uint32, fp8 e4m3/e5m2 x sum, min)");
       return (int)ncclInvalidArgument;
     }
     return comm->allReduce(sendbuff, recvbuff, bytes, dt, o, MSCCLPP_AMD_ALGO_AUTO, 0, 0, (hipStream_t)stream);
@@ -343,10 +343,18 @@ ncclResult_t ncclMemFree(void* ptr) {
 // =============================================================================================
 int mscclppAmdCommAllReduce(ncclComm_t comm, const void* sendbuff, void* recvbuff, size_t count, int ncclDtype,
                             int ncclOp, int algo, int nblocks, int nthreads, void* stream) {
+  return mscclppAmdCommAllReduceAccum(comm, sendbuff, recvbuff, count, ncclDtype, ncclOp, -1, algo, nblocks, nthreads,
+                                      stream);
+}
+
+int mscclppAmdReduceType(int ncclDtype, int accumNcclDtype) { return reduceTypeFromNccl(ncclDtype, accumNcclDtype); }
+
+int mscclppAmdCommAllReduceAccum(ncclComm_t comm, const void* sendbuff, void* recvbuff, size_t count, int ncclDtype,
+                                 int ncclOp, int accumNcclDtype, int algo, int nblocks, int nthreads, void* stream) {
   return guarded([&] {
     if (!comm || !sendbuff || !recvbuff || count == 0) return (int)ncclInvalidArgument;
     const size_t tb = ncclTypeBytes((ncclDataType_t)ncclDtype);
-    const int dt = dtypeFromNccl((ncclDataType_t)ncclDtype);
+    const int dt = reduceTypeFromNccl(ncclDtype, accumNcclDtype);
     const int o = opFromNccl((ncclRedOp_t)ncclOp);
     if (dt < 0 || o < 0 || tb == 0) return (int)ncclInvalidArgument;
     if (comm->nranks == 1) {

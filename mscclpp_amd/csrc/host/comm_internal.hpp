@@ -112,8 +112,22 @@ inline int dtypeFromNccl(ncclDataType_t t) {
     case ncclFloat32: return MSCCLPP_AMD_F32;
     case ncclInt32: return MSCCLPP_AMD_I32;
     case ncclUint32: return MSCCLPP_AMD_U32;
+    case ncclFloat8e4m3: return MSCCLPP_AMD_E4M3;  // OCP on gfx950 (datatype_conversion.hpp:29-40)
+    case ncclFloat8e5m2: return MSCCLPP_AMD_E5M2;
     default: return -1;
   }
+}
+// (element dtype, accumulation dtype) -> reduce-type code; accum < 0 means AUTO = the element type
+// (algorithm.cc:47), FP8 may accumulate in half or float (dispatchFp8Accum, common.hpp:89-100).
+inline int reduceTypeFromNccl(int ncclDtype, int accum) {
+  const int dt = dtypeFromNccl((ncclDataType_t)ncclDtype);
+  if (dt < 0 || accum < 0 || accum == ncclDtype) return dt;
+  if (dt == MSCCLPP_AMD_E4M3 || dt == MSCCLPP_AMD_E5M2) {
+    const int e5 = dt == MSCCLPP_AMD_E5M2;
+    if (accum == ncclFloat16) return e5 ? MSCCLPP_AMD_E5M2_ACC_F16 : MSCCLPP_AMD_E4M3_ACC_F16;
+    if (accum == ncclFloat32) return e5 ? MSCCLPP_AMD_E5M2_ACC_F32 : MSCCLPP_AMD_E4M3_ACC_F32;
+  }
+  return -1;  // the reference returns no kernel for other (dtype, accum) pairs
 }
 inline size_t ncclTypeBytes(ncclDataType_t t) {
   switch (t) {

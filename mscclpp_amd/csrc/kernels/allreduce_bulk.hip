@@ -139,9 +139,18 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
               w[k] = load16<kSystem>(rscr, (uint32_t)((uint64_t)src * g.pass) + u * 16u);
             }
           }
+          if constexpr (AccWord<DT, OP>::kWide) {
+            // calVectorAccum<T, AccumT> (allreduce_fullmesh.cu:102-108, allreduce_rsag.cu:88-95)
+            Accum<DT, OP, 4> sum(acc);
 #pragma unroll
-          for (int k = 1; k < kMaxRanks; ++k)
-            if (k < nranks) acc = reduce4<DT, OP>(acc, w[k]);
+            for (int k = 1; k < kMaxRanks; ++k)
+              if (k < nranks) sum.add(w[k]);
+            acc = sum.template get<u32x4>();
+          } else {
+#pragma unroll
+            for (int k = 1; k < kMaxRanks; ++k)
+              if (k < nranks) acc = reduce4<DT, OP>(acc, w[k]);
+          }
         }
         store_payload<kPlain>(rout, myOut, (uint64_t)u * 16, acc, vb);
         if constexpr (MODE != 1) {
@@ -231,11 +240,11 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
   if (!bulkScratchRequired(nranks, bytes, views[0].scratchBytes, &g, nblocks)) return 5;
   const int order = (algo == MSCCLPP_AMD_ALGO_RSAG && mode != 2) ? 1 : 0;
   if (mode == 2) {  // byte movement only: map to the f16 or f32 instantiation by element width
-    dtype = (dtype == kF16 || dtype == kBF16) ? kF16 : kF32;
+    dtype = elem_bytes(dtype) == 2 ? kF16 : kF32;
     op = kSum;
   }
   g_launch_status = 0;
-  MSCCLPP_AMD_DISPATCH(dtype, op, launchBulk, views, nviews, g, nranks, nblocks, nthreads, budget, s, order, mode);
+  MSCCLPP_AMD_DISPATCH_ALL(dtype, op, launchBulk, views, nviews, g, nranks, nblocks, nthreads, budget, s, order, mode);
   if (g_launch_status) return g_launch_status;
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
     for (uint32_t j = b * T + tid; j < npk; j += G * T) {
       const uint64_t off = soff + (uint64_t)j * 8;
       const uint32_t valid = clamp_valid(g.bytes, off, 8);
-      u32x2 acc = payload_ld(rin, in, off, valid);
+      Accum<DT, OP, 2> sum(payload_ld(rin, in, off, valid));  // upcastVector (:98-99)
       u32x2 w[kMaxRanks];
       bool ready = true;
 #pragma unroll
@@ -152,13 +152,14 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
       if (ready) {
 #pragma unroll
         for (int p = 0; p < kMaxRanks; ++p)
-          if (p < nranks && p != rank) acc = reduce2<DT, OP>(acc, w[p]);
+          if (p < nranks && p != rank) sum.add(w[p]);
       } else {
         for (int p = 0; p < nranks; ++p) {
           if (p == rank) continue;
-          acc = reduce2<DT, OP>(acc, unit_get(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, false, budget, v.err));
+          sum.add(unit_get(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, false, budget, v.err));
         }
       }
+      const u32x2 acc = sum.template get<u32x2>();  // downcastVector (:107-108)
       payload_st(rout, out, off, acc, valid);
       // broadcast: a runtime loop, so one descriptor is live at a time (SGPR budget)
 #pragma unroll 1
@@ -216,7 +217,7 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
     const bool single = 2ull * j + 1 >= g.W;
     const uint64_t off = (uint64_t)j * 8;
     const uint32_t valid = clamp_valid(g.bytes, off, single ? 4 : 8);
-    u32x2 acc = payload_ld(rin, in, off, valid);
+    Accum<DT, OP, 2> sum(payload_ld(rin, in, off, valid));  // upcastVector (:54)
     u32x2 w[kMaxRanks];
     bool ready = true;
 #pragma unroll
@@ -225,25 +226,35 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
     if (ready) {
 #pragma unroll
       for (int p = 0; p < kMaxRanks; ++p)
-        if (p < nranks && p != rank) acc = reduce2<DT, OP>(acc, w[p]);
+        if (p < nranks && p != rank) sum.add(w[p]);
     } else {
       for (int p = 0; p < nranks; ++p) {
         if (p == rank) continue;
-        acc = reduce2<DT, OP>(acc, unit_get(rscr, (uint32_t)(p * region) + j * 16u, flag, single, budget, v.err));
+        sum.add(unit_get(rscr, (uint32_t)(p * region) + j * 16u, flag, single, budget, v.err));
       }
     }
-    payload_st(rout, out, off, acc, valid);
+    payload_st(rout, out, off, sum.template get<u32x2>(), valid);  // downcastVector (:61)
   }
   bump_flags(v.flags, flag);
 }
 
 // ---- host-side geometry + launch -------------------------------------------------------------------
-static inline bool is2byte(int dtype) { return dtype == kF16 || dtype == kBF16; }
+// 32-bit words the LL kernels cover: (count*sizeof(T)+sizeof(T))/sizeof(int) for 1- and 2-byte T
+// (allreduce_packet.cu:51-52, allreduce_allpair_packet.cu:20).  Deviation: for 1-byte T with
+// count % 4 in {1, 2} that stops short of the buffer (its last bytes would never be reduced), so
+// the words are rounded up there; every other size keeps the reference's count.
+static inline uint64_t llWords(size_t bytes, int dtype) {
+  const int es = elem_bytes(dtype);
+  if (es == 4) return bytes / 4;
+  uint64_t W = (bytes + es) / 4;
+  if (W * 4 < bytes) W = (bytes + 3) / 4;
+  return W;
+}
 
 static LL16Geom ll16Geometry(int nranks, size_t bytes, int dtype) {
   LL16Geom g{};
   g.bytes = bytes;
-  g.W = is2byte(dtype) ? (bytes + 2) / 4 : bytes / 4;  // (count*sizeof(T)+sizeof(T))/4 for 2-byte T
+  g.W = llWords(bytes, dtype);
   g.wpr = g.W / (uint64_t)nranks;
   if (g.wpr % 2) g.wpr += 1;
   // Deviation from allreduce_packet.cu:62-63: when W % n != 0 and W / n is even the reference's
@@ -263,7 +274,7 @@ static LL16Geom ll16Geometry(int nranks, size_t bytes, int dtype) {
 static LL8Geom ll8Geometry(size_t bytes, int dtype) {
   LL8Geom g{};
   g.bytes = bytes;
-  g.W = is2byte(dtype) ? (bytes + 2) / 4 : bytes / 4;
+  g.W = llWords(bytes, dtype);
   g.units = (uint32_t)((g.W + 1) / 2);
   return g;
 }
@@ -370,7 +381,7 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
     if (g.W == 0) return 4;
     for (int i = 0; i < nviews; ++i)
       if (views[i].scratchBytes < ll16ScratchRequired(nranks, bytes, dtype)) return 5;
-    MSCCLPP_AMD_DISPATCH(dtype, op, launchLL16, views, nviews, g, nranks, nblocks, nthreads, budget, s);
+    MSCCLPP_AMD_DISPATCH_ALL(dtype, op,launchLL16, views, nviews, g, nranks, nblocks, nthreads, budget, s);
   } else {
     ll8Defaults(nranks, bytes, nblocks, nthreads);
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
@@ -378,7 +389,7 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
     if (g.W == 0) return 4;
     for (int i = 0; i < nviews; ++i)
       if (views[i].scratchBytes < ll8ScratchRequired(nranks, bytes, dtype)) return 5;
-    MSCCLPP_AMD_DISPATCH(dtype, op, launchLL8, views, nviews, g, nranks, nblocks, nthreads, budget, s);
+    MSCCLPP_AMD_DISPATCH_ALL(dtype, op,launchLL8, views, nviews, g, nranks, nblocks, nthreads, budget, s);
   }
   if (g_ll_launch_status) return g_ll_launch_status;
   return hipGetLastError() == hipSuccess ? 0 : 1;

@@ -267,6 +267,6 @@ extern "C" int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts
   if (nblocks % 2) nblocks += 1;
   if (nblocks > 1024) return 4;
   const uint64_t nunits = bytes / 16;
-  MSCCLPP_AMD_DISPATCH(dtype, op, launchSelfReduce, x, y, pkts, out, nunits, flags, nblocks, budgetTicks, err, stream);
+  MSCCLPP_AMD_DISPATCH_ALL(dtype, op, launchSelfReduce, x, y, pkts, out, nunits, flags, nblocks, budgetTicks, err, stream);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

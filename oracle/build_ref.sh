@@ -12,7 +12,7 @@ if [ ! -d "$REF/include/mscclpp" ]; then
   echo "reference tree not present: skipping oracle/_ref" >&2
   exit 0
 fi
-if [ "$OUT/libref.so" -nt "$HERE/ref_harness.hip" ]; then exit 0; fi
+if [ "$OUT/libref.so" -nt "$HERE/ref_harness.hip" ] && [ "$OUT/libref.so" -nt "$HERE/build_ref.sh" ]; then exit 0; fi
 # -D__HIP_PLATFORM_AMD__ selects the reference's HIP branch (gpu_data_types.hpp:50)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -D__HIP_PLATFORM_AMD__ \
   -I"$REF/include" "$HERE/ref_harness.hip" -o "$OUT/libref.so"

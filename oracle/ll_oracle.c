@@ -23,7 +23,32 @@
 
 /* ---- dtype / op codes (mirror include/mscclpp_amd/mscclpp_amd.h) ---------------------- */
 enum { ORC_F16 = 0, ORC_BF16 = 1, ORC_F32 = 2, ORC_I32 = 3, ORC_U32 = 4 };
+/* OCP FP8 reduce types: element e4m3 / e5m2, accumulated in the element type, half or float
+ * (calVectorAccum<T, AccumT>, src/core/include/reduce_kernel.hpp:139-189; common.hpp:89-100). */
+enum { ORC_E4M3 = 5, ORC_E5M2 = 6, ORC_E4M3_ACC_F16 = 7, ORC_E5M2_ACC_F16 = 8, ORC_E4M3_ACC_F32 = 9,
+       ORC_E5M2_ACC_F32 = 10 };
 enum { ORC_SUM = 0, ORC_MIN = 1 };
+
+static int orc_is_fp8(int dt) { return dt >= ORC_E4M3 && dt <= ORC_E5M2_ACC_F32; }
+static int orc_is_e5m2(int dt) { return dt == ORC_E5M2 || dt == ORC_E5M2_ACC_F16 || dt == ORC_E5M2_ACC_F32; }
+static int orc_acc_kind(int dt) {
+  if (dt == ORC_E4M3_ACC_F16 || dt == ORC_E5M2_ACC_F16) return 1;
+  if (dt == ORC_E4M3_ACC_F32 || dt == ORC_E5M2_ACC_F32) return 2;
+  return 0;
+}
+static int orc_elem_bytes(int dt) { return (dt == ORC_F16 || dt == ORC_BF16) ? 2 : (orc_is_fp8(dt) ? 1 : 4); }
+
+/* 32-bit words the LL kernels cover: (count*sizeof(T)+sizeof(T))/4 for 1- and 2-byte T
+ * (allreduce_packet.cu:51-54, allreduce_allpair_packet.cu:20).  Deviation: 1-byte T
+ * with count % 4 in {1, 2} would stop short of the buffer, so W is rounded up there only. */
+static uint64_t orc_ll_words(int dt, uint64_t count) {
+  int es = orc_elem_bytes(dt);
+  uint64_t bytes = count * (uint64_t)es;
+  if (es == 4) return count;
+  uint64_t W = (bytes + (uint64_t)es) / 4;
+  if (W * 4 < bytes) W = (bytes + 3) / 4;
+  return W;
+}
 
 /* ---- scalar conversions ---------------------------------------------------------------- */
 static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
@@ -150,14 +175,146 @@ uint32_t oracle_f32_min(uint32_t a, uint32_t b) {
   if (na && nb) return a | 0x00400000u;
   if (na) return b;
   if (nb) return a;
+  if (u2f(a) == u2f(b)) return a | b; /* v_min_f32 orders -0 below +0 */
   return f2u(fminf(u2f(a), u2f(b)));
 }
 
 uint16_t oracle_f32_to_f16(float f) { return float_to_half_rne(f); }
 uint16_t oracle_f32_to_bf16(float f) { return float_to_bf16_rne(f); }
 
+/* ---- OCP FP8 (gfx950 formats) ---------------------------------------------------------------
+ * The reference's ROCm gfx950 build takes the generic branches of gpu_data_types.hpp (the packed
+ * fp8 paths there are gfx942-only), so per element:
+ *   float(fp8)        -> v_cvt_f32_fp8 / _bf8: exact for finite values        (amd_hip_fp8.h:638-650)
+ *   __hip_fp8_*(f)    -> non-NaN/Inf saturated to +-448 / +-57344, then RNE  (amd_hip_fp8.h:548-592)
+ * The NaN / Inf images of the two hardware conversions were pinned against the device by
+ * tests/test_fp8_gpu.py (the reference's own conversions run on the GPU): every NaN byte decodes
+ * to 0xFFC00000; every float NaN encodes to 0xFF (e4m3) / 0xFE (e5m2); +-Inf encodes to 0x7F/0xFF
+ * (e4m3, no infinities) and 0x7C/0xFC (e5m2). */
+static float fp8_decode(uint8_t b, int e5m2) {
+  uint32_t sign = (b & 0x80u) ? 0x80000000u : 0u;
+  float v;
+  if (!e5m2) {
+    uint32_t e = (b >> 3) & 0xfu, m = b & 7u;
+    if ((b & 0x7fu) == 0x7fu) return u2f(0xffc00000u);
+    v = e ? ldexpf(1.0f + (float)m / 8.0f, (int)e - 7) : ldexpf((float)m / 8.0f, -6);
+  } else {
+    uint32_t e = (b >> 2) & 0x1fu, m = b & 3u;
+    if (e == 0x1fu) return m ? u2f(0xffc00000u) : u2f(sign | 0x7f800000u);
+    v = e ? ldexpf(1.0f + (float)m / 4.0f, (int)e - 15) : ldexpf((float)m / 4.0f, -14);
+  }
+  return sign ? -v : v;
+}
+
+/* hardware float -> fp8 (no clamp), RNE; NaN / Inf images as the device produces them */
+static uint8_t fp8_encode_hw(float f, int e5m2) {
+  uint32_t x = f2u(f);
+  uint8_t sign = (uint8_t)((x >> 24) & 0x80u);
+  float a = fabsf(f);
+  if ((x & 0x7fffffffu) > 0x7f800000u) return e5m2 ? 0xfeu : 0xffu;            /* NaN, any sign */
+  if ((x & 0x7fffffffu) == 0x7f800000u) return (uint8_t)(sign | (e5m2 ? 0x7cu : 0x7fu)); /* Inf */
+  int mbits = e5m2 ? 2 : 3, bias = e5m2 ? 15 : 7;
+  int emin = 1 - bias; /* smallest normal exponent */
+  if (a < ldexpf(1.0f, emin)) {
+    /* subnormal range: integer multiple of 2^(emin - mbits); a carry to 2^mbits is the smallest normal */
+    float q = rintf(ldexpf(a, mbits - emin));
+    return (uint8_t)(sign | (uint8_t)q);
+  }
+  int e;
+  frexpf(a, &e); /* a = fr * 2^e, fr in [0.5, 1) */
+  e -= 1;        /* a = 1.m * 2^e */
+  float r = rintf(ldexpf(a, mbits - e)); /* in [2^mbits, 2^(mbits+1)] */
+  uint32_t bits = ((uint32_t)(e + bias) << mbits) + (uint32_t)r - (1u << mbits);
+  uint32_t maxbits = e5m2 ? 0x7bu : 0x7eu;
+  if (bits > maxbits) bits = e5m2 ? 0x7cu : 0x7fu; /* only reachable without saturation */
+  return (uint8_t)(sign | bits);
+}
+
+/* __hip_fp8_e4m3(float) / __hip_fp8_e5m2(float) with __HIP_SATFINITE */
+static uint8_t fp8_encode_sat(float f, int e5m2) {
+  uint32_t x = f2u(f);
+  if ((x & 0x7f800000u) != 0x7f800000u) {
+    float m = e5m2 ? 57344.0f : 448.0f;
+    if (f > m) f = m;
+    if (f < -m) f = -m;
+  }
+  return fp8_encode_hw(f, e5m2);
+}
+
+/* software fp8 -> half of amd_hip_fp8.h:403-541: exact, every NaN -> +0x7C01, e5m2 inf -> inf */
+static uint16_t fp8_to_half_sw(uint8_t b, int e5m2) {
+  if (!e5m2 && (b & 0x7fu) == 0x7fu) return 0x7c01u;
+  if (e5m2 && (b & 0x7cu) == 0x7cu && (b & 3u)) return 0x7c01u;
+  if (e5m2) return (uint16_t)((uint16_t)b << 8);
+  return float_to_half_rne(fp8_decode(b, 0));
+}
+
+/* __half add / compare without clip (calElements<__half>, reduce_kernel.hpp:16-24) */
+static uint16_t half_add_noclip(uint16_t a, uint16_t b) {
+  if (half_isnan(a) || half_isnan(b)) return 0x7e00u; /* a quiet +NaN: only its NaN-ness reaches fp8 */
+  return float_to_half_rne(half_to_float(a) + half_to_float(b));
+}
+static uint16_t half_lt_min(uint16_t a, uint16_t b) { return half_to_float(a) < half_to_float(b) ? a : b; }
+
+uint8_t oracle_fp8_encode_sat(float f, int e5m2) { return fp8_encode_sat(f, e5m2); }
+float oracle_fp8_decode(uint8_t b, int e5m2) { return fp8_decode(b, e5m2); }
+
+/* device fminf (v_min_f32, IEEE mode): a NaN operand yields the other one, and -0 < +0 */
+static float fminf_dev(float x, float y) {
+  if (x == y) return u2f(f2u(x) | f2u(y));
+  return fminf(x, y);
+}
+
+/* T == AccumT (gpu_data_types.hpp:425-443, 499-516 with clip :353-371, min :690-750) */
+static uint8_t fp8_reduce_same(uint8_t a, uint8_t b, int e5m2, int op) {
+  float x = fp8_decode(a, e5m2), y = fp8_decode(b, e5m2);
+  if (op == ORC_MIN) return fp8_encode_sat(fminf_dev(x, y), e5m2);
+  uint8_t s = fp8_encode_sat(x + y, e5m2);
+  if (!e5m2) return s; /* clip<__fp8_e4m3> is the identity */
+  float f = fmaxf(fp8_decode(s, 1), -57344.0f); /* NaN -> -57344 */
+  f = fminf(f, 57344.0f);
+  return fp8_encode_sat(f, 1);
+}
+
+/* dst[i] = down(up(src[0][i]) (op) up(src[1][i]) (op) ...) for fp8 reduce types, nsrc sources in
+ * sum order, over nbytes elements (calVectorAccum, reduce_kernel.hpp:171-189). */
+static void fp8_reduce_seq(int dt, int op, int nsrc, const uint8_t* const* src, size_t nbytes, uint8_t* dst) {
+  int e5 = orc_is_e5m2(dt), kind = orc_acc_kind(dt);
+  for (size_t i = 0; i < nbytes; i++) {
+    if (kind == 0) {
+      uint8_t a = src[0][i];
+      for (int k = 1; k < nsrc; k++) a = fp8_reduce_same(a, src[k][i], e5, op);
+      dst[i] = a;
+    } else if (kind == 2) {
+      float a = fp8_decode(src[0][i], e5);
+      for (int k = 1; k < nsrc; k++) {
+        float v = fp8_decode(src[k][i], e5);
+        a = (op == ORC_SUM) ? a + v : (a < v ? a : v);
+      }
+      dst[i] = fp8_encode_sat(a, e5);
+    } else {
+      uint16_t a = fp8_to_half_sw(src[0][i], e5);
+      for (int k = 1; k < nsrc; k++) {
+        uint16_t v = fp8_to_half_sw(src[k][i], e5);
+        a = (op == ORC_SUM) ? half_add_noclip(a, v) : half_lt_min(a, v);
+      }
+      dst[i] = fp8_encode_sat(half_to_float(a), e5);
+    }
+  }
+}
+
 /* calVectorAccum<T,T,Op> over one 32-bit word (reduce_kernel.hpp:86-134, 171-175). */
 static uint32_t reduce_word(int dtype, int op, uint32_t acc, uint32_t val) {
+  if (orc_is_fp8(dtype)) { /* one accumulation step: down(up(acc) (op) up(val)) per byte */
+    uint8_t a[4], v[4], r[4];
+    const uint8_t* s[2] = {a, v};
+    memcpy(a, &acc, 4);
+    memcpy(v, &val, 4);
+    fp8_reduce_seq(dtype, op, 2, s, 4, r);
+    uint32_t out;
+    memcpy(&out, r, 4);
+    return out;
+  }
   switch (dtype) {
     case ORC_F16: {
       uint16_t a0 = acc & 0xffff, a1 = acc >> 16, v0 = val & 0xffff, v1 = val >> 16;
@@ -186,6 +343,18 @@ static uint32_t reduce_word(int dtype, int op, uint32_t acc, uint32_t val) {
 /* acc[i] = acc[i] (op) val[i] for nwords 32-bit words. */
 void oracle_reduce_words(int dtype, int op, uint32_t* acc, const uint32_t* val, size_t nwords) {
   for (size_t i = 0; i < nwords; i++) acc[i] = reduce_word(dtype, op, acc[i], val[i]);
+}
+
+/* dst = src[0] (op) src[1] (op) ... (op) src[nsrc-1], in this order, accumulating in the reduce
+ * type's AccumT (upcastVector / calVectorAccum / downcastVector, reduce_kernel.hpp:139-189).
+ * dst may alias src[0]. */
+void oracle_reduce_seq(int dtype, int op, int nsrc, const uint32_t* const* src, size_t nwords, uint32_t* dst) {
+  if (orc_is_fp8(dtype)) {
+    fp8_reduce_seq(dtype, op, nsrc, (const uint8_t* const*)src, nwords * 4, (uint8_t*)dst);
+    return;
+  }
+  if (dst != src[0]) memmove(dst, src[0], nwords * 4);
+  for (int k = 1; k < nsrc; k++) oracle_reduce_words(dtype, op, dst, src[k], nwords);
 }
 
 /* ---- LL packets -------------------------------------------------------------------------- */
@@ -254,11 +423,7 @@ typedef struct {
 } orc_ll16_geom;
 
 void oracle_ll16_geometry(int dtype, uint64_t count, int n, uint64_t* out6) {
-  uint64_t W;
-  if (dtype == ORC_F16 || dtype == ORC_BF16)
-    W = (count * 2 + 2) / 4; /* :51-52 */
-  else
-    W = count; /* :53-54, 4-byte types */
+  uint64_t W = orc_ll_words(dtype, count); /* :51-54 */
   uint64_t wpr = W / (uint64_t)n; /* :62 */
   if (wpr % 2) wpr = wpr + 1;     /* :63, (x*sizeof(T)+sizeof(T))/sizeof(T) = x+1 */
   /* Deviation (documented in DESIGN.md): where the reference's slices stop short of W (W % n != 0
@@ -295,16 +460,20 @@ void oracle_allreduce_packet(int dtype, int op, int n, const uint32_t* const* in
       oracle_ll16_pack(in[s] + (uint64_t)q * wpr, ppr, flag, dstp);
     }
   /* step 2: rank r reduces its slice and broadcasts reduced packets (:92-123) */
-  uint32_t* tmp = (uint32_t*)malloc(wpr * 4 + 8);
+  uint32_t* tmp = (uint32_t*)malloc((size_t)n * (wpr * 4 + 8));
   for (int r = 0; r < n; r++) {
     uint32_t* acc = out[r] + (uint64_t)r * wpr;
-    memcpy(acc, in[r] + (uint64_t)r * wpr, wpr * 4);
+    const uint32_t* srcs[64];
+    int ns = 0;
+    srcs[ns++] = in[r] + (uint64_t)r * wpr; /* own copy first, then peers ascending */
     for (int p = 0; p < n; p++) {
       if (p == r) continue;
       const uint32_t* pk = scratch[r] + (base + (uint64_t)p * ppr * 16) / 4;
-      oracle_ll16_unpack(pk, ppr, flag, tmp);
-      oracle_reduce_words(dtype, op, acc, tmp, wpr);
+      uint32_t* t = tmp + (size_t)ns * (wpr + 2);
+      oracle_ll16_unpack(pk, ppr, flag, t);
+      srcs[ns++] = t;
     }
+    oracle_reduce_seq(dtype, op, ns, srcs, wpr, acc);
     for (int q = 0; q < n; q++) {
       if (q == r) continue;
       uint32_t* dstp = scratch[q] + (base + roff + (uint64_t)r * ppr * 16) / 4;
@@ -327,21 +496,25 @@ void oracle_allreduce_packet(int dtype, int op, int n, const uint32_t* const* in
 void oracle_allreduce_allpairs(int dtype, int op, int n, const uint32_t* const* in, uint64_t count,
                                uint32_t flag, uint64_t half_bytes, uint32_t* const* scratch,
                                uint32_t* const* out) {
-  uint64_t W = (dtype == ORC_F16 || dtype == ORC_BF16) ? (count * 2 + 2) / 4 : count;
+  uint64_t W = orc_ll_words(dtype, count);
   uint64_t base = (flag % 2) ? half_bytes : 0;
   for (int s = 0; s < n; s++)
     for (int q = 0; q < n; q++) {
       if (q == s) continue;
       oracle_ll8_pack(in[s], W, flag, scratch[q] + (base + (uint64_t)s * W * 8) / 4);
     }
-  uint32_t* tmp = (uint32_t*)malloc(W * 4 + 8);
+  uint32_t* tmp = (uint32_t*)malloc((size_t)n * (W * 4 + 8));
   for (int r = 0; r < n; r++) {
-    memcpy(out[r], in[r], W * 4);
+    const uint32_t* srcs[64];
+    int ns = 0;
+    srcs[ns++] = in[r]; /* own first, then peers ascending (:51-60) */
     for (int p = 0; p < n; p++) {
       if (p == r) continue;
-      oracle_ll8_unpack(scratch[r] + (base + (uint64_t)p * W * 8) / 4, W, flag, tmp);
-      oracle_reduce_words(dtype, op, out[r], tmp, W);
+      uint32_t* t = tmp + (size_t)ns * (W + 2);
+      oracle_ll8_unpack(scratch[r] + (base + (uint64_t)p * W * 8) / 4, W, flag, t);
+      srcs[ns++] = t;
     }
+    oracle_reduce_seq(dtype, op, ns, srcs, W, out[r]);
   }
   free(tmp);
 }
@@ -354,13 +527,16 @@ void oracle_allreduce_allpairs(int dtype, int op, int n, const uint32_t* const* 
 static void reduce_range(int dtype, int op, int n, const uint32_t* const* in, int owner, int order_kind,
                          uint64_t w0, uint64_t nw, uint32_t* dst) {
   int start = (order_kind == 2) ? (owner + 1) % n : owner;
-  memcpy(dst, in[start] + w0, nw * 4);
+  const uint32_t* srcs[64];
+  int ns = 0;
+  srcs[ns++] = in[start] + w0;
   if (order_kind == 0) {
     for (int p = 0; p < n; p++)
-      if (p != owner) oracle_reduce_words(dtype, op, dst, in[p] + w0, nw);
+      if (p != owner) srcs[ns++] = in[p] + w0;
   } else {
-    for (int k = 1; k < n; k++) oracle_reduce_words(dtype, op, dst, in[(start + k) % n] + w0, nw);
+    for (int k = 1; k < n; k++) srcs[ns++] = in[(start + k) % n] + w0;
   }
+  oracle_reduce_seq(dtype, op, ns, srcs, nw, dst);
 }
 
 /* AllReduce over n ranks where slice q (of `slice_words`, the last slice takes the rest) is
@@ -403,6 +579,8 @@ void oracle_lcg_fill(int dtype, uint64_t count, int rank, int seq, void* dst) {
       ((uint16_t*)dst)[i] = float_to_bf16_rne(v);
     else if (dtype == ORC_F32)
       ((uint32_t*)dst)[i] = f2u(v);
+    else if (orc_is_fp8(dtype))
+      ((uint8_t*)dst)[i] = fp8_encode_sat(v, orc_is_e5m2(dtype));
     else
       ((uint32_t*)dst)[i] = (uint32_t)(int32_t)(v * 2147483647.0f);
   }

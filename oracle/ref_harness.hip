@@ -60,6 +60,61 @@ __global__ void refUnpackReduceLL16(const void* pkts, const uint32_t* x, uint32_
   }
 }
 
+// ---- OCP FP8 (built without MSCCLPP_ROCM_FP8_FNUZ: gfx950's native formats) -----------------
+// calVectorAccum<T, AccumT, Op> (reduce_kernel.hpp:171-189) restated over the reference's own
+// operators: T == AccumT -> calVector (f8x4 operator+ / mscclpp::min, :112-134); otherwise
+// mscclpp::to<> upcast, calElements<AccumT> per element (a + b / mscclpp::min), to<> downcast.
+template <int DT> struct RefFp8;
+template <> struct RefFp8<5> { using T = __fp8_e4m3; using A = __fp8_e4m3; };
+template <> struct RefFp8<6> { using T = __fp8_e5m2; using A = __fp8_e5m2; };
+template <> struct RefFp8<7> { using T = __fp8_e4m3; using A = __half; };
+template <> struct RefFp8<8> { using T = __fp8_e5m2; using A = __half; };
+template <> struct RefFp8<9> { using T = __fp8_e4m3; using A = float; };
+template <> struct RefFp8<10> { using T = __fp8_e5m2; using A = float; };
+
+template <int DT, int OP>
+__global__ void refFp8AccumKernel(const uint32_t* src, int nsrc, size_t n, uint32_t* out) {
+  using T = typename RefFp8<DT>::T;
+  using A = typename RefFp8<DT>::A;
+  using FromVec = VectorType<T, 4>;
+  for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    if constexpr (std::is_same_v<T, A>) {
+      FromVec acc = bit_cast<FromVec, uint32_t>(src[i]);
+      for (int k = 1; k < nsrc; ++k) {
+        FromVec v = bit_cast<FromVec, uint32_t>(src[(size_t)k * n + i]);
+        acc = (OP == 0) ? acc + v : mscclpp::min(acc, v);
+      }
+      out[i] = bit_cast<uint32_t, FromVec>(acc);
+    } else {
+      using ToVec = VectorType<A, 4>;
+      ToVec acc = mscclpp::to<ToVec>(bit_cast<FromVec, uint32_t>(src[i]));
+      for (int k = 1; k < nsrc; ++k) {
+        ToVec v = mscclpp::to<ToVec>(bit_cast<FromVec, uint32_t>(src[(size_t)k * n + i]));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc.data[e] = (OP == 0) ? acc.data[e] + v.data[e] : mscclpp::min(acc.data[e], v.data[e]);
+      }
+      out[i] = bit_cast<uint32_t, FromVec>(mscclpp::to<FromVec>(acc));
+    }
+  }
+}
+
+// The conversions themselves: __fp8_e4m3(float) / __fp8_e5m2(float) and float(fp8) of every byte.
+__global__ void refFp8ConvertKernel(const float* in, size_t n, uint8_t* e4, uint8_t* e5, float* d4, float* d5) {
+  const size_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    e4[i] = __fp8_e4m3(in[i]).__x;
+    e5[i] = __fp8_e5m2(in[i]).__x;
+  }
+  if (i < 256) {
+    __fp8_e4m3 a;
+    a.__x = (__hip_fp8_storage_t)i;
+    __fp8_e5m2 b;
+    b.__x = (__hip_fp8_storage_t)i;
+    d4[i] = float(a);
+    d5[i] = float(b);
+  }
+}
+
 #define REF_DISPATCH(dtype, op, KERNEL, ...)                                         \
   do {                                                                               \
     int key = (dtype) * 2 + (op);                                                    \
@@ -95,6 +150,26 @@ int refSelfReduceLL16(int dtype, int op, const void* x, const void* y, void* pkt
   hipLaunchKernelGGL(refPackLL16, dim3(256), dim3(256), 0, (hipStream_t)stream, pkts, y, bytes, flag);
   REF_DISPATCH(dtype, op, refUnpackReduceLL16, dim3(256), dim3(256), 0, (hipStream_t)stream, (const void*)pkts,
                (const uint32_t*)x, (uint32_t*)out, bytes / 8, flag);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// dst = src[0] (op) ... (op) src[nsrc-1] (src: nsrc arrays of nwords words, back to back), fp8
+// reduce type dtype 5..10 (element e4m3/e5m2 x AccumT element/half/float).
+int refFp8Accum(int dtype, int op, const uint32_t* src, int nsrc, size_t nwords, uint32_t* out, void* stream) {
+  const int key = dtype * 2 + op;
+  hipStream_t s = (hipStream_t)stream;
+#define REF_FP8(D)                                                                                          \
+  if (key == D * 2) hipLaunchKernelGGL((refFp8AccumKernel<D, 0>), dim3(256), dim3(256), 0, s, src, nsrc, nwords, out); \
+  else if (key == D * 2 + 1) hipLaunchKernelGGL((refFp8AccumKernel<D, 1>), dim3(256), dim3(256), 0, s, src, nsrc, nwords, out);
+  REF_FP8(5) else REF_FP8(6) else REF_FP8(7) else REF_FP8(8) else REF_FP8(9) else REF_FP8(10) else return 4;
+#undef REF_FP8
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int refFp8Convert(const float* in, size_t n, uint8_t* e4, uint8_t* e5, float* d4, float* d5, void* stream) {
+  const size_t threads = n > 256 ? n : 256;
+  hipLaunchKernelGGL(refFp8ConvertKernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream, in, n, e4, e5,
+                     d4, d5);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

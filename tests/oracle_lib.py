@@ -8,7 +8,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
 
 F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
+# OCP fp8 reduce types: element type (e4m3 / e5m2) x accumulation type (element, half, float)
+E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32 = 5, 6, 7, 8, 9, 10
+FP8_TYPES = (E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32)
 SUM, MIN = 0, 1
+
+
+def itemsize(dtype):
+    return 2 if dtype in (F16, BF16) else (1 if dtype in FP8_TYPES else 4)
+
+
+def is_e5m2(dtype):
+    return dtype in (E5M2, E5M2_ACC_F16, E5M2_ACC_F32)
+
+
+def ll_words(dtype, count):
+    """32-bit words the LL kernels cover (allreduce_packet.cu:51-54 + the 1-byte deviation)."""
+    es = itemsize(dtype)
+    if es == 4:
+        return count
+    nbytes = count * es
+    w = (nbytes + es) // 4
+    return (nbytes + 3) // 4 if w * 4 < nbytes else w
 
 _L = None
 
@@ -28,6 +49,9 @@ def L():
             ("oracle_f16_min", [u16, u16], u16), ("oracle_bf16_min", [u16, u16], u16),
             ("oracle_f32_add", [u32, u32], u32), ("oracle_f32_min", [u32, u32], u32),
             ("oracle_reduce_words", [i32, i32, vp, vp, sz], None),
+            ("oracle_reduce_seq", [i32, i32, i32, vp, sz, vp], None),
+            ("oracle_fp8_encode_sat", [ctypes.c_float, i32], ctypes.c_uint8),
+            ("oracle_fp8_decode", [ctypes.c_uint8, i32], ctypes.c_float),
             ("oracle_ll16_pack", [vp, sz, u32, vp], None), ("oracle_ll16_unpack", [vp, sz, u32, vp], sz),
             ("oracle_ll8_pack", [vp, sz, u32, vp], None), ("oracle_ll8_unpack", [vp, sz, u32, vp], sz),
             ("oracle_self_reduce", [i32, i32, vp, vp, sz, u32, vp, vp], sz),
@@ -108,7 +132,7 @@ def allreduce_packet(dtype, op, inputs, count, flag, half_bytes):
 
 def allreduce_allpairs(dtype, op, inputs, count, flag, half_bytes):
     n = len(inputs)
-    W = (count * 2 + 2) // 4 if dtype in (F16, BF16) else count
+    W = ll_words(dtype, count)
     ins = [np.zeros(W + 4, np.uint32) for _ in range(n)]
     for r in range(n):
         src = np.ascontiguousarray(inputs[r]).view(np.uint8)
@@ -135,7 +159,23 @@ def trigger_encode(typ, dst_id, dst_off, src_id, src_off, nbytes, sem):
 
 
 def lcg(dtype, count, rank, seq):
-    itemsize = 2 if dtype in (F16, BF16) else 4
-    out = np.zeros(count * itemsize, np.uint8)
+    isz = itemsize(dtype)
+    out = np.zeros(count * isz, np.uint8)
     L().oracle_lcg_fill(dtype, count, rank, seq, _p(out))
-    return out.view(np.uint16 if itemsize == 2 else np.uint32)
+    return out.view({1: np.uint8, 2: np.uint16, 4: np.uint32}[isz])
+
+
+def reduce_seq(dtype, op, srcs):
+    """srcs[0] (op) srcs[1] (op) ... in order, accumulated in the reduce type's AccumT."""
+    srcs = [np.ascontiguousarray(a).view(np.uint32) for a in srcs]
+    out = np.zeros(srcs[0].size, np.uint32)
+    L().oracle_reduce_seq(dtype, op, len(srcs), _ptr_array(srcs), out.size, _p(out))
+    return out
+
+
+def fp8_decode(b, e5m2):
+    return L().oracle_fp8_decode(int(b), int(e5m2))
+
+
+def fp8_encode_sat(f, e5m2):
+    return int(L().oracle_fp8_encode_sat(float(f), int(e5m2)))

@@ -49,6 +49,10 @@ def test_self_reduce_matches_reference_device_code(built, ref, dt, op):
 
     nbytes = 1 << 20
     x, y = _words(nbytes // 4, 1), _words(nbytes // 4, 2)
+    # signed zeros in both orders (min(-0, +0) = -0 on the device)
+    x[:64], y[:64] = 0x80000000, 0
+    x[64:128], y[64:128] = 0, 0x80000000
+    x[128:192], y[128:192] = 0x80008000, 0x00000000
     xd, yd = _dev_words(x), _dev_words(y)
     # reference harness
     rpk = m.DeviceBuffer(2 * nbytes)
