@@ -12,6 +12,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "bootstrap.hpp"
@@ -185,11 +186,6 @@ struct ncclComm {
   // peer mappings opened through IPC: (peer, peer allocation base) -> mapped base here
   std::map<std::pair<int, uint64_t>, void*> opened;
   // registered output buffers: local allocation base -> per-peer mapped pointers of that buffer
-  struct Reg {
-    uint64_t bytes;
-    std::array<uint64_t, MSCCLPP_AMD_MAX_RANKS> peerBase;  // mapped peer allocation bases
-    std::array<uint64_t, MSCCLPP_AMD_MAX_RANKS> peerOffsetBase;
-  };
   std::map<std::pair<uint64_t, uint64_t>, std::array<void*, MSCCLPP_AMD_MAX_RANKS>> outRegs;
   std::mutex mu;
 
@@ -255,10 +251,20 @@ struct ncclComm {
     info("rank " + std::to_string(rank) + " scratch grown to " + std::to_string(want));
   }
 
+  // Peer pointers of `out` (the bulk kernels write results straight into every peer's output,
+  // allreduce_fullmesh.cu:110-113).  Cached per local (allocation, offset) like the reference's
+  // per-buffer context cache (algorithm.cc:52-60, keyed on the local buffer only): a repeated call
+  // on the same buffer costs no host round trip.  As in the reference, every rank must pass its
+  // matching buffer when a buffer is first used.
+  std::map<std::tuple<uint64_t, uint64_t, uint64_t>, std::array<void*, MSCCLPP_AMD_MAX_RANKS>> outPtrs;
+
   std::array<void*, MSCCLPP_AMD_MAX_RANKS> registerOutput(void* out) {
     void* base = nullptr;
     size_t sz = 0;
     HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)out));
+    const auto pkey = std::make_tuple((uint64_t)base, (uint64_t)sz, (uint64_t)((char*)out - (char*)base));
+    auto pit = outPtrs.find(pkey);
+    if (pit != outPtrs.end()) return pit->second;
     auto key = std::make_pair((uint64_t)base, (uint64_t)sz);
     auto it = outRegs.find(key);
     std::array<void*, MSCCLPP_AMD_MAX_RANKS> peersOfBase;
@@ -275,6 +281,7 @@ struct ncclComm {
     boot->allGather(&off, offs.data(), sizeof(off));
     std::array<void*, MSCCLPP_AMD_MAX_RANKS> res{};
     for (int r = 0; r < nranks; ++r) res[r] = (r == rank) ? out : (char*)peersOfBase[r] + offs[r];
+    outPtrs[pkey] = res;
     return res;
   }
 

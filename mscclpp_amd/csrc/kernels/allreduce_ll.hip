@@ -11,9 +11,13 @@
 //                    Every rank puts its whole buffer as LL8 packets into every peer's scratch and
 //                    reduces all n streams locally.
 //
-// gfx950 choices (vs. the reference's CUDA-shaped loops): one lane moves 16 payload bytes = two
-// LL16 packets (or four LL8 packets) as two 16-byte buffer stores with system-scope write-through
-// (sc0 sc1); polls are 16-byte system-scope loads issued for all peers before any spin; peer
+// Sums accumulate through Accum<DT, OP, 2> (reduce_device.hpp): the element type itself, or for
+// FP8 the half / float AccumT of calVectorAccum (allreduce_packet.cu:95-108).
+//
+// gfx950 choices (vs. the reference's CUDA-shaped loops): one lane moves one 16-byte unit (8
+// payload bytes = one LL16 packet or two LL8 packets) as a single buffer store with system-scope
+// write-through (sc0 sc1), so a wave writes 1 KiB of whole lines; polls are 16-byte system-scope
+// loads issued for all peers before any spin; peer
 // pointers come from kernel arguments (scalar loads), not from channel handles copied to LDS; loops
 // over peers are unrolled to the 8-GPU maximum with predicates so the per-peer values stay in VGPRs.
 #include "common.hpp"
@@ -98,10 +102,6 @@ __device__ __forceinline__ void payload_st(__amdgpu_buffer_rsrc_t r, uint8_t* ba
 #pragma unroll
   for (int i = 0; i < 8; ++i)
     if ((uint32_t)i < valid) base[off + i] = (uint8_t)((i < 4 ? v.x : v.y) >> ((i % 4) * 8));
-}
-template <int DT, int OP>
-__device__ __forceinline__ u32x2 reduce2(u32x2 a, u32x2 b) {
-  return u32x2{reduce_word<DT, OP>(a.x, b.x), reduce_word<DT, OP>(a.y, b.y)};
 }
 
 template <int DT, int OP, int NV>
