@@ -34,7 +34,8 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--bytes", type=int, default=48 << 20)
-    p.add_argument("--algo", default=None, help="force an AllReduce algorithm (N>1): packet|allpair|fullmesh|rsag")
+    p.add_argument("--algo", default=None,
+                   help="force an AllReduce algorithm (N>1): packet|allpair|fullmesh|rsag|rsag_zc")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="N>1: skip the LL latency sweep and the fp32 1 GiB run")
@@ -249,23 +250,29 @@ def bench_multi(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
-    # ---- pick the launch shape (untimed; every rank tries the same candidates in the same order)
-    algo = args.algo or {1: "packet", 2: "allpair", 3: "fullmesh", 4: "rsag"}[m.lib().mscclppAmdSelectAlgo(n, S, 0)]
-    if algo in ("fullmesh", "rsag"):
-        cands = [(64, 512), (32, 512), (128, 512), (64, 256), (128, 256)]
-    else:
-        cands = [(0, 0)]
+    # ---- pick the algorithm and launch shape (untimed; every rank tries the same candidates in the
+    # same order).  Large buckets: the scratch-based all-pairs RS+AG (fullmesh, puts) and the
+    # zero-copy RS+AG (reads peers' inputs, writes peers' outputs) -- which one drives xGMI better
+    # is measured here, on the node, not assumed.
+    sel = {1: "packet", 2: "allpair", 3: "fullmesh", 4: "rsag", 5: "rsag_zc"}[m.lib().mscclppAmdSelectAlgo(n, S, 0)]
+    algos = [args.algo] if args.algo else ([sel, "rsag_zc"] if sel == "fullmesh" else [sel])
+    cands = []
+    for a in algos:
+        if a in ("fullmesh", "rsag", "rsag_zc"):
+            cands += [(a, nb_, nt_) for nb_, nt_ in ((64, 512), (32, 512), (128, 512), (64, 256), (128, 256))]
+        else:
+            cands.append((a, 0, 0))
     tune = {}
-    for nb, nt in cands:
+    for a, nb, nt in cands:
         try:
             for _ in range(2):
-                comm.all_reduce(x, out, algo=algo, nblocks=nb, nthreads=nt)
-            tune[(nb, nt)] = tmax(_time_calls(lambda: comm.all_reduce(x, out, algo=algo, nblocks=nb, nthreads=nt), 5))
+                comm.all_reduce(x, out, algo=a, nblocks=nb, nthreads=nt)
+            tune[(a, nb, nt)] = tmax(_time_calls(lambda: comm.all_reduce(x, out, algo=a, nblocks=nb, nthreads=nt), 5))
         except Exception as e:  # a rejected shape is simply skipped
-            tune[(nb, nt)] = float("inf")
+            tune[(a, nb, nt)] = float("inf")
             if rank == 0:
-                print(f"tune {nb}x{nt}: {e}", file=sys.stderr)
-    nb, nt = min(tune, key=tune.get)
+                print(f"tune {a} {nb}x{nt}: {e}", file=sys.stderr)
+    algo, nb, nt = min(tune, key=tune.get)
 
     def step():
         comm.all_reduce(x, out, algo=algo, nblocks=nb, nthreads=nt)
@@ -298,9 +305,11 @@ def bench_multi(args):
     ok = bool(torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=5e-4 * n)) and errc == 0
     algbw = S / t / 1e9
     ceiling = n * XGMI_LINK_GBS / 2  # all-pairs algbw ceiling
-    # HBM bytes one rank's bulk AllReduce moves (reads S input + (n-1)/n S scratch; writes S/n own
-    # output + (n-1)/n S incoming scratch + (n-1)/n S incoming output)
-    hbm = S * (1 + 3 * (n - 1) / n + 1 / n)
+    # HBM bytes one rank's AllReduce moves.  fullmesh/rsag: reads S input + (n-1)/n S scratch;
+    # writes S/n own output + (n-1)/n S incoming scratch + (n-1)/n S incoming output.  rsag_zc: reads
+    # S of input (own slice locally, the rest by the peers), writes S of output (own slice locally,
+    # the rest by the peers).  LL paths: priced like fullmesh (their packets double the bytes).
+    hbm = 2 * S if algo == "rsag_zc" else S * (1 + 3 * (n - 1) / n + 1 / n)
     res = {
         "metric": "device-resident AllReduce algbw GB/s fp16 at 1/2/4/8 MI355X; % xGMI roofline",
         "value": round(algbw, 2),
@@ -320,9 +329,9 @@ def bench_multi(args):
         "xgmi": {"allpairs_algbw_ceiling": round(ceiling, 1), "frac": round(algbw / ceiling, 4),
                  "link_GBs_assumed": XGMI_LINK_GBS, "wire_bytes_per_rank": int(2 * (n - 1) * S / n)},
         "roofline": {"bound": "hbm", "achieved": round(hbm / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "traffic": None, "kernel": f"allreduceBulkKernel ({algo})",
+                     "unit": "GB/s", "traffic": None, "kernel": "allreduceZeroCopyKernel" if algo == "rsag_zc" else f"allreduceBulkKernel ({algo})",
                      "kernel_us": round(kern_ms * 1e3, 2), "algorithmic_bytes_per_launch": int(hbm)},
-        "tune_ms": {f"{k[0]}x{k[1]}": round(v * 1e3, 4) for k, v in tune.items()},
+        "tune_ms": {f"{k[0]}:{k[1]}x{k[2]}": round(v * 1e3, 4) for k, v in tune.items()},
         "correct": ok,
     }
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / HBM_PEAK_GBS, 4)

@@ -53,7 +53,9 @@ enum {
   MSCCLPP_AMD_ALGO_PACKET = 1,   /* default_allreduce_packet: LL16 two-hop (allreduce_packet.cu:15-151) */
   MSCCLPP_AMD_ALGO_ALLPAIR = 2,  /* default_allreduce_allpair_packet: LL8 one-hop (allreduce_allpair_packet.cu:15-69) */
   MSCCLPP_AMD_ALGO_FULLMESH = 3, /* default_allreduce_fullmesh: bulk all-pairs RS+AG (allreduce_fullmesh.cu:24-166) */
-  MSCCLPP_AMD_ALGO_RSAG = 4      /* default_allreduce_rsag: ring-order bulk RS+AG (allreduce_rsag.cu:33-128) */
+  MSCCLPP_AMD_ALGO_RSAG = 4,     /* default_allreduce_rsag: ring-order bulk RS+AG (allreduce_rsag.cu:33-128) */
+  MSCCLPP_AMD_ALGO_RSAG_ZC = 5   /* default_allreduce_rsag_zero_copy: reads peers' inputs, writes peers' outputs,
+                                    no scratch (allreduce_rsag_zero_copy.cu:41-112) */
 };
 
 /* One rank's view of the buffers of an AllReduce.  Pointers to other ranks' memory are the
@@ -73,6 +75,7 @@ typedef struct {
   uint64_t scratchBytes;
   int32_t rank;
   int32_t pad;
+  const void* peerInput[MSCCLPP_AMD_MAX_RANKS];    /* rank q's input as mapped here (zero-copy reads) */
 } mscclppAmdRankView;
 
 /* ---- memory ------------------------------------------------------------------------------- */

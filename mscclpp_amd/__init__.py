@@ -20,8 +20,8 @@ F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
 # OCP fp8 reduce types: element type x accumulation type (Algorithm::execute accumDtype)
 E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32 = 5, 6, 7, 8, 9, 10
 SUM, MIN = 0, 1
-ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG = 0, 1, 2, 3, 4
-ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4}
+ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC = 0, 1, 2, 3, 4, 5
+ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4, "rsag_zc": 5}
 MAX_RANKS = 8
 FLAG_SLOTS = 1024
 MAX_CHANNELS = 128
@@ -68,6 +68,7 @@ class RankView(ctypes.Structure):
         ("scratchBytes", ctypes.c_uint64),
         ("rank", ctypes.c_int32),
         ("pad", ctypes.c_int32),
+        ("peerInput", ctypes.c_void_p * MAX_RANKS),
     ]
 
 
@@ -227,6 +228,7 @@ class InProcessRanks:
             for q in range(self.n):
                 v.peerScratch[q] = scr[q].ptr
                 v.peerOutput[q] = outputs[q].data_ptr()
+                v.peerInput[q] = inputs[q].data_ptr()
                 v.peerTokens[q] = self.tokens[q].ptr
             v.tokens = self.tokens[r].ptr
             v.expected = self.expected[r].data_ptr()
@@ -240,7 +242,7 @@ class InProcessRanks:
                    accum=None):
         dt = reduce_code(inputs[0].dtype, accum)
         nbytes = inputs[0].numel() * inputs[0].element_size()
-        bulk = algo in (ALGO_FULLMESH, ALGO_RSAG)
+        bulk = algo in (ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC)
         arr = self.views(inputs, outputs, bulk=bulk)
         code = lib().mscclppAmdAllReduceLaunch(algo, arr, self.n, self.n, nbytes, dt, op, nblocks, nthreads,
                                                budget_ticks, stream_ptr(stream))

@@ -57,23 +57,26 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
     if (budgetTicks == 0) budgetTicks = spinBudgetTicks();
     // validate every pointer the kernel will dereference before launching (a fault here would
     // take the GPU down; a bad argument must come back as ncclInvalidArgument instead)
-    const bool bulk = algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG;
+    const bool zc = algo == MSCCLPP_AMD_ALGO_RSAG_ZC;
+    const bool bulk = algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG || zc;
     unsigned seen = 0;
     for (int i = 0; i < nviews; ++i) {
       const mscclppAmdRankView& v = views[i];
       if (v.rank < 0 || v.rank >= nranks || (seen >> v.rank) & 1u) return (int)ncclInvalidArgument;
       seen |= 1u << v.rank;
-      if (!v.input || !v.output || !v.scratch || !v.flags || !v.err || v.scratchBytes == 0) return (int)ncclInvalidArgument;
+      if (!v.input || !v.output || !v.flags || !v.err) return (int)ncclInvalidArgument;
+      if (!zc && (!v.scratch || v.scratchBytes == 0)) return (int)ncclInvalidArgument;
       for (int q = 0; q < nranks; ++q) {
-        if (!v.peerScratch[q]) return (int)ncclInvalidArgument;
+        if (!zc && !v.peerScratch[q]) return (int)ncclInvalidArgument;
         if (bulk && (!v.peerOutput[q] || !v.peerTokens[q])) return (int)ncclInvalidArgument;
+        if (zc && !v.peerInput[q]) return (int)ncclInvalidArgument;
       }
       if (bulk && (!v.tokens || !v.expected)) return (int)ncclInvalidArgument;
     }
     if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR)
       return launchAllReduceLL(algo, views, nviews, nranks, bytes, dtype, op, nblocks, nthreads, budgetTicks,
                                (hipStream_t)stream);
-    if (algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG)
+    if (bulk)
       return launchAllReduceBulk(algo, views, nviews, nranks, bytes, dtype, op, nblocks, nthreads, budgetTicks,
                                  (hipStream_t)stream);
     return (int)ncclInvalidArgument;
@@ -107,6 +110,7 @@ size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype) 
   if (algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG) {
     return bulkScratchRequired(nranks, bytes, (size_t)1 << 40, nullptr, 64);
   }
+  if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC) return 0;  // no scratch: peers' inputs are read in place
   return 0;
 }
 

@@ -153,6 +153,7 @@ inline int envAlgo() {
   if (s == "allpair" || s == "allpair_packet") return MSCCLPP_AMD_ALGO_ALLPAIR;
   if (s == "fullmesh") return MSCCLPP_AMD_ALGO_FULLMESH;
   if (s == "rsag") return MSCCLPP_AMD_ALGO_RSAG;
+  if (s == "rsag_zc" || s == "rsag_zero_copy") return MSCCLPP_AMD_ALGO_RSAG_ZC;
   return MSCCLPP_AMD_ALGO_AUTO;
 }
 
@@ -324,6 +325,17 @@ struct ncclComm {
       for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
       auto outs = registerOutput(out);
       for (int r = 0; r < nranks; ++r) v.peerOutput[r] = outs[r];
+      return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
+    }
+    if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC) {
+      // zero-copy: peers' inputs and outputs are mapped once per buffer (the reference registers
+      // both as remote memories, allreduce_rsag_zero_copy.cu:25-27); no scratch
+      auto outs = registerOutput(out);
+      auto ins = registerOutput(const_cast<void*>(in));
+      for (int r = 0; r < nranks; ++r) {
+        v.peerOutput[r] = outs[r];
+        v.peerInput[r] = ins[r];
+      }
       return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
     }
     return ncclInvalidArgument;

@@ -171,6 +171,70 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
   }
 }
 
+// Zero-copy RS+AG (allreduceRsAgZeroCopy, allreduce_rsag_zero_copy.cu:41-112): no scratch.  Each
+// rank reads its own slice straight out of every peer's input buffer over xGMI, sums in ring order
+// (own, r+1, r+2, ...; :90-96), and writes the result into its own output and every peer's output
+// (:101-106).  Per channel (= workgroup) one handshake at entry -- the peers' inputs are ready and
+// their previous call no longer reads mine or writes my output -- and one at exit, after every
+// wave has drained its remote stores, so each output is complete when the kernel ends.  xGMI bytes
+// per rank and direction equal fullmesh's (2*(n-1)/n*S); HBM traffic drops by the scratch
+// round trip.
+template <int DT, int OP, int NV>
+__global__ void __launch_bounds__(512) allreduceZeroCopyKernel(Views<NV> views, BulkGeom g, int nranks, uint64_t budget) {
+  const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
+  const int rank = v.rank;
+  const uint32_t T = blockDim.x, tid = threadIdx.x, b = blockIdx.x;
+  const uint64_t bOff = (uint64_t)b * g.blk;
+  uint64_t bLen = 0;
+  if (bOff < g.slice) bLen = (bOff + g.blk > g.slice) ? g.slice - bOff : g.blk;
+  const uint32_t nUnits = (uint32_t)((bLen + 15) / 16);
+  block_handshake(v, nranks, rank, b, budget);
+  const uint64_t myOff = (uint64_t)rank * g.slice + bOff;
+  if (nUnits && myOff < g.bytes) {
+    const uint64_t valid = g.bytes - myOff;
+    const uint8_t* myIn = (const uint8_t*)v.input + myOff;
+    uint8_t* myOut = (uint8_t*)v.output + myOff;
+    const auto rin = make_rsrc(myIn);
+    const auto rout = make_rsrc(myOut);
+    for (uint32_t u = tid; u < nUnits; u += T) {
+      const uint32_t vb = clamp_valid(valid, (uint64_t)u * 16, 16);
+      if (vb == 0) break;
+      const u32x4 own = load_payload<kNonTemporal>(rin, myIn, (uint64_t)u * 16, vb);
+      u32x4 w[kMaxRanks];
+#pragma unroll
+      for (int k = 1; k < kMaxRanks; ++k) {
+        if (k < nranks) {
+          const uint8_t* pin = (const uint8_t*)v.peerInput[(rank + k) % nranks] + myOff;
+          w[k] = vb >= 16 ? load16<kSystem>(make_rsrc(pin), u * 16u) : load_tail(pin + (uint64_t)u * 16, vb);
+        }
+      }
+      u32x4 acc;
+      if constexpr (AccWord<DT, OP>::kWide) {
+        Accum<DT, OP, 4> sum(own);
+#pragma unroll
+        for (int k = 1; k < kMaxRanks; ++k)
+          if (k < nranks) sum.add(w[k]);
+        acc = sum.template get<u32x4>();
+      } else {
+        acc = own;
+#pragma unroll
+        for (int k = 1; k < kMaxRanks; ++k)
+          if (k < nranks) acc = reduce4<DT, OP>(acc, w[k]);
+      }
+      store_payload<kPlain>(rout, myOut, (uint64_t)u * 16, acc, vb);
+#pragma unroll 1
+      for (int k = 1; k < nranks; ++k) {
+        uint8_t* po = (uint8_t*)v.peerOutput[(rank + k) % nranks] + myOff;
+        if (vb >= 16)
+          store16<kSystem>(make_rsrc(po), u * 16u, acc);
+        else
+          store_tail(po + (uint64_t)u * 16, acc, vb);
+      }
+    }
+  }
+  block_handshake(v, nranks, rank, b, budget);
+}
+
 static thread_local int g_launch_status = 0;
 
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks) {
@@ -230,11 +294,49 @@ static void launchBulk(const mscclppAmdRankView* views, int nviews, const BulkGe
 }
 
 // mode 0 AllReduce (bytes = whole buffer), 1 ReduceScatter / 2 AllGather (bytes = n * block, block % 16 == 0)
+template <int DT, int OP, int NV>
+static void launchZeroCopyT(const Views<NV>& vw, int nviews, const BulkGeom& g, int nranks, int nblocks, int nthreads,
+                            uint64_t budget, hipStream_t s) {
+  if (!grid_coresident(allreduceZeroCopyKernel<DT, OP, NV>, nthreads, (long)nblocks * nviews)) {
+    g_launch_status = 5;  // ncclInvalidUsage: handshakes of a non-resident grid would deadlock
+    return;
+  }
+  hipLaunchKernelGGL((allreduceZeroCopyKernel<DT, OP, NV>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks,
+                     budget);
+}
+
+template <int DT, int OP>
+static void launchZeroCopy(const mscclppAmdRankView* views, int nviews, const BulkGeom& g, int nranks, int nblocks,
+                           int nthreads, uint64_t budget, hipStream_t s) {
+  if (nviews == 1) {
+    Views<1> vw;
+    vw.v[0] = views[0];
+    launchZeroCopyT<DT, OP, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+  } else {
+    Views<kMaxRanks> vw{};
+    for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
+    launchZeroCopyT<DT, OP, kMaxRanks>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+  }
+}
+
 int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes,
                          int dtype, int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s) {
   if (nblocks <= 0) nblocks = 64;
   if (nthreads <= 0) nthreads = 512;
   if (nblocks > kMaxChannels || nthreads > 512 || nthreads % 64 || nthreads < 64) return 4;
+  if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC) {
+    if (mode != 0) return 4;
+    BulkGeom g{};
+    g.bytes = bytes;
+    g.slice = ((bytes + nranks - 1) / nranks + 15) & ~15ull;
+    g.pass = g.slice;
+    g.npasses = 1;
+    g.blk = ((g.slice + nblocks - 1) / nblocks + 15) & ~15ull;
+    g_launch_status = 0;
+    MSCCLPP_AMD_DISPATCH_ALL(dtype, op, launchZeroCopy, views, nviews, g, nranks, nblocks, nthreads, budget, s);
+    if (g_launch_status) return g_launch_status;
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+  }
   if (mode != 0 && (bytes % ((size_t)16 * nranks))) return 5;
   BulkGeom g{};
   if (!bulkScratchRequired(nranks, bytes, views[0].scratchBytes, &g, nblocks)) return 5;

@@ -88,13 +88,14 @@ def test_ll_allreduce_bit_exact(built, algo, n, dt, count, special):
                 assert np.array_equal(got, scr[r]), f"scratch image of rank {r}"
 
 
-@pytest.mark.parametrize("algo,order", [("fullmesh", 0), ("rsag", 1)])
+@pytest.mark.parametrize("algo,order", [("fullmesh", 0), ("rsag", 1), ("rsag_zc", 1)])
 @pytest.mark.parametrize("n,dt,count", [(2, O.F16, 1 << 16), (8, O.F16, 1 << 18), (8, O.F32, 100000),
-                                        (4, O.BF16, 65536 + 8), (8, O.I32, 4096), (7, O.F32, 12345)])
+                                        (4, O.BF16, 65536 + 8), (8, O.I32, 4096), (7, O.F32, 12345),
+                                        (8, O.F16, 1001)])
 def test_bulk_allreduce_bit_exact(built, algo, order, n, dt, count):
     import mscclpp_amd as m
 
-    algo_code = m.ALGO_FULLMESH if algo == "fullmesh" else m.ALGO_RSAG
+    algo_code = m.ALGO_NAMES[algo]
     nbytes = count * ITEM[dt]
     slice_bytes = ((nbytes + n - 1) // n + 15) // 16 * 16
     ranks = m.InProcessRanks(n, 1 << 16, bulk_scratch_bytes=max(n * slice_bytes, 1 << 20))
@@ -116,12 +117,12 @@ def test_bulk_allreduce_bit_exact(built, algo, order, n, dt, count):
             _cmp(_bytes(douts[r]), exp[r].view(np.uint8)[:nbytes], dt)
 
 
-@pytest.mark.parametrize("algo", ["packet", "allpair", "fullmesh"])
+@pytest.mark.parametrize("algo", ["packet", "allpair", "fullmesh", "rsag_zc"])
 def test_in_place(built, algo):
     import mscclpp_amd as m
 
     n, dt, count = 8, O.F16, 8192
-    code = {"packet": m.ALGO_PACKET, "allpair": m.ALGO_ALLPAIR, "fullmesh": m.ALGO_FULLMESH}[algo]
+    code = m.ALGO_NAMES[algo]
     nbytes = count * 2
     ranks = m.InProcessRanks(n, max(m.scratch_required(code, n, nbytes, dt), 1 << 16), bulk_scratch_bytes=1 << 20)
     ins = _inputs(dt, n, count)
@@ -129,9 +130,10 @@ def test_in_place(built, algo):
     ranks.all_reduce(bufs, bufs, code, nblocks=(n - 1) * 2 if code == m.ALGO_PACKET else 8, nthreads=256)
     torch.cuda.synchronize()
     assert ranks.errors() == [0] * n
-    if code == m.ALGO_FULLMESH:
+    if code in (m.ALGO_FULLMESH, m.ALGO_RSAG_ZC):
         sl = ((nbytes + n - 1) // n + 15) // 16 * 16
-        exp = O.allreduce_sliced(dt, O.SUM, [a.view(np.uint32) for a in ins], nbytes // 4, sl // 4, 0)
+        exp = O.allreduce_sliced(dt, O.SUM, [a.view(np.uint32) for a in ins], nbytes // 4, sl // 4,
+                                 0 if code == m.ALGO_FULLMESH else 1)
     elif code == m.ALGO_PACKET:
         exp, _ = O.allreduce_packet(dt, O.SUM, ins, count, 1, 1 << 20)
     else:
@@ -145,7 +147,8 @@ def test_int32_kat(built):
     import mscclpp_amd as m
 
     n = 8
-    for code, nb in ((m.ALGO_ALLPAIR, 4), (m.ALGO_PACKET, 14), (m.ALGO_FULLMESH, 8), (m.ALGO_RSAG, 8)):
+    for code, nb in ((m.ALGO_ALLPAIR, 4), (m.ALGO_PACKET, 14), (m.ALGO_FULLMESH, 8), (m.ALGO_RSAG, 8),
+                     (m.ALGO_RSAG_ZC, 8)):
         count = 1 << 14
         ranks = m.InProcessRanks(n, max(m.scratch_required(code, n, count * 4, O.I32), 1 << 16),
                                  bulk_scratch_bytes=1 << 20)

@@ -184,13 +184,13 @@ def test_fp8_ll_allreduce_bit_exact(built, algo, n, dt, count):
                 assert np.array_equal(img, scr[r]), f"scratch image of rank {r}"
 
 
-@pytest.mark.parametrize("algo,order", [("fullmesh", 0), ("rsag", 1)])
+@pytest.mark.parametrize("algo,order", [("fullmesh", 0), ("rsag", 1), ("rsag_zc", 1)])
 @pytest.mark.parametrize("n,dt,count", [(8, O.E4M3, 1 << 18), (8, O.E5M2_ACC_F32, 100000), (4, O.E4M3_ACC_F16, 65536 + 16),
                                         (7, O.E5M2, 12345), (8, O.E4M3_ACC_F32, 4096)])
 def test_fp8_bulk_allreduce_bit_exact(built, algo, order, n, dt, count):
     import mscclpp_amd as m
 
-    code = m.ALGO_FULLMESH if algo == "fullmesh" else m.ALGO_RSAG
+    code = m.ALGO_NAMES[algo]
     slice_bytes = ((count + n - 1) // n + 15) // 16 * 16
     ranks = m.InProcessRanks(n, 1 << 16, bulk_scratch_bytes=max(n * slice_bytes, 1 << 20))
     for call in range(2):
