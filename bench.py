@@ -259,7 +259,7 @@ def bench_multi(args):
     cands = []
     for a in algos:
         if a in ("fullmesh", "rsag", "rsag_zc"):
-            cands += [(a, nb_, nt_) for nb_, nt_ in ((64, 512), (32, 512), (128, 512), (64, 256), (128, 256))]
+            cands += [(a, nb_, nt_) for nb_, nt_ in ((64, 512), (128, 512), (256, 512), (128, 256), (256, 256))]
         else:
             cands.append((a, 0, 0))
     tune = {}

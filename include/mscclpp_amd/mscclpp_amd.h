@@ -28,7 +28,7 @@ extern "C" {
 
 #define MSCCLPP_AMD_MAX_RANKS 8
 #define MSCCLPP_AMD_FLAG_SLOTS 1024
-#define MSCCLPP_AMD_MAX_CHANNELS 128
+#define MSCCLPP_AMD_MAX_CHANNELS 256
 
 /* dtype / op codes of the extension API (ncclDataType_t / ncclRedOp_t are mapped onto these) */
 enum { MSCCLPP_AMD_F16 = 0, MSCCLPP_AMD_BF16 = 1, MSCCLPP_AMD_F32 = 2, MSCCLPP_AMD_I32 = 3, MSCCLPP_AMD_U32 = 4 };
@@ -54,8 +54,12 @@ enum {
   MSCCLPP_AMD_ALGO_ALLPAIR = 2,  /* default_allreduce_allpair_packet: LL8 one-hop (allreduce_allpair_packet.cu:15-69) */
   MSCCLPP_AMD_ALGO_FULLMESH = 3, /* default_allreduce_fullmesh: bulk all-pairs RS+AG (allreduce_fullmesh.cu:24-166) */
   MSCCLPP_AMD_ALGO_RSAG = 4,     /* default_allreduce_rsag: ring-order bulk RS+AG (allreduce_rsag.cu:33-128) */
-  MSCCLPP_AMD_ALGO_RSAG_ZC = 5   /* default_allreduce_rsag_zero_copy: reads peers' inputs, writes peers' outputs,
+  MSCCLPP_AMD_ALGO_RSAG_ZC = 5,  /* default_allreduce_rsag_zero_copy: reads peers' inputs, writes peers' outputs,
                                     no scratch (allreduce_rsag_zero_copy.cu:41-112) */
+  /* the int32 kernels of the mscclpp-test harness (test/mscclpp-test/allreduce_test.cu), by number */
+  MSCCLPP_AMD_ALGO_TEST_K5 = 105, /* allreduce5 (AMD branch): in-place RS by remote reads + ring AG by gets (:959-970) */
+  MSCCLPP_AMD_ALGO_TEST_K6 = 106, /* allreduce6: LL16 two-hop, harness scratch layout (:972-1034) */
+  MSCCLPP_AMD_ALGO_TEST_K7 = 107  /* allreduce7: LL8 two-hop, harness scratch layout (:1036-1093) */
 };
 
 /* One rank's view of the buffers of an AllReduce.  Pointers to other ranks' memory are the

@@ -21,10 +21,12 @@ F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
 E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32 = 5, 6, 7, 8, 9, 10
 SUM, MIN = 0, 1
 ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC = 0, 1, 2, 3, 4, 5
-ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4, "rsag_zc": 5}
+ALGO_TEST_K5, ALGO_TEST_K6, ALGO_TEST_K7 = 105, 106, 107  # mscclpp-test allreduce5 / 6 / 7 (int32)
+ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4, "rsag_zc": 5,
+              "k5": ALGO_TEST_K5, "k6": ALGO_TEST_K6, "k7": ALGO_TEST_K7}
 MAX_RANKS = 8
 FLAG_SLOTS = 1024
-MAX_CHANNELS = 128
+MAX_CHANNELS = 256
 
 # ncclDataType_t / ncclRedOp_t (include/mscclpp_amd/nccl.h, values of the reference nccl.h:217-253)
 NCCL_DTYPES = {torch.float16: 6, torch.bfloat16: 9, torch.float32: 7, torch.int32: 2,
@@ -218,6 +220,8 @@ class InProcessRanks:
 
     def views(self, inputs, outputs, bulk=False):
         arr = (RankView * self.n)()
+        if bulk and self.bulk is None:  # zero-copy kernels (rsag_zc, k5) need no bulk scratch
+            bulk = False
         scr = self.bulk if bulk else self.scratch
         sbytes = self.bulk_bytes if bulk else self.scratch_bytes
         for r in range(self.n):
@@ -242,7 +246,7 @@ class InProcessRanks:
                    accum=None):
         dt = reduce_code(inputs[0].dtype, accum)
         nbytes = inputs[0].numel() * inputs[0].element_size()
-        bulk = algo in (ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC)
+        bulk = algo in (ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC, ALGO_TEST_K5)
         arr = self.views(inputs, outputs, bulk=bulk)
         code = lib().mscclppAmdAllReduceLaunch(algo, arr, self.n, self.n, nbytes, dt, op, nblocks, nthreads,
                                                budget_ticks, stream_ptr(stream))

@@ -57,8 +57,11 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
     if (budgetTicks == 0) budgetTicks = spinBudgetTicks();
     // validate every pointer the kernel will dereference before launching (a fault here would
     // take the GPU down; a bad argument must come back as ncclInvalidArgument instead)
-    const bool zc = algo == MSCCLPP_AMD_ALGO_RSAG_ZC;
+    const bool k5 = algo == MSCCLPP_AMD_ALGO_TEST_K5;
+    const bool zc = algo == MSCCLPP_AMD_ALGO_RSAG_ZC || k5;  // no scratch: peers' user buffers directly
     const bool bulk = algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG || zc;
+    const bool ll = algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR ||
+                    algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7;
     unsigned seen = 0;
     for (int i = 0; i < nviews; ++i) {
       const mscclppAmdRankView& v = views[i];
@@ -69,11 +72,11 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
       for (int q = 0; q < nranks; ++q) {
         if (!zc && !v.peerScratch[q]) return (int)ncclInvalidArgument;
         if (bulk && (!v.peerOutput[q] || !v.peerTokens[q])) return (int)ncclInvalidArgument;
-        if (zc && !v.peerInput[q]) return (int)ncclInvalidArgument;
+        if (zc && !k5 && !v.peerInput[q]) return (int)ncclInvalidArgument;
       }
       if (bulk && (!v.tokens || !v.expected)) return (int)ncclInvalidArgument;
     }
-    if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR)
+    if (ll)
       return launchAllReduceLL(algo, views, nviews, nranks, bytes, dtype, op, nblocks, nthreads, budgetTicks,
                                (hipStream_t)stream);
     if (bulk)
@@ -110,7 +113,8 @@ size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype) 
   if (algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG) {
     return bulkScratchRequired(nranks, bytes, (size_t)1 << 40, nullptr, 64);
   }
-  if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC) return 0;  // no scratch: peers' inputs are read in place
+  if (algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7) return testLLScratchRequired(nranks, bytes);
+  if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC || algo == MSCCLPP_AMD_ALGO_TEST_K5) return 0;  // peers' buffers read in place
   return 0;
 }
 

@@ -28,6 +28,7 @@ int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, i
                         int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
 size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype);
 size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype);
+size_t testLLScratchRequired(int nranks, size_t bytes);
 struct BulkGeom;
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks);
 }  // namespace mscclpp_amd
@@ -305,9 +306,12 @@ struct ncclComm {
     if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = envAlgo();
     if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = mscclppAmdSelectAlgo(nranks, bytes, dtype);
     mscclppAmdRankView v = baseView(in, out);
-    if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR) {
-      const size_t need = algo == MSCCLPP_AMD_ALGO_PACKET ? ll16ScratchRequired(nranks, bytes, dtype)
-                                                          : ll8ScratchRequired(nranks, bytes, dtype);
+    if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR || algo == MSCCLPP_AMD_ALGO_TEST_K6 ||
+        algo == MSCCLPP_AMD_ALGO_TEST_K7) {
+      const size_t need = algo == MSCCLPP_AMD_ALGO_PACKET    ? ll16ScratchRequired(nranks, bytes, dtype)
+                          : algo == MSCCLPP_AMD_ALGO_ALLPAIR ? ll8ScratchRequired(nranks, bytes, dtype)
+                                                             : testLLScratchRequired(nranks, bytes);
+      if (need == 0) return ncclInvalidUsage;
       ensure(llScratch, llBytes, peerLL, need);
       v.scratch = llScratch;
       v.scratchBytes = llBytes;
@@ -325,6 +329,15 @@ struct ncclComm {
       for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
       auto outs = registerOutput(out);
       for (int r = 0; r < nranks; ++r) v.peerOutput[r] = outs[r];
+      return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
+    }
+    if (algo == MSCCLPP_AMD_ALGO_TEST_K5) {
+      if (in != out) {
+        warn("mscclpp-test kernel 5 runs in place (sendbuff == recvbuff)");
+        return ncclInvalidUsage;
+      }
+      auto bufs = registerOutput(out);
+      for (int r = 0; r < nranks; ++r) v.peerOutput[r] = bufs[r];
       return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
     }
     if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC) {

@@ -235,6 +235,58 @@ __global__ void __launch_bounds__(512) allreduceZeroCopyKernel(Views<NV> views, 
   block_handshake(v, nranks, rank, b, budget);
 }
 
+// mscclpp-test allreduce5, AMD branch (test/mscclpp-test/allreduce_test.cu:959-970 ->
+// localReduceScatterMem3 :375-435, localRingAllGatherMem2 :586-617): in place on the user buffer,
+// no scratch.  Reduce-scatter: rank r adds chunk r of every peer's buffer (remote reads, channel
+// order (i + r) % nPeers, :402-404) into its own chunk r; all-gather: rank r gets chunk q out of
+// rank q's buffer (same channel order, :604-608).  The reference gates each phase with one
+// signal/wait per peer plus a grid-wide DeviceSyncer; here each workgroup owns the same sub-range
+// of every chunk in both phases and handshakes only with the peers' workgroup of the same index --
+// at entry, between the phases (a peer overwrites its copy of my chunk only in its all-gather,
+// after I have read it) and at exit (peers have finished reading my buffer when my kernel ends).
+template <int DT, int OP, int NV>
+__global__ void __launch_bounds__(512) allreduceTestK5Kernel(Views<NV> views, BulkGeom g, int nranks, uint64_t budget) {
+  const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
+  const int rank = v.rank;
+  const int nPeers = nranks - 1;
+  const uint32_t T = blockDim.x, tid = threadIdx.x, b = blockIdx.x;
+  const uint64_t bOff = (uint64_t)b * g.blk;
+  uint64_t bLen = 0;
+  if (bOff < g.slice) bLen = (bOff + g.blk > g.slice) ? g.slice - bOff : g.blk;
+  const uint32_t nUnits = (uint32_t)(bLen / 16);  // the host keeps chunks a multiple of 16 bytes
+  uint8_t* buf = (uint8_t*)v.output;
+  auto peerOf = [&](int i) {  // channel (i + rank) % nPeers -> its rank
+    const int c = (i + rank) % nPeers;
+    return c < rank ? c : c + 1;
+  };
+  block_handshake(v, nranks, rank, b, budget);
+  {
+    const uint64_t off = (uint64_t)rank * g.slice + bOff;
+    const auto rb = make_rsrc(buf + off);
+    for (uint32_t u = tid; u < nUnits; u += T) {
+      u32x4 w[kMaxRanks];
+#pragma unroll
+      for (int i = 0; i < kMaxRanks - 1; ++i)
+        if (i < nPeers) w[i] = load16<kSystem>(make_rsrc((const uint8_t*)v.peerOutput[peerOf(i)] + off), u * 16u);
+      u32x4 acc = load16<kPlain>(rb, u * 16u);
+#pragma unroll
+      for (int i = 0; i < kMaxRanks - 1; ++i)
+        if (i < nPeers) acc = reduce4<DT, OP>(acc, w[i]);
+      store16<kPlain>(rb, u * 16u, acc);
+    }
+  }
+  block_handshake(v, nranks, rank, b, budget);
+#pragma unroll 1
+  for (int i = 0; i < nPeers; ++i) {
+    const int q = peerOf(i);
+    const uint64_t off = (uint64_t)q * g.slice + bOff;
+    const auto rsrc = make_rsrc((const uint8_t*)v.peerOutput[q] + off);
+    const auto rdst = make_rsrc(buf + off);
+    for (uint32_t u = tid; u < nUnits; u += T) store16<kPlain>(rdst, u * 16u, load16<kSystem>(rsrc, u * 16u));
+  }
+  block_handshake(v, nranks, rank, b, budget);
+}
+
 static thread_local int g_launch_status = 0;
 
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks) {
@@ -324,6 +376,50 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
   if (nblocks <= 0) nblocks = 64;
   if (nthreads <= 0) nthreads = 512;
   if (nblocks > kMaxChannels || nthreads > 512 || nthreads % 64 || nthreads < 64) return 4;
+  if (algo == MSCCLPP_AMD_ALGO_TEST_K5) {
+    // (the harness launches 24 x 1024, allreduce_test.cu:1126-1129; here the channel defaults apply)
+    if (mode != 0 || (dtype != kI32 && dtype != kU32)) return 4;
+    if (bytes % ((size_t)16 * nranks)) return 5;  // chunks of whole 16-byte units (reference: 4 * worldSize)
+    for (int i = 0; i < nviews; ++i)
+      if (views[i].input != views[i].output) return 5;  // allreduce5 runs in place (isInPlace, :1262-1264)
+    BulkGeom g{};
+    g.bytes = bytes;
+    g.slice = bytes / nranks;
+    g.pass = g.slice;
+    g.npasses = 1;
+    g.blk = ((g.slice + nblocks - 1) / nblocks + 15) & ~15ull;
+    g_launch_status = 0;
+    auto go = [&](auto kern) {
+      if (!grid_coresident(kern, nthreads, (long)nblocks * nviews)) {
+        g_launch_status = 5;
+        return;
+      }
+      if (nviews == 1) {
+        Views<1> vw;
+        vw.v[0] = views[0];
+        hipLaunchKernelGGL(kern, dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
+      }
+    };
+    auto goN = [&](auto kern) {
+      if (!grid_coresident(kern, nthreads, (long)nblocks * nviews)) {
+        g_launch_status = 5;
+        return;
+      }
+      Views<kMaxRanks> vw{};
+      for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
+      hipLaunchKernelGGL(kern, dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
+    };
+    const bool u32 = dtype == kU32, mn = op == kMin;
+    if (nviews == 1) {
+      if (u32) mn ? go(allreduceTestK5Kernel<kU32, kMin, 1>) : go(allreduceTestK5Kernel<kU32, kSum, 1>);
+      else mn ? go(allreduceTestK5Kernel<kI32, kMin, 1>) : go(allreduceTestK5Kernel<kI32, kSum, 1>);
+    } else {
+      if (u32) mn ? goN(allreduceTestK5Kernel<kU32, kMin, kMaxRanks>) : goN(allreduceTestK5Kernel<kU32, kSum, kMaxRanks>);
+      else mn ? goN(allreduceTestK5Kernel<kI32, kMin, kMaxRanks>) : goN(allreduceTestK5Kernel<kI32, kSum, kMaxRanks>);
+    }
+    if (g_launch_status) return g_launch_status;
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+  }
   if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC) {
     if (mode != 0) return 4;
     BulkGeom g{};

@@ -27,9 +27,11 @@ namespace mscclpp_amd {
 struct LL16Geom {
   uint64_t bytes;   // payload bytes actually in the buffers
   uint64_t W;       // 32-bit words the algorithm covers (allreduce_packet.cu:51-54)
-  uint64_t wpr;     // words per rank slice, even (:62-63)
-  uint64_t ppr;     // packets per rank slice
-  uint64_t roff;    // byte offset of the reduced-slice region inside a scratch half (:74)
+  uint64_t wpr;     // words per rank slice (even for allreducePacket, :62-63)
+  uint64_t ppr;     // 16-byte packet units per rank slice = wpr / 2
+  uint64_t roff;    // byte offset of the reduced-slice region from the input region (:74)
+  uint64_t hbOdd;   // scratch byte offset of the input region when the flag is odd (:60: half)
+  uint64_t hbEven;  // ... when the flag is even (:60: 0)
   uint32_t units;   // packets per slice (= ppr)
   uint32_t pad;
 };
@@ -111,13 +113,18 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
   const int nPeers = nranks - 1;
   const uint32_t T = blockDim.x, tid = threadIdx.x, G = gridDim.x, b = blockIdx.x;
   const uint32_t flag = v.flags[b];
-  const uint64_t base = (flag & 1u) ? v.scratchBytes / 2 : 0;  // numScratchBuff = 2 (allreduce_packet.cu:60)
+  const uint64_t base = (flag & 1u) ? g.hbOdd : g.hbEven;  // numScratchBuff = 2 (allreduce_packet.cu:60)
   const uint8_t* in = (const uint8_t*)v.input;
   uint8_t* out = (uint8_t*)v.output;
   uint8_t* scr = (uint8_t*)v.scratch + base;
   const auto rin = make_rsrc(in);
   const auto rout = make_rsrc(out);
   const uint64_t sliceBytes = g.wpr * 4;
+  // bytes of slice q inside the buffer: the unit at byte `off` of it may carry `valid` of them
+  auto sliceEnd = [&](int q) {
+    const uint64_t e = (uint64_t)(q + 1) * sliceBytes;
+    return e < g.bytes ? e : g.bytes;
+  };
   const uint32_t npk = (uint32_t)g.ppr;          // packets (units) per slice
   const uint32_t bpp = G / (uint32_t)nPeers;     // blocks per peer for steps 1 and 3
   const bool inPeerGroup = b < bpp * (uint32_t)nPeers;
@@ -129,9 +136,10 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
   if (inPeerGroup) {
     const auto rdst = make_rsrc((uint8_t*)v.peerScratch[remote] + base + (uint64_t)rank * g.ppr * 16);
     const uint64_t soff = (uint64_t)remote * sliceBytes;
+    const uint64_t send = sliceEnd(remote);
     for (uint32_t j = lb * T + tid; j < npk; j += bpp * T) {
       const uint64_t off = soff + (uint64_t)j * 8;
-      unit_put<kSystem>(rdst, j * 16u, payload_ld(rin, in, off, clamp_valid(g.bytes, off, 8)), flag, false);
+      unit_put<kSystem>(rdst, j * 16u, payload_ld(rin, in, off, clamp_valid(send, off, 8)), flag, false);
     }
   }
 
@@ -140,9 +148,10 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
   {
     const auto rscr = make_rsrc(scr);
     const uint64_t soff = (uint64_t)rank * sliceBytes;
+    const uint64_t send = sliceEnd(rank);
     for (uint32_t j = b * T + tid; j < npk; j += G * T) {
       const uint64_t off = soff + (uint64_t)j * 8;
-      const uint32_t valid = clamp_valid(g.bytes, off, 8);
+      const uint32_t valid = clamp_valid(send, off, 8);
       Accum<DT, OP, 2> sum(payload_ld(rin, in, off, valid));  // upcastVector (:98-99)
       u32x2 w[kMaxRanks];
       bool ready = true;
@@ -175,10 +184,11 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
   if (inPeerGroup) {
     const auto rres = make_rsrc(scr + g.roff + (uint64_t)remote * g.ppr * 16);
     const uint64_t soff = (uint64_t)remote * sliceBytes;
+    const uint64_t send = sliceEnd(remote);
     for (uint32_t j = lb * T + tid; j < npk; j += bpp * T) {
       const uint64_t off = soff + (uint64_t)j * 8;
       const u32x2 w = unit_get(rres, j * 16u, flag, false, budget, v.err);
-      payload_st(rout, out, off, w, clamp_valid(g.bytes, off, 8));
+      payload_st(rout, out, off, w, clamp_valid(send, off, 8));
     }
   }
   bump_flags(v.flags, flag);
@@ -279,6 +289,36 @@ static LL8Geom ll8Geometry(size_t bytes, int dtype) {
   return g;
 }
 
+// mscclpp-test kernels 6 / 7 (test/mscclpp-test/allreduce_test.cu:972-1093): the same two-hop
+// algorithm on int32 with the harness's own scratch layout -- no slice rounding
+// (nelemsPerRank = nelems / worldSize), input region at packet (flag & 1 ? 0 : nPkts) and result
+// region at (flag & 1 ? 2 : 3) * nPkts (:987-991, :1048-1051).  k7 moves LL8 packets; two
+// consecutive LL8 packets are byte-identical to one LL16 packet of the same payload, and k7's
+// offsets in 8-byte packets equal k6's in 16-byte packets, so with an even nelemsPerRank both
+// scratch images are exactly those of this kernel.  Restriction (checked by the host): bytes is a
+// multiple of 8 * nranks.
+static bool testLLGeometry(int nranks, size_t bytes, LL16Geom* out) {
+  if (bytes == 0 || bytes % (8 * (size_t)nranks)) return false;
+  LL16Geom g{};
+  g.bytes = bytes;
+  g.W = bytes / 4;
+  g.wpr = g.W / nranks;
+  g.ppr = g.wpr / 2;
+  const uint64_t nPkts = g.W / 2;
+  g.roff = 2 * nPkts * 16;
+  g.hbOdd = 0;
+  g.hbEven = nPkts * 16;
+  g.units = (uint32_t)g.ppr;
+  *out = g;
+  return true;
+}
+
+size_t testLLScratchRequired(int nranks, size_t bytes) {
+  LL16Geom g;
+  if (!testLLGeometry(nranks, bytes, &g)) return 0;
+  return 4 * (g.W / 2) * 16;  // nPacket * 2 (data, result) * 2 (double buffering), :1282-1286
+}
+
 size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype) {
   LL16Geom g = ll16Geometry(nranks, bytes, dtype);
   if (g.W == 0) return 0;
@@ -377,11 +417,27 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
   if (algo == MSCCLPP_AMD_ALGO_PACKET) {
     ll16Defaults(nranks, bytes, nblocks, nthreads);
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
-    const LL16Geom g = ll16Geometry(nranks, bytes, dtype);
+    LL16Geom g = ll16Geometry(nranks, bytes, dtype);
     if (g.W == 0) return 4;
     for (int i = 0; i < nviews; ++i)
-      if (views[i].scratchBytes < ll16ScratchRequired(nranks, bytes, dtype)) return 5;
+      if (views[i].scratchBytes != views[0].scratchBytes || views[i].scratchBytes < ll16ScratchRequired(nranks, bytes, dtype))
+        return 5;
+    g.hbOdd = views[0].scratchBytes / 2;  // (flag % numScratchBuff) ? scratchBufferSize / 2 : 0 (:60)
+    g.hbEven = 0;
     MSCCLPP_AMD_DISPATCH_ALL(dtype, op,launchLL16, views, nviews, g, nranks, nblocks, nthreads, budget, s);
+  } else if (algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7) {
+    // harness defaults (allreduce_test.cu:1134-1141): k6 21 x 512, k7 28 x 1024 -> 512-lane waves here
+    if (nthreads <= 0) nthreads = 512;
+    if (nblocks <= 0) nblocks = algo == MSCCLPP_AMD_ALGO_TEST_K6 ? 21 : 28;
+    nblocks = nblocks / (nranks - 1) * (nranks - 1);
+    if (nblocks < nranks - 1) nblocks = nranks - 1;
+    if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
+    if (dtype != kI32 && dtype != kU32) return 4;  // the mscclpp-test kernels are int32 AllReduces
+    LL16Geom g;
+    if (!testLLGeometry(nranks, bytes, &g)) return 5;
+    for (int i = 0; i < nviews; ++i)
+      if (views[i].scratchBytes < testLLScratchRequired(nranks, bytes)) return 5;
+    MSCCLPP_AMD_DISPATCH(dtype, op, launchLL16, views, nviews, g, nranks, nblocks, nthreads, budget, s);
   } else {
     ll8Defaults(nranks, bytes, nblocks, nthreads);
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;

@@ -490,6 +490,39 @@ void oracle_allreduce_packet(int dtype, int op, int n, const uint32_t* const* in
   free(tmp);
 }
 
+/* mscclpp-test allreduce6 / allreduce7 (test/mscclpp-test/allreduce_test.cu:972-1093), int32.
+ * nelemsPerRank = nelems / n (the host requires it even); 16-byte packets in the harness layout:
+ * input region at packet (flag & 1 ? 0 : nPkts), result region at packet (flag & 1 ? 2 : 3) * nPkts
+ * (:987-991; k7's 8-byte LL8 packets at (flag & 1 ? 0 : nelems) etc. are the same bytes, :1048-1051).
+ * Sum: 0 + peers ascending + own (:999-1010), wrapping int32 adds. */
+void oracle_mscclpp_test_ll(int n, const uint32_t* const* in, uint64_t nelems, uint32_t flag,
+                            uint32_t* const* scratch, uint32_t* const* out) {
+  uint64_t nPkts = nelems / 2, epr = nelems / (uint64_t)n, ppr = epr / 2;
+  uint64_t inBase = (flag & 1u) ? 0 : nPkts, resBase = (flag & 1u) ? 2 * nPkts : 3 * nPkts;
+  for (int s = 0; s < n; s++) /* step 1 */
+    for (int q = 0; q < n; q++)
+      if (q != s) oracle_ll16_pack(in[s] + (uint64_t)q * epr, ppr, flag, scratch[q] + (inBase + (uint64_t)s * ppr) * 4);
+  uint32_t* tmp = (uint32_t*)malloc(epr * 4 + 8);
+  uint32_t* acc = (uint32_t*)malloc(epr * 4 + 8);
+  for (int r = 0; r < n; r++) { /* step 2 */
+    memset(acc, 0, epr * 4);
+    for (int p = 0; p < n; p++) {
+      if (p == r) continue;
+      oracle_ll16_unpack(scratch[r] + (inBase + (uint64_t)p * ppr) * 4, ppr, flag, tmp);
+      for (uint64_t i = 0; i < epr; i++) acc[i] += tmp[i];
+    }
+    for (uint64_t i = 0; i < epr; i++) acc[i] += in[r][(uint64_t)r * epr + i];
+    memcpy(out[r] + (uint64_t)r * epr, acc, epr * 4);
+    for (int q = 0; q < n; q++)
+      if (q != r) oracle_ll16_pack(acc, ppr, flag, scratch[q] + (resBase + (uint64_t)r * ppr) * 4);
+  }
+  for (int r = 0; r < n; r++) /* step 3 */
+    for (int p = 0; p < n; p++)
+      if (p != r) oracle_ll16_unpack(scratch[r] + (resBase + (uint64_t)p * ppr) * 4, ppr, flag, out[r] + (uint64_t)p * epr);
+  free(tmp);
+  free(acc);
+}
+
 /* allreduceAllPairs (allreduce_allpair_packet.cu:15-69): one-hop LL8.  Rank s writes its
  * whole buffer (W words, W=(2c+2)/4 for 2-byte types) as LL8 packets into every peer's scratch
  * at s*W packets (:28, :40-41); rank r sums x_r then peers ascending (:49-61). */

@@ -59,6 +59,7 @@ def L():
             ("oracle_allreduce_packet", [i32, i32, i32, vp, u64, u32, u64, vp, vp], None),
             ("oracle_allreduce_allpairs", [i32, i32, i32, vp, u64, u32, u64, vp, vp], None),
             ("oracle_allreduce_sliced", [i32, i32, i32, vp, u64, u64, i32, vp], None),
+            ("oracle_mscclpp_test_ll", [i32, vp, u64, u32, vp, vp], None),
             ("oracle_trigger_encode", [u64, u32, u64, u32, u64, u64, u32, vp], None),
             ("oracle_fifo_commit_bit", [u64, u32], u64),
             ("oracle_lcg_fill", [i32, u64, i32, i32, vp], None),
@@ -141,6 +142,16 @@ def allreduce_allpairs(dtype, op, inputs, count, flag, half_bytes):
     outs = [np.zeros(W + 4, np.uint32) for _ in range(n)]
     L().oracle_allreduce_allpairs(dtype, op, n, _ptr_array(ins), count, flag, half_bytes, _ptr_array(scr),
                                   _ptr_array(outs))
+    return outs, scr
+
+
+def mscclpp_test_ll(inputs, nelems, flag, scratch_bytes):
+    """mscclpp-test allreduce6/7: outputs and the full scratch images (harness layout)."""
+    n = len(inputs)
+    ins = [np.ascontiguousarray(a).view(np.uint32) for a in inputs]
+    scr = [np.zeros(scratch_bytes // 4, np.uint32) for _ in range(n)]
+    outs = [np.zeros(nelems, np.uint32) for _ in range(n)]
+    L().oracle_mscclpp_test_ll(n, _ptr_array(ins), nelems, flag, _ptr_array(scr), _ptr_array(outs))
     return outs, scr
 
 

@@ -1,0 +1,97 @@
+"""GPU parity of the mscclpp-test AllReduce kernels restated for gfx950 (SURVEY §8a row a16:
+test/mscclpp-test/allreduce_test.cu allreduce5 / allreduce6 / allreduce7), n ranks in one process.
+
+k6 / k7: outputs and the whole packet scratch image (harness layout, flag parity double buffering)
+bit-exact against the oracle's restatement; k5 (in place, remote reads + gets): exact int32 sums.
+Plus the harness's known answer (input = rank -> n(n-1)/2, allreduce_test.cu:1172-1183)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_i32(n, count, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(-2 ** 31, 2 ** 31, count, dtype=np.int64).astype(np.int32) for _ in range(n)]
+
+
+@pytest.mark.parametrize("kernel", ["k6", "k7"])
+@pytest.mark.parametrize("n,count", [(2, 4096), (4, 8192), (8, 6144), (8, 65536), (3, 1536), (8, 16)])
+def test_ll_test_kernels_bit_exact(built, kernel, n, count):
+    import mscclpp_amd as m
+
+    code = m.ALGO_NAMES[kernel]
+    sb = m.scratch_required(code, n, count * 4, m.I32)
+    assert sb == 8 * count * 4
+    ranks = m.InProcessRanks(n, sb)
+    for call, flag in enumerate((1, 2, 3)):
+        ins = _rand_i32(n, count, 10 * call + n)
+        dins = [torch.from_numpy(a).cuda() for a in ins]
+        douts = [torch.zeros_like(d) for d in dins]
+        ranks.all_reduce(dins, douts, code)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        exp, scr = O.mscclpp_test_ll([a.view(np.uint32) for a in ins], count, flag, sb)
+        want = np.sum(np.stack([a.astype(np.int64) for a in ins]), axis=0).astype(np.uint32)  # wrapping
+        for r in range(n):
+            got = douts[r].cpu().numpy().view(np.uint32)
+            assert np.array_equal(exp[r], want)
+            assert np.array_equal(got, want), f"rank {r}"
+        if call == 0:
+            for r in range(n):
+                img = ranks.scratch_tensor(r, sb).cpu().numpy().view(np.uint32)
+                assert np.array_equal(img, scr[r]), f"scratch image of rank {r}"
+
+
+@pytest.mark.parametrize("n,count", [(2, 4096), (4, 65536), (8, 8192), (8, 1 << 18), (5, 640)])
+def test_k5_in_place(built, n, count):
+    import mscclpp_amd as m
+
+    ranks = m.InProcessRanks(n, 1 << 16)
+    for call in range(3):
+        ins = _rand_i32(n, count, 100 + call)
+        bufs = [torch.from_numpy(a.copy()).cuda() for a in ins]
+        ranks.all_reduce(bufs, bufs, m.ALGO_TEST_K5, nblocks=24, nthreads=512)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        want = np.sum(np.stack([a.astype(np.int64) for a in ins]), axis=0).astype(np.uint32)
+        for r in range(n):
+            assert np.array_equal(bufs[r].cpu().numpy().view(np.uint32), want), f"rank {r}"
+
+
+def test_harness_kat(built):
+    """allreduce_test.cu:1172-1183: every rank's input is its rank; every output is n(n-1)/2."""
+    import mscclpp_amd as m
+
+    n, count = 8, 1 << 14
+    for kernel in ("k5", "k6", "k7"):
+        code = m.ALGO_NAMES[kernel]
+        ranks = m.InProcessRanks(n, max(m.scratch_required(code, n, count * 4, m.I32), 1 << 16))
+        ins = [torch.full((count,), r, dtype=torch.int32, device="cuda") for r in range(n)]
+        outs = ins if kernel == "k5" else [torch.empty_like(t) for t in ins]
+        ranks.all_reduce(ins, outs, code)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        for o in outs:
+            assert torch.all(o == n * (n - 1) // 2), kernel
+
+
+def test_restrictions(built):
+    """k5 runs in place; k5/k6/k7 are int32 kernels; k6/k7 need bytes % (8 * n) == 0."""
+    import mscclpp_amd as m
+
+    n = 4
+    ranks = m.InProcessRanks(n, 1 << 20)
+    a = [torch.zeros(1024, dtype=torch.int32, device="cuda") for _ in range(n)]
+    b = [torch.zeros_like(t) for t in a]
+    with pytest.raises(m.MscclppError):
+        ranks.all_reduce(a, b, m.ALGO_TEST_K5)  # out of place
+    f = [torch.zeros(1024, dtype=torch.float16, device="cuda") for _ in range(n)]
+    with pytest.raises(m.MscclppError):
+        ranks.all_reduce(f, f, m.ALGO_TEST_K6)
+    odd = [torch.zeros(4 * n + 4, dtype=torch.int32, device="cuda") for _ in range(n)]
+    with pytest.raises(m.MscclppError):
+        ranks.all_reduce(odd, [torch.empty_like(t) for t in odd], m.ALGO_TEST_K6)
