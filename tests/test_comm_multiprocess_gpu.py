@@ -15,6 +15,7 @@ pytestmark = pytest.mark.gpu
 CASES = [  # (algo, dtype code, count)
     ("allpair", 0, 4096), ("packet", 0, 1 << 18), ("fullmesh", 0, 1 << 20), ("rsag", 2, 100000),
     ("packet", 1, 30000), ("auto", 0, 48 << 19), ("auto", 2, 1000), ("fullmesh", 1, 12345),
+    ("rsag_zc", 0, 1 << 20), ("rsag_zc", 2, 12345),
 ]
 
 
@@ -56,7 +57,7 @@ def _worker(rank, n, uid, q):
                     w = np.zeros(nw, np.uint32)
                     w.view(np.uint8)[:nbytes] = a.view(np.uint8)
                     pad.append(w)
-                e = O.allreduce_sliced(dt, O.SUM, pad, nw, sl // 4, 1 if sel == "rsag" else 0)[rank].view(np.uint8)[:nbytes]
+                e = O.allreduce_sliced(dt, O.SUM, pad, nw, sl // 4, 1 if sel in ("rsag", "rsag_zc") else 0)[rank].view(np.uint8)[:nbytes]
             got = out.cpu().contiguous().view(torch.uint8).numpy()
             results.append((algo, dt, count, errc, int(np.count_nonzero(got != e))))
         # ncclReduceScatter + ncclAllGather reconstruct the AllReduce (fp32, block 8192)

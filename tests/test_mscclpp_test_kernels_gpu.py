@@ -95,3 +95,28 @@ def test_restrictions(built):
     odd = [torch.zeros(4 * n + 4, dtype=torch.int32, device="cuda") for _ in range(n)]
     with pytest.raises(m.MscclppError):
         ranks.all_reduce(odd, [torch.empty_like(t) for t in odd], m.ALGO_TEST_K6)
+
+
+@pytest.mark.parametrize("kernel", ["5", "6", "7", "rsag_zc"])
+def test_harness_two_processes(built, tmp_path, kernel):
+    """tools/allreduce_test_perf.py (the mscclpp-test runTest loop) with 2 ranks sharing cuda:0:
+    graph-captured timing, the n(n-1)/2 data check and the JSONL perf rows."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "perf.jsonl"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str({"5": 29611, "6": 29612, "7": 29613}.get(kernel, 29614)),
+           os.path.join(root, "tools", "allreduce_test_perf.py"), "-b", "64K", "-e", "1M", "-f", "4", "-k", kernel,
+           "-w", "2", "-n", "5", "-G", "2", "-o", str(out)]
+    env = dict(os.environ, MSCCLPP_AMD_SPIN_TIMEOUT_MS="5000")
+    r = subprocess.run(cmd, cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "Out of bounds values : 0 OK" in r.stdout
+    rows = [json.loads(line) for line in out.read_text().splitlines()]
+    assert [row["size"] for row in rows] == [64 << 10, 256 << 10, 1 << 20]
+    assert all(row["ranks"] == 2 and row["time"] > 0 and row["busBw"] == pytest.approx(row["algBw"]) for row in rows)
