@@ -407,6 +407,29 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         del xs, os_
     except Exception as e:
         extras["fp32_1GiB_rsag_error"] = str(e)
+    try:
+        # the mscclpp-test kernels on the sizes the reference publishes (BASELINE.md §1,
+        # test/deploy/perf_ndmv4.jsonl / perf_ndmv5.jsonl), timed like common.cc:202-227
+        # (20 calls in one graph, 15 launches), int32 data = rank
+        mt = {}
+        for k, kb, pub in (("k6", 24, "A100 7.24 us / H100 6.18 us"), ("k6", 48, "A100 7.91 us / H100 6.62 us"),
+                           ("k6", 72, "A100 8.28 us / H100 6.91 us"), ("k7", 48, None),
+                           ("k5", 48 << 10, "A100 397.79 us, 126.52 GB/s")):
+            cnt = kb * 256
+            if (kb << 10) % (16 * n):
+                continue
+            xs = torch.full((cnt,), comm.rank, dtype=torch.int32, device=dev)
+            os_ = xs if k == "k5" else torch.empty_like(xs)
+            us = tmax(graph_time_per_call(lambda: comm.all_reduce(xs, os_, algo=k), calls=20, replays=15,
+                                          sync=barrier)) * 1e6
+            row = {"us": round(us, 2), "algbw_GBs": round((kb << 10) / us / 1e3, 2)}
+            if pub:
+                row["reference_published"] = pub
+            mt[f"{k}_{kb}KiB" if kb < 1024 else f"{k}_{kb >> 10}MiB"] = row
+            del xs, os_
+        extras["mscclpp_test"] = mt
+    except Exception as e:
+        extras["mscclpp_test_error"] = str(e)
     extras["device_error"] = comm.device_error()
     return extras
 
