@@ -387,6 +387,10 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         extras["ll_latency_error"] = str(e)
     try:
         glat = {}
+        # the first graph a process times runs slow (a one-time cost, tools/ll_small_probe.py:
+        # 32 us for the first size, 3.3 us for the same size measured again) -- discard one
+        xw = torch.rand(512, device=dev).half()
+        graph_time_per_call(lambda: comm.all_reduce(xw, torch.empty_like(xw)), sync=barrier)
         for kb in (1, 4, 16, 64, 256, 1024):
             cnt = kb * 512
             xs = torch.rand(cnt, device=dev).half()
