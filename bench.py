@@ -431,6 +431,13 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
                 row["reference_published"] = pub
             mt[f"{k}_{kb}KiB" if kb < 1024 else f"{k}_{kb >> 10}MiB"] = row
             del xs, os_
+        # allreduce1: the int32 ring whose bytes move through PortChannels and the host proxy
+        # (perf_ndmv4.jsonl:4: 1 GiB, 7701.98 us, 139.41 GB/s on 8 x A100)
+        barrier()
+        us, ok, _ = comm.proxy_ring_all_reduce((1 << 30) // 4, iters=3, graph_launches=2)
+        us = tmax(us)
+        mt["k1_1GiB"] = {"us": round(us, 1), "algbw_GBs": round((1 << 30) / us / 1e3, 2), "correct": ok,
+                         "reference_published": "A100 7701.98 us, 139.41 GB/s"}
         extras["mscclpp_test"] = mt
     except Exception as e:
         extras["mscclpp_test_error"] = str(e)

@@ -142,6 +142,15 @@ int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, int iters, 
 /* PortChannel all-to-all through the proxy (mode 0: put+signal, 1: putWithSignal,
  * 2: putWithSignalAndFlush).  out[0] = us per iteration, out[1] = 1 if correct, out[2] = NUMA node. */
 int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int mode, int iters, double* out);
+/* mscclpp-test allreduce1 (test/mscclpp-test/allreduce_test.cu:730-839): int32 ring RS + AG whose data
+ * moves through PortChannels and the host proxy (hipMemcpyAsync).  out[0] = us per AllReduce (graph of
+ * `iters` kernels replayed `graphLaunches` times), out[1] = 1 if every element is n(n-1)/2, out[2] =
+ * NUMA node of the proxy thread.  nblocks <= 0: the harness's 24 (x 1024 threads). */
+int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int iters, int graphLaunches, int nblocks,
+                                 double* out);
+int mscclppAmdLaunchRingProxyAllReduce(int* buff, const int* scratch, int rank, int nranks, size_t nelems,
+                                       const void* channels4, void* gridBarrier, int nblocks, int nthreads,
+                                       uint64_t budget, uint32_t* err, void* stream);
 int mscclppAmdLaunchHostOffloadKernel(int rank, int nranks, const void* fifoHandle, void* semHandles, int handleIndex,
                                       uint64_t budget, uint32_t* err, void* stream);
 int mscclppAmdLaunchPortChannelPut(void* chans, int nchans, const uint64_t* dstOffs, const uint64_t* srcOffs,

@@ -118,6 +118,7 @@ def lib():
         "mscclppAmdCommScratch": [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)],
         "mscclppAmdCommFlags": [vp, ctypes.POINTER(vp)],
         "mscclppAmdCommAllGatherHost": [vp, vp, vp, sz],
+        "mscclppAmdProxyRingAllReduce": [vp, sz, i32, i32, i32, ctypes.POINTER(ctypes.c_double)],
         "mscclppAmdExecutionPlanCreate": [ctypes.c_char_p, i32, ctypes.POINTER(vp)],
         "mscclppAmdExecutionPlanDestroy": [vp],
         "mscclppAmdExecutionPlanIsInPlace": [vp],
@@ -345,6 +346,14 @@ class Communicator:
         check(lib().ncclAllGather(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(recv.data_ptr()), send.numel(),
                                   NCCL_DTYPES[send.dtype], self.comm, stream_ptr(stream)), "ncclAllGather")
         return recv
+
+    def proxy_ring_all_reduce(self, nelems, iters=20, graph_launches=15, nblocks=0):
+        """mscclpp-test allreduce1: int32 ring RS+AG through the host proxy (input = rank).
+        Returns (us per AllReduce, correct, proxy NUMA node)."""
+        out = (ctypes.c_double * 3)()
+        check(lib().mscclppAmdProxyRingAllReduce(self.comm, nelems, iters, graph_launches, nblocks, out),
+              "proxy ring allreduce")
+        return out[0], out[1] == 1.0, int(out[2])
 
     def barrier(self):
         check(lib().mscclppAmdCommBarrier(self.comm), "barrier")

@@ -23,6 +23,9 @@
 
 extern "C" int mscclppAmdLaunchHostOffloadKernel(int rank, int nranks, const void* fifoHandle, void* semHandles,
                                                  int handleIndex, uint64_t budget, uint32_t* err, void* stream);
+extern "C" int mscclppAmdLaunchRingProxyAllReduce(int* buff, const int* scratch, int rank, int nranks, size_t nelems,
+                                                  const void* channels4, void* gridBarrier, int nblocks, int nthreads,
+                                                  uint64_t budget, uint32_t* err, void* stream);
 extern "C" int mscclppAmdLaunchPortChannelPut(void* chans, int nchans, const uint64_t* dstOffs, const uint64_t* srcOffs,
                                               uint64_t chunk, int mode, void* stream);
 
@@ -456,6 +459,146 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
     (void)hipFree(expct);
     (void)hipFree(src);
     (void)hipFree(dst);
+    return (int)ncclSuccess;
+  });
+}
+
+// =============================================================================================
+// Harness 3: mscclpp-test allreduce1 -- ring RS + AG through the host proxy (allreduce_test.cu:
+// 730-839; setup :1300-1400): int32, input = rank, expected n(n-1)/2 (:1172-1183).  Two PortChannels
+// to the next rank (round 1: my buffer -> its scratch, round 2: my buffer -> its buffer), one
+// Host2Device semaphore per (round, source).  out[0] = us per AllReduce (graph of `iters` kernels
+// replayed `graphLaunches` times, common.cc:202-227), out[1] = 1 if every element is n(n-1)/2,
+// out[2] = NUMA node of the proxy thread.
+// =============================================================================================
+extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int iters, int graphLaunches, int nblocks,
+                                           double* out) {
+  return guarded([&] {
+    if (!comm || !out || nelems == 0 || iters <= 0 || graphLaunches <= 0) return (int)ncclInvalidArgument;
+    const int n = comm->nranks, rank = comm->rank;
+    if (n < 2 || nelems % (size_t)n) return (int)ncclInvalidArgument;
+    if (nblocks <= 0) nblocks = 24;  // runColl: 24 x 1024 (allreduce_test.cu:1122-1125)
+    const size_t bytes = nelems * sizeof(int);
+    const int next = (rank + 1) % n, prev = (rank + n - 1) % n;
+    int* buff = (int*)allocUncached(bytes);
+    int* scratch = (int*)allocUncached(bytes);
+    auto peerBuff = comm->exchange(buff);
+    auto peerScratch = comm->exchange(scratch);
+    // tokens[round][source rank], written by the sources' proxies
+    uint64_t* tok = (uint64_t*)allocUncached(2 * n * 8);
+    uint64_t* expct = nullptr;
+    HIPCHECK(hipMalloc((void**)&expct, 2 * n * 8));
+    HIPCHECK(hipMemset(expct, 0, 2 * n * 8));
+    auto peerTok = comm->exchange(tok);
+    uint64_t *hcnt = nullptr, *flushDone = nullptr, *dFlushDone = nullptr;
+    HIPCHECK(hipHostMalloc((void**)&hcnt, 2 * 8, hipHostMallocDefault));
+    std::memset(hcnt, 0, 2 * 8);
+    HIPCHECK(hipHostMalloc((void**)&flushDone, 2 * 64, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(flushDone, 0, 2 * 64);
+    HIPCHECK(hipHostGetDevicePointer((void**)&dFlushDone, flushDone, 0));
+    uint32_t* err = nullptr;
+    HIPCHECK(hipMalloc((void**)&err, 64));
+    HIPCHECK(hipMemset(err, 0, 64));
+    void* gb = nullptr;
+    HIPCHECK(hipMalloc(&gb, 64));
+    HIPCHECK(hipMemset(gb, 0, 64));
+    Conn conn;
+    HIPCHECK(hipStreamCreateWithFlags(&conn.stream, hipStreamNonBlocking));
+    // MemoryId 0 = my buffer, 1 = next's scratch, 2 = next's buffer; semaphoreId = round
+    void* mem[3] = {buff, peerScratch[next], peerBuff[next]};
+    Proxy proxy(comm->device, 512, [&](const ProxyTrigger& t, uint64_t pos) {  // ProxyService::handleTrigger
+      const int round = (int)t.fields.semaphoreId;
+      if (round < 0 || round > 1) return false;
+      if (t.fields.type & kTriggerData)
+        (void)hipMemcpyAsync((char*)mem[t.fields.dstMemoryId] + t.fields.dstOffset,
+                             (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
+                             hipMemcpyDeviceToDevice, conn.stream);
+      if (t.fields.type & kTriggerFlag) {
+        uint64_t* c = &hcnt[round];
+        __atomic_store_n(c, *c + 1, __ATOMIC_RELAXED);
+        (void)hipMemcpyAsync((uint64_t*)peerTok[next] + round * n + rank, c, 8, hipMemcpyHostToDevice, conn.stream);
+      }
+      if (t.fields.type & kTriggerSync) {
+        (void)hipStreamSynchronize(conn.stream);
+        __atomic_store_n(&flushDone[round * 8], pos + 1, __ATOMIC_RELEASE);
+      }
+      return false;
+    });
+    proxy.start();
+    const uint64_t budget = spinBudgetTicks();
+    PortChannelDeviceHandle ch[4] = {};
+    for (int round = 0; round < 2; ++round) {
+      PortChannelDeviceHandle& snd = ch[round * 2];      // to next
+      PortChannelDeviceHandle& rcv = ch[round * 2 + 1];  // from prev: only its semaphore is used
+      snd.semaphoreId = (uint32_t)round;
+      snd.src = 0;
+      snd.dst = (uint32_t)(1 + round);
+      snd.fifo = proxy.fifo().deviceHandle();
+      snd.flushDonePos = dFlushDone + round * 8;
+      snd.budget = budget;
+      snd.err = err;
+      snd.semaphore = {tok + round * n + next, expct + round * n + next};
+      rcv = snd;
+      rcv.semaphore = {tok + round * n + prev, expct + round * n + prev};
+    }
+    hipStream_t st;
+    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    std::vector<int> init(nelems, rank);
+    auto reset = [&] { HIPCHECK(hipMemcpy(buff, init.data(), bytes, hipMemcpyHostToDevice)); };
+    auto launch = [&] {
+      int rc = mscclppAmdLaunchRingProxyAllReduce(buff, scratch, rank, n, nelems, ch, gb, nblocks, 1024, budget, err, st);
+      if (rc) throw std::runtime_error("ring kernel launch failed: " + std::to_string(rc));
+    };
+    // correctness first (checkData, common.cc:346-360)
+    reset();
+    comm->boot->barrier();
+    launch();
+    HIPCHECK(hipStreamSynchronize(st));
+    std::vector<int> back(nelems);
+    HIPCHECK(hipMemcpy(back.data(), buff, bytes, hipMemcpyDeviceToHost));
+    bool ok = true;
+    const int expected = n * (n - 1) / 2;
+    for (size_t i = 0; i < nelems && ok; ++i) ok = back[i] == expected;
+    comm->boot->barrier();
+    // benchTime: iters launches in one graph, graphLaunches replays after a barrier
+    hipGraph_t graph;
+    hipGraphExec_t inst;
+    HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    for (int i = 0; i < iters; ++i) launch();
+    HIPCHECK(hipStreamEndCapture(st, &graph));
+    HIPCHECK(hipGraphInstantiate(&inst, graph, nullptr, nullptr, 0));
+    comm->boot->barrier();
+    const double t0 = nowSec();
+    for (int l = 0; l < graphLaunches; ++l) HIPCHECK(hipGraphLaunch(inst, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    const double t1 = nowSec();
+    comm->boot->barrier();
+    uint32_t e = 0;
+    HIPCHECK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost));
+    out[0] = (t1 - t0) * 1e6 / iters / graphLaunches;
+    out[1] = (ok && e == 0) ? 1.0 : 0.0;
+    out[2] = (double)proxy.numaNode();
+    proxy.stop();
+    (void)hipStreamSynchronize(conn.stream);
+    (void)hipStreamDestroy(conn.stream);
+    (void)hipGraphExecDestroy(inst);
+    (void)hipGraphDestroy(graph);
+    (void)hipStreamDestroy(st);
+    comm->boot->barrier();  // peers no longer touch my buffers / tokens
+    for (int r = 0; r < n; ++r)
+      if (r != rank) {
+        comm->forgetMapping(r, peerBuff[r]);
+        comm->forgetMapping(r, peerScratch[r]);
+        comm->forgetMapping(r, peerTok[r]);
+      }
+    (void)hipFree(gb);
+    (void)hipFree(err);
+    (void)hipHostFree(flushDone);
+    (void)hipHostFree(hcnt);
+    (void)hipFree(tok);
+    (void)hipFree(expct);
+    (void)hipFree(scratch);
+    (void)hipFree(buff);
     return (int)ncclSuccess;
   });
 }

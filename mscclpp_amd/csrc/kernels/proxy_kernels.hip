@@ -43,9 +43,153 @@ __global__ void portChannelPutKernel(PortChannelDeviceHandle* chans, int nchans,
   ch.wait();
 }
 
+// ---- mscclpp-test allreduce1: ring RS + AG driven through the host proxy ------------------------
+// test/mscclpp-test/allreduce_test.cu:730-839.  Thread 0 of block 0 drives two PortChannels to the
+// next rank on the ring (first round: my buffer -> its scratch; second round: my buffer -> its
+// buffer) and waits on the two from the previous rank; every block sums with vectorSum; blocks meet
+// at a grid barrier between steps (DeviceSyncer, concurrency_device.hpp:28-69).  Chunk c is
+// reduced starting at rank c+1 and ending at its owner c.  The buffers
+// are uncached (mscclpp::GpuBuffer on AMD, gpu_utils.hpp:375-376), so the proxy's copy engine and
+// every XCD see each other's writes; the barrier adds system-scope release / acquire anyway.
+struct GridBarrier {
+  uint32_t count;
+  uint32_t gen;
+};
+
+__device__ __forceinline__ void grid_sync(GridBarrier* gb, uint64_t budget, uint32_t* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t g = __hip_atomic_load(&gb->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (__hip_atomic_fetch_add(&gb->count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(&gb->count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gb->gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      SpinGuard sg(budget);
+      while (__hip_atomic_load(&gb->gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        __builtin_amdgcn_s_sleep(1);
+        if (sg.expired()) {
+          report_error(err, kErrSemaphoreTimeout);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+// dst += src over nElem ints, all blocks (vectorSum, allreduce_test.cu:45-68)
+__device__ __forceinline__ void ringVectorSum(int* dst, const int* src, size_t nElem) {
+  const size_t n4 = nElem / 4, stride = (size_t)blockDim.x * gridDim.x;
+  int4* d4 = (int4*)dst;
+  const int4* s4 = (const int4*)src;
+  for (size_t i = threadIdx.x + (size_t)blockIdx.x * blockDim.x; i < n4; i += stride) {
+    int4 a = d4[i];
+    const int4 b = s4[i];
+    a.x += b.x;
+    a.y += b.y;
+    a.z += b.z;
+    a.w += b.w;
+    d4[i] = a;
+  }
+  for (size_t i = n4 * 4 + threadIdx.x + (size_t)blockIdx.x * blockDim.x; i < nElem; i += stride) dst[i] += src[i];
+}
+
+struct RingChannels {
+  PortChannelDeviceHandle fstSend, fstRecv, sndSend, sndRecv;
+};
+
+__global__ void __launch_bounds__(1024) ringProxyAllReduceKernel(int* buff, const int* scratch, int rank, int worldSize,
+                                                                 size_t nelems, RingChannels ch, GridBarrier* gb,
+                                                                 uint64_t budget, uint32_t* err) {
+  const bool isComm = threadIdx.x == 0 && blockIdx.x == 0;
+  const int n = worldSize;
+  const size_t chunkNelem = nelems / n;
+  const size_t half = chunkNelem / 2, rest = chunkNelem - half;
+  // step 1 (:745-751)
+  size_t chunkIndex = (rank + n - 1) % n;
+  size_t offset = chunkIndex * chunkNelem * sizeof(int);
+  if (isComm && chunkNelem > 1) ch.fstSend.putWithSignal(offset, offset, half * sizeof(int));
+  // steps 2 .. n-1 (:753-781)
+  for (int step = 2; step < n; ++step) {
+    if (isComm) {
+      if (chunkNelem > 1) {
+        ch.fstRecv.wait();
+        ch.fstSend.flush();
+      }
+      ch.fstSend.putWithSignal(offset + half * sizeof(int), offset + half * sizeof(int), rest * sizeof(int));
+    }
+    grid_sync(gb, budget, err);
+    chunkIndex = (rank + n - step) % n;
+    offset = chunkIndex * chunkNelem * sizeof(int);
+    int* dst = (int*)((char*)buff + offset);
+    const int* src = (const int*)((const char*)scratch + offset);
+    ringVectorSum(dst, src, half);
+    if (isComm) {
+      ch.fstRecv.wait();
+      ch.fstSend.flush();
+      if (chunkNelem > 1) ch.fstSend.putWithSignal(offset, offset, half * sizeof(int));
+    }
+    grid_sync(gb, budget, err);
+    ringVectorSum(dst + half, src + half, rest);
+  }
+  // step n (:783-815)
+  if (isComm) {
+    if (chunkNelem > 1) {
+      ch.fstRecv.wait();
+      ch.fstSend.flush();
+    }
+    ch.fstSend.putWithSignal(offset + half * sizeof(int), offset + half * sizeof(int), rest * sizeof(int));
+  }
+  grid_sync(gb, budget, err);
+  offset = (size_t)rank * chunkNelem * sizeof(int);
+  int* dst = (int*)((char*)buff + offset);
+  const int* src = (const int*)((const char*)scratch + offset);
+  ringVectorSum(dst, src, half);
+  if (isComm) {
+    ch.fstRecv.wait();
+    ch.fstSend.flush();
+    if (chunkNelem > 1) ch.sndSend.putWithSignal(offset, offset, half * sizeof(int));
+  }
+  grid_sync(gb, budget, err);
+  ringVectorSum(dst + half, src + half, rest);
+  if (isComm) {
+    if (chunkNelem > 1) {
+      ch.sndRecv.wait();
+      ch.sndSend.flush();
+    }
+    ch.sndSend.putWithSignalAndFlush(offset + half * sizeof(int), offset + half * sizeof(int), rest * sizeof(int));
+  }
+  // steps n+1 .. 2n-2: forward the reduced chunks around the ring (:817-832)
+  for (int i = 1; i < n - 1; ++i) {
+    if (isComm) ch.sndRecv.wait();
+    grid_sync(gb, budget, err);
+    chunkIndex = (rank + n - i) % n;
+    if (isComm)
+      ch.sndSend.putWithSignalAndFlush(chunkIndex * chunkNelem * sizeof(int), chunkIndex * chunkNelem * sizeof(int),
+                                       chunkNelem * sizeof(int));
+  }
+  if (isComm) ch.sndRecv.wait();  // final receive (:834-838)
+}
+
 }  // namespace mscclpp_amd
 
 using namespace mscclpp_amd;
+
+extern "C" int mscclppAmdLaunchRingProxyAllReduce(int* buff, const int* scratch, int rank, int nranks, size_t nelems,
+                                                  const void* channels4, void* gridBarrier, int nblocks, int nthreads,
+                                                  uint64_t budget, uint32_t* err, void* stream) {
+  if (!buff || !scratch || !channels4 || !gridBarrier || nranks < 2 || nblocks <= 0 || nthreads <= 0 ||
+      nthreads > 1024 || nthreads % 64)
+    return 4;
+  if (!grid_coresident(ringProxyAllReduceKernel, nthreads, nblocks)) return 5;
+  RingChannels ch = *reinterpret_cast<const RingChannels*>(channels4);
+  hipLaunchKernelGGL(ringProxyAllReduceKernel, dim3(nblocks), dim3(nthreads), 0, (hipStream_t)stream, buff, scratch,
+                     rank, nranks, nelems, ch, (GridBarrier*)gridBarrier, budget, err);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 extern "C" int mscclppAmdLaunchHostOffloadKernel(int rank, int nranks, const void* fifoHandle, void* semHandles,
                                                  int handleIndex, uint64_t budget, uint32_t* err, void* stream) {

@@ -97,7 +97,7 @@ def test_restrictions(built):
         ranks.all_reduce(odd, [torch.empty_like(t) for t in odd], m.ALGO_TEST_K6)
 
 
-@pytest.mark.parametrize("kernel", ["5", "6", "7", "rsag_zc"])
+@pytest.mark.parametrize("kernel", ["1", "5", "6", "7", "rsag_zc"])
 def test_harness_two_processes(built, tmp_path, kernel):
     """tools/allreduce_test_perf.py (the mscclpp-test runTest loop) with 2 ranks sharing cuda:0:
     graph-captured timing, the n(n-1)/2 data check and the JSONL perf rows."""
@@ -109,7 +109,7 @@ def test_harness_two_processes(built, tmp_path, kernel):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = tmp_path / "perf.jsonl"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str({"5": 29611, "6": 29612, "7": 29613}.get(kernel, 29614)),
+           "--master-addr", "127.0.0.1", "--master-port", str({"1": 29610, "5": 29611, "6": 29612, "7": 29613}.get(kernel, 29614)),
            os.path.join(root, "tools", "allreduce_test_perf.py"), "-b", "64K", "-e", "1M", "-f", "4", "-k", kernel,
            "-w", "2", "-n", "5", "-G", "2", "-o", str(out)]
     env = dict(os.environ, MSCCLPP_AMD_SPIN_TIMEOUT_MS="5000")

@@ -7,8 +7,8 @@ checkData :346-360) and allreduce_test.cu (runColl :1107-1170, initData :1172-11
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
         tools/allreduce_test_perf.py -b 24K -e 48M -f 2 -k 6 -o perf.jsonl
 
-Kernels (-k): 5, 6, 7 -- the harness's own int32 kernels (allreduce5 AMD branch, allreduce6 LL16,
-allreduce7 LL8; MSCCLPP_AMD_ALGO_TEST_K*); or a product algorithm name (packet, allpair, fullmesh,
+Kernels (-k): 1, 5, 6, 7 -- the harness's own int32 kernels (allreduce1 ring through the host proxy,
+allreduce5 AMD branch, allreduce6 LL16, allreduce7 LL8); or a product algorithm name (packet, allpair, fullmesh,
 rsag, rsag_zc) run on the same int32 data.  Timing is the reference's: `iters` calls captured in one
 HIP graph, the graph launched `-G` times after a barrier, time / iters / launches, averaged over
 ranks (-a 1); data check = the known answer input = rank -> n(n-1)/2 on every element.  Rows are
@@ -27,7 +27,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-IN_PLACE = {"5": True, "6": False, "7": False}  # isInPlace (allreduce_test.cu:1262-1264)
+IN_PLACE = {"1": True, "5": True, "6": False, "7": False}  # isInPlace (allreduce_test.cu:1262-1264)
 
 
 def parse_size(v):
@@ -60,6 +60,37 @@ def sizes(a):
         s = s * a.stepfactor if a.stepfactor > 1 else s + a.stepbytes
 
 
+def run_k1(a, m, comm, rank, world):
+    """-k 1: each size runs mscclppAmdProxyRingAllReduce (setup, data check, graph timing inside)."""
+    errors = 0
+    if rank == 0:
+        print("#       size         count     time   algbw   busbw  #wrong   (allreduce1: ring via host proxy)",
+              flush=True)
+    for size in sizes(a):
+        count = size // 4
+        us, ok, _ = comm.proxy_ring_all_reduce(count, a.iters, a.cudagraph)
+        t = torch.tensor([us], dtype=torch.float64)
+        dist.all_reduce(t)
+        us = float(t[0]) / world
+        ok_t = torch.tensor([0 if ok else 1], dtype=torch.int64)
+        dist.all_reduce(ok_t)
+        errors += int(ok_t[0])
+        alg = size / 1e3 / us
+        bus = alg * 2 * (world - 1) / world
+        if rank == 0:
+            print(f"{size:12d}  {count:12d}  {us:7.1f}  {alg:6.2f}  {bus:6.2f}  {int(ok_t[0]):5d}", flush=True)
+            if a.output_file:
+                with open(a.output_file, "a") as f:
+                    f.write(json.dumps({"name": "allreduce", "kernel": "1", "ranks": world, "ranksPerNode": world,
+                                        "size": size, "time": us, "algBw": alg, "busBw": bus}) + "\n")
+    if rank == 0:
+        print(f"# Out of bounds values : {errors} {'OK' if errors == 0 else 'FAILED'}", flush=True)
+    comm.destroy()
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.exit(1 if errors else 0)
+
+
 def main():
     a = parse()
     import mscclpp_amd as m
@@ -71,7 +102,7 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = m.Communicator.from_torch_dist()
     kname = a.kernel_num
-    algo = m.ALGO_NAMES["k" + kname] if kname in IN_PLACE else m.ALGO_NAMES[kname]
+    algo = None if kname == "1" else (m.ALGO_NAMES["k" + kname] if kname in IN_PLACE else m.ALGO_NAMES[kname])
     in_place = IN_PLACE.get(kname, False)
     dev = torch.device("cuda", local % ndev)
     maxc = a.maxbytes // 4
@@ -96,6 +127,8 @@ def main():
         dist.all_reduce(t, op=op)
         return float(t[0]) / (world if a.average == 1 else 1)
 
+    if kname == "1":  # allreduce1: the proxy-driven ring owns its buffers, channels and proxy thread
+        return run_k1(a, m, comm, rank, world)
     # warm-up at the largest and the smallest size (runTest :232-250)
     for sz in (a.maxbytes, a.minbytes):
         for _ in range(a.warmup_iters):
