@@ -184,6 +184,32 @@ struct Conn {
   hipStream_t stream = nullptr;
 };
 
+// Stream-ordered remote token update (Host2DeviceSemaphore::signal -> CudaIpcConnection::
+// updateAndSync, semaphore.cc:154-156, connection.cc:159-177).  HIP reads a pinned source when the
+// copy executes, not when it is enqueued, so a single host counter could be read after a later
+// increment and release a waiter before the data copies queued ahead of that later signal.  Each
+// value therefore gets its own slot of a pinned ring; a slot is reused only after a stream
+// synchronize has retired every copy of the previous lap.
+class TokenWriter {
+ public:
+  TokenWriter() { HIPCHECK(hipHostMalloc((void**)&slots_, kSlots * sizeof(uint64_t), hipHostMallocDefault)); }
+  ~TokenWriter() { (void)hipHostFree(slots_); }
+  TokenWriter(const TokenWriter&) = delete;
+  TokenWriter& operator=(const TokenWriter&) = delete;
+  void signal(uint64_t* remoteToken, hipStream_t s) {
+    ++value_;
+    if (value_ % kSlots == 0) (void)hipStreamSynchronize(s);
+    uint64_t* slot = &slots_[value_ % kSlots];
+    *slot = value_;
+    (void)hipMemcpyAsync(remoteToken, slot, sizeof(uint64_t), hipMemcpyHostToDevice, s);
+  }
+
+ private:
+  static constexpr uint64_t kSlots = 1024;
+  uint64_t* slots_ = nullptr;
+  uint64_t value_ = 0;
+};
+
 }  // namespace host
 }  // namespace mscclpp_amd
 
@@ -214,9 +240,8 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
     HIPCHECK(hipMalloc((void**)&expct, 2 * n * 8));
     HIPCHECK(hipMemset(expct, 0, 2 * n * 8));
     auto peerTok = comm->exchange(tok);
-    uint64_t* hcnt = nullptr;
-    HIPCHECK(hipHostMalloc((void**)&hcnt, 2 * n * 8, hipHostMallocDefault));
-    std::memset(hcnt, 0, 2 * n * 8);
+    std::vector<std::unique_ptr<TokenWriter>> writers(2 * n);
+    for (auto& w : writers) w = std::make_unique<TokenWriter>();
     std::vector<Host2DeviceSemaphoreDeviceHandle> hh(2 * n);
     for (int s = 0; s < 2; ++s)
       for (int r = 0; r < n; ++r) hh[s * n + r] = {tok + s * n + r, expct + s * n + r};
@@ -237,10 +262,7 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
           const int nghr = (rank + k) % n;
           (void)hipMemcpyAsync((char*)peers[nghr] + rank * perRank, (char*)data + rank * perRank, perRank,
                                hipMemcpyDeviceToDevice, conns[nghr].stream);
-          uint64_t* c = &hcnt[set * n + nghr];
-          __atomic_store_n(c, *c + 1, __ATOMIC_RELAXED);
-          (void)hipMemcpyAsync((uint64_t*)peerTok[nghr] + set * n + rank, c, 8, hipMemcpyHostToDevice,
-                               conns[nghr].stream);
+          writers[set * n + nghr]->signal((uint64_t*)peerTok[nghr] + set * n + rank, conns[nghr].stream);
         }
       }
       return false;
@@ -314,7 +336,6 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
       }
     (void)hipFree(err);
     (void)hipFree(dh);
-    (void)hipHostFree(hcnt);
     (void)hipFree(tok);
     (void)hipFree(expct);
     (void)hipFree(data);
@@ -343,14 +364,14 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
     std::vector<void*> mem(1 + n);
     mem[0] = src;
     for (int q = 0; q < n; ++q) mem[1 + q] = peerDst[q];
-    uint64_t *tok = nullptr, *expct = nullptr, *hcnt = nullptr, *flushDone = nullptr, *dFlushDone = nullptr;
+    uint64_t *tok = nullptr, *expct = nullptr, *flushDone = nullptr, *dFlushDone = nullptr;
     HIPCHECK(hipMalloc((void**)&tok, n * 8));
     HIPCHECK(hipMemset(tok, 0, n * 8));
     HIPCHECK(hipMalloc((void**)&expct, n * 8));
     HIPCHECK(hipMemset(expct, 0, n * 8));
     auto peerTok = comm->exchange(tok);
-    HIPCHECK(hipHostMalloc((void**)&hcnt, n * 8, hipHostMallocDefault));
-    std::memset(hcnt, 0, n * 8);
+    std::vector<std::unique_ptr<TokenWriter>> writers(n);
+    for (auto& w : writers) w = std::make_unique<TokenWriter>();
     HIPCHECK(hipHostMalloc((void**)&flushDone, n * 64, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(flushDone, 0, n * 64);
     HIPCHECK(hipHostGetDevicePointer((void**)&dFlushDone, flushDone, 0));
@@ -369,10 +390,8 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
                              (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
                              hipMemcpyDeviceToDevice, conns[q].stream);
       if (t.fields.type & kTriggerFlag) {
-        uint64_t* c = &hcnt[q];
-        __atomic_store_n(c, *c + 1, __ATOMIC_RELAXED);
         // remote token slot of peer q for source `rank`
-        (void)hipMemcpyAsync((uint64_t*)peerTok[q] + rank, c, 8, hipMemcpyHostToDevice, conns[q].stream);
+        writers[q]->signal((uint64_t*)peerTok[q] + rank, conns[q].stream);
       }
       if (t.fields.type & kTriggerSync) {
         (void)hipStreamSynchronize(conns[q].stream);
@@ -454,7 +473,6 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
     (void)hipFree(dch);
     (void)hipFree(err);
     (void)hipHostFree(flushDone);
-    (void)hipHostFree(hcnt);
     (void)hipFree(tok);
     (void)hipFree(expct);
     (void)hipFree(src);
@@ -490,9 +508,8 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     HIPCHECK(hipMalloc((void**)&expct, 2 * n * 8));
     HIPCHECK(hipMemset(expct, 0, 2 * n * 8));
     auto peerTok = comm->exchange(tok);
-    uint64_t *hcnt = nullptr, *flushDone = nullptr, *dFlushDone = nullptr;
-    HIPCHECK(hipHostMalloc((void**)&hcnt, 2 * 8, hipHostMallocDefault));
-    std::memset(hcnt, 0, 2 * 8);
+    uint64_t *flushDone = nullptr, *dFlushDone = nullptr;
+    TokenWriter writers[2];
     HIPCHECK(hipHostMalloc((void**)&flushDone, 2 * 64, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(flushDone, 0, 2 * 64);
     HIPCHECK(hipHostGetDevicePointer((void**)&dFlushDone, flushDone, 0));
@@ -514,9 +531,7 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
                              (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
                              hipMemcpyDeviceToDevice, conn.stream);
       if (t.fields.type & kTriggerFlag) {
-        uint64_t* c = &hcnt[round];
-        __atomic_store_n(c, *c + 1, __ATOMIC_RELAXED);
-        (void)hipMemcpyAsync((uint64_t*)peerTok[next] + round * n + rank, c, 8, hipMemcpyHostToDevice, conn.stream);
+        writers[round].signal((uint64_t*)peerTok[next] + round * n + rank, conn.stream);
       }
       if (t.fields.type & kTriggerSync) {
         (void)hipStreamSynchronize(conn.stream);
@@ -594,7 +609,6 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     (void)hipFree(gb);
     (void)hipFree(err);
     (void)hipHostFree(flushDone);
-    (void)hipHostFree(hcnt);
     (void)hipFree(tok);
     (void)hipFree(expct);
     (void)hipFree(scratch);

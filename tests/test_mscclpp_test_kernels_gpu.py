@@ -120,3 +120,21 @@ def test_harness_two_processes(built, tmp_path, kernel):
     rows = [json.loads(line) for line in out.read_text().splitlines()]
     assert [row["size"] for row in rows] == [64 << 10, 256 << 10, 1 << 20]
     assert all(row["ranks"] == 2 and row["time"] > 0 and row["busBw"] == pytest.approx(row["algBw"]) for row in rows)
+
+
+def test_k1_large_chunks_two_processes(built, tmp_path):
+    """allreduce1 at 64 MiB: copies long enough that the proxy runs ahead of its copy stream --
+    every signal must carry its own token value (TokenWriter in proxy.cpp), or a waiter is released
+    before the data queued ahead of a later signal has landed."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29615",
+           os.path.join(root, "tools", "allreduce_test_perf.py"), "-b", "64M", "-e", "64M", "-k", "1",
+           "-n", "2", "-G", "1"]
+    r = subprocess.run(cmd, cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "Out of bounds values : 0 OK" in r.stdout
