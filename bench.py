@@ -188,7 +188,7 @@ def bench_single(args):
                    "bytes": S, "parallelism": "single-gpu"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": committed_traffic(S),
-                     "kernel": "selfReduceLL16PmKernel", "kernel_us": round(kern_ms * 1e3, 2),
+                     "kernel": "selfReduceLL16LdsKernel", "kernel_us": round(kern_ms * 1e3, 2),
                      "algorithmic_bytes_per_launch": 7 * S},
     }
     if args.no_extras:  # profiling runs: only the headline launches, so per-kernel stats are of one size

@@ -27,7 +27,7 @@ extern "C" {
 #endif
 
 #define MSCCLPP_AMD_MAX_RANKS 8
-#define MSCCLPP_AMD_FLAG_SLOTS 1024
+#define MSCCLPP_AMD_FLAG_SLOTS 4096
 #define MSCCLPP_AMD_MAX_CHANNELS 256
 
 /* dtype / op codes of the extension API (ncclDataType_t / ncclRedOp_t are mapped onto these) */

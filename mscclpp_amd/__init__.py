@@ -25,7 +25,7 @@ ALGO_TEST_K5, ALGO_TEST_K6, ALGO_TEST_K7 = 105, 106, 107  # mscclpp-test allredu
 ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4, "rsag_zc": 5,
               "k5": ALGO_TEST_K5, "k6": ALGO_TEST_K6, "k7": ALGO_TEST_K7}
 MAX_RANKS = 8
-FLAG_SLOTS = 1024
+FLAG_SLOTS = 4096
 MAX_CHANNELS = 256
 
 # ncclDataType_t / ncclRedOp_t (include/mscclpp_amd/nccl.h, values of the reference nccl.h:217-253)

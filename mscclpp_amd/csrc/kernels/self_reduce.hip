@@ -175,13 +175,125 @@ __global__ void __launch_bounds__(256) selfReduceLL16PmKernel(const uint8_t* __r
   bump_flags(flags, flag);
 }
 
+// LDS-staged packets: the payload side moves 16 bytes per lane (one dwordx4 per wave instruction,
+// 1 KiB per wave) and the packet side stays packet-major (lane j owns packet j).  A wave turns its
+// 1 KiB of payload into 128 packets through 1 KiB of its own LDS: each lane writes its 16 bytes, then
+// reads back the 8 bytes of packet j and of packet 64 + j; the consumer runs the same swizzle in
+// reverse before the 16-byte-per-lane sum and output store.  LDS traffic per wave-tile is three
+// ds ops per side; the crossing stays inside one wave, so no barrier is needed (one wave's LDS
+// operations complete in order).
+template <int DT, int OP, int U>
+__global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
+                                                               uint8_t* pkts, uint8_t* __restrict__ out, uint64_t bytes,
+                                                               uint32_t* flags, uint64_t budget, uint32_t* err) {
+  constexpr uint32_t kWaves = 4;
+  constexpr uint64_t kTileBytes = (uint64_t)kWaves * U * 1024;  // payload bytes per workgroup and round
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves][U][1024];
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  const uint32_t flag = flags[b];
+  const uint64_t ntiles = (bytes + kTileBytes - 1) / kTileBytes;
+  const uint32_t partner = b ^ 1u;
+  // payload byte offset of (tile, sub-tile k) for this wave: 1 KiB chunks dealt k-major over waves
+  auto chunk = [&](uint64_t t, int k) { return t * kTileBytes + (uint64_t)(k * kWaves + wave) * 1024; };
+  u32x4 yw[U];
+  auto load_y = [&](uint64_t t) {
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t c = chunk(t, k);
+      if (c + lane * 16 < bytes) yw[k] = load16<kNonTemporal>(make_rsrc(y + c), lane * 16);
+    }
+  };
+  if (b < ntiles) load_y(b);
+  for (uint64_t base = 0; base < ntiles; base += G) {
+    const uint64_t t = base + b;
+    const uint64_t tp = base + partner;
+    const bool consume = partner < G && tp < ntiles;
+    u32x4 a[U];
+    if (consume) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint64_t c = chunk(tp, k);
+        if (c + lane * 16 < bytes) a[k] = load16<kNonTemporal>(make_rsrc(x + c), lane * 16);
+      }
+    }
+    // ---- pack: payload -> LDS -> packet-major stores (packets j and 64 + j of each 1 KiB chunk)
+    if (t < ntiles) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) *(u32x4*)&lds[wave][k][lane * 16] = yw[k];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint64_t c = chunk(t, k);
+        const auto rp = make_rsrc(pkts + 2 * c);
+        const u32x2 lo = *(const u32x2*)&lds[wave][k][lane * 8];
+        const u32x2 hi = *(const u32x2*)&lds[wave][k][512 + lane * 8];
+        if (c + lane * 8 < bytes) store16<kSystem>(rp, lane * 16, LL16Packet::make(lo.x, lo.y, flag));
+        if (c + 512 + lane * 8 < bytes) store16<kSystem>(rp, 1024 + lane * 16, LL16Packet::make(hi.x, hi.y, flag));
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (t + G < ntiles) load_y(t + G);
+    }
+    // ---- consume my partner's tile: packet-major polls -> LDS -> payload-major sum and store
+    if (consume) {
+      u32x4 v[2 * U];
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint64_t c = chunk(tp, k);
+        const auto rp = make_rsrc(pkts + 2 * c);
+        if (c + lane * 8 < bytes) {
+          v[2 * k] = load16<kSystem>(rp, lane * 16);
+          ok &= LL16Packet::ready(v[2 * k], flag);
+        }
+        if (c + 512 + lane * 8 < bytes) {
+          v[2 * k + 1] = load16<kSystem>(rp, 1024 + lane * 16);
+          ok &= LL16Packet::ready(v[2 * k + 1], flag);
+        }
+      }
+      if (!ok) {
+#pragma unroll
+        for (int i = 0; i < 2 * U; ++i) {
+          const uint64_t c = chunk(tp, i / 2);
+          const uint32_t off = (i & 1) * 1024 + lane * 16;
+          if (c + (i & 1) * 512 + lane * 8 < bytes && !LL16Packet::ready(v[i], flag)) {
+            const auto rp = make_rsrc(pkts + 2 * c);
+            SpinGuard g(budget);
+            do {
+              v[i] = load16<kSystem>(rp, off);
+              if (g.expired()) {
+                report_error(err, kErrPacketTimeout);
+                break;
+              }
+            } while (!LL16Packet::ready(v[i], flag));
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        *(u32x2*)&lds[wave][k][lane * 8] = u32x2{v[2 * k].x, v[2 * k].z};
+        *(u32x2*)&lds[wave][k][512 + lane * 8] = u32x2{v[2 * k + 1].x, v[2 * k + 1].z};
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint64_t c = chunk(tp, k);
+        const u32x4 p = *(const u32x4*)&lds[wave][k][lane * 16];
+        if (c + lane * 16 < bytes) store16<kNonTemporal>(make_rsrc(out + c), lane * 16, reduce4<DT, OP>(a[k], p));
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  bump_flags(flags, flag);
+}
+
 template <int DT, int OP>
-static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out, uint64_t nunits, uint32_t* flags,
+static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                              int nblocks, uint64_t budget, uint32_t* err, hipStream_t stream) {
-  // packet-major mapping, 8 packets per lane per round, system-scope packet stores and polls
-  // (tools/sweep_self_reduce.py: 57-58 us at 48 MiB vs 82 us for the payload-major form)
-  hipLaunchKernelGGL((selfReduceLL16PmKernel<DT, OP, 8, kSystem, kSystem>), dim3(nblocks), dim3(256), 0, stream,
-                     (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, nunits * 2, flags, budget, err);
+  // LDS-staged packets, 2 KiB of payload per wave and round (tools/sweep_self_reduce.py: 56.3-57.3 us
+  // at 48 MiB and 1024 workgroups vs 57.7-58.9 us for the packet-major register form, variant 13)
+  hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2>), dim3(nblocks), dim3(256), 0, stream, (const uint8_t*)x,
+                     (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err);
 }
 
 // Streaming copy (read S, write S) used by the benchmark to measure the achievable HBM ceiling on
@@ -212,7 +324,7 @@ extern "C" int mscclppAmdSelfReduceLL16Variant(const void* x, const void* y, voi
                                                uint32_t* flags, int nblocks, int variant, uint64_t budgetTicks,
                                                uint32_t* err, void* streamPtr) {
   hipStream_t s = (hipStream_t)streamPtr;
-  if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > 1024) return 4;
+  if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > kFlagSlots) return 4;
   if (nblocks % 2) nblocks += 1;
   const uint64_t nunits = bytes / 16;
 #define SRV(U, SP, LP)                                                                                        \
@@ -239,6 +351,14 @@ extern "C" int mscclppAmdSelfReduceLL16Variant(const void* x, const void* y, voi
     case 14: SRVPM(8, kNonTemporal, kSystem); break;
     case 15: SRVPM(8, kAgent, kAgent); break;
 #undef SRVPM
+#define SRVLDS(U)                                                                                             \
+  hipLaunchKernelGGL((selfReduceLL16LdsKernel<kF16, kSum, U>), dim3(nblocks), dim3(256), 0, s, (const uint8_t*)x, \
+                     (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, (uint64_t)bytes, flags, budgetTicks, err)
+    case 16: SRVLDS(4); break;
+    case 17: SRVLDS(8); break;
+    case 18: SRVLDS(2); break;
+    case 19: SRVLDS(1); break;
+#undef SRVLDS
     default: return 4;
   }
 #undef SRV
@@ -259,14 +379,13 @@ extern "C" int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts
   hipStream_t stream = (hipStream_t)streamPtr;
   if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0) return 4;
   if (nblocks <= 0) {
-    // one 16 KiB payload tile (2048 packets) per workgroup and round; 1024 workgroups = 4 per CU,
-    // all resident at the kernel's 102 VGPRs, so every partner pair is co-resident
-    const uint64_t tiles = (bytes + 16383) / 16384;
+    // one 8 KiB payload tile per workgroup and round; 1024 workgroups = 4 per CU (8 KiB LDS each),
+    // all resident, so every partner pair is co-resident
+    const uint64_t tiles = (bytes + 8191) / 8192;
     nblocks = (int)(tiles < 1024 ? tiles : 1024);
   }
   if (nblocks % 2) nblocks += 1;
   if (nblocks > 1024) return 4;
-  const uint64_t nunits = bytes / 16;
-  MSCCLPP_AMD_DISPATCH_ALL(dtype, op, launchSelfReduce, x, y, pkts, out, nunits, flags, nblocks, budgetTicks, err, stream);
+  MSCCLPP_AMD_DISPATCH_ALL(dtype, op, launchSelfReduce, x, y, pkts, out, (uint64_t)bytes, flags, nblocks, budgetTicks, err, stream);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -14,7 +14,7 @@ out_dir, tag = sys.argv[1], sys.argv[2]
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(root, "profiles")
 os.makedirs(prof, exist_ok=True)
-KERNEL = "selfReduceLL16PmKernel"
+KERNEL = "selfReduceLL16LdsKernel"
 
 
 def rows(pattern):

@@ -24,7 +24,7 @@ dev = torch.device("cuda", 0)
 x = torch.rand(n, device=dev).half()
 y = torch.rand(n, device=dev).half()
 out = torch.empty_like(x)
-flags = torch.ones(1024, dtype=torch.int32, device=dev)
+flags = torch.ones(m.FLAG_SLOTS, dtype=torch.int32, device=dev)
 err = torch.zeros(16, dtype=torch.int32, device=dev)
 pk_unc = m.DeviceBuffer(2 * S, uncached=True)
 pk_reg = m.DeviceBuffer(2 * S, uncached=False)
@@ -54,7 +54,7 @@ for pkname, pk in (("uncached", pk_unc), ("regular", pk_reg)):
     for variant in [int(v) for v in os.environ.get('VARIANTS', '0,5,6,10,11,12,13,14,15').split(',')]:
         if pkname == "regular" and variant in (3, 4, 7, 8, 9, 14):
             continue  # nt / plain stores stay in the writer XCD's L2: never visible cross-XCD
-        for nb in (256, 512, 1024):
+        for nb in [int(g) for g in os.environ.get("GRIDS", "256,512,1024").split(",")]:
             configs.append((pkname, pk, variant, nb))
 # correctness of every config once
 for pkname, pk, variant, nb in configs:
