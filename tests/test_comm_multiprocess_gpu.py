@@ -1,4 +1,4 @@
-"""Two processes, one rank each, both on cuda:0, through the NCCL ABI (ncclGetUniqueId ->
+"""Two (and 4, 8) processes, one rank each, all on cuda:0, through the NCCL ABI (ncclGetUniqueId ->
 ncclCommInitRank -> ncclAllReduce): exercises the TCP bootstrap, hipIpc handle exchange of
 scratch / semaphores / output buffers between processes, and every algorithm, checked bit-exactly
 against the CPU oracle (same LCG inputs as test/torch/correctness_test.py:44-56)."""
@@ -19,9 +19,11 @@ CASES = [  # (algo, dtype code, count)
 ]
 
 
-def _worker(rank, n, uid, q):
+def _worker(rank, n, uid, q, cases=None, rsag=True):
     try:
         os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "5000")
+        if n > 2:  # many ranks on one device: one hardware queue each keeps every rank's queue mapped
+            os.environ["GPU_MAX_HW_QUEUES"] = "1"
         import torch
 
         import mscclpp_amd as m
@@ -31,7 +33,7 @@ def _worker(rank, n, uid, q):
         comm = m.Communicator(rank, n, uid)
         tdt = {0: torch.float16, 1: torch.bfloat16, 2: torch.float32}
         results = []
-        for algo, dt, count in CASES:
+        for algo, dt, count in (cases or CASES):
             ins = [O.lcg(dt, count, r, 3) for r in range(n)]
             x = torch.from_numpy(ins[rank].view(np.int16 if dt < 2 else np.int32).copy()).view(tdt[dt]).cuda()
             out = torch.zeros_like(x)
@@ -61,19 +63,20 @@ def _worker(rank, n, uid, q):
             got = out.cpu().contiguous().view(torch.uint8).numpy()
             results.append((algo, dt, count, errc, int(np.count_nonzero(got != e))))
         # ncclReduceScatter + ncclAllGather reconstruct the AllReduce (fp32, block 8192)
-        block = 8192
+        block = 8192 if rsag else 0
         ins = [O.lcg(2, block * n, r, 9) for r in range(n)]
         x = torch.from_numpy(ins[rank].view(np.int32).copy()).view(torch.float32).cuda()
         rs = torch.zeros(block, dtype=torch.float32, device="cuda")
         ag = torch.zeros(block * n, dtype=torch.float32, device="cuda")
-        for _ in range(2):
-            comm.reduce_scatter(x, rs)
-            comm.all_gather(rs, ag)
-        torch.cuda.synchronize()
-        nw = block * n
-        e = O.allreduce_sliced(2, O.SUM, [a.view(np.uint32) for a in ins], nw, block, 0)[0]
-        got = ag.cpu().numpy().view(np.uint32)
-        results.append(("rs+ag", 2, nw, comm.device_error(), int(np.count_nonzero(got != e))))
+        if rsag:
+            for _ in range(2):
+                comm.reduce_scatter(x, rs)
+                comm.all_gather(rs, ag)
+            torch.cuda.synchronize()
+            nw = block * n
+            e = O.allreduce_sliced(2, O.SUM, [a.view(np.uint32) for a in ins], nw, block, 0)[0]
+            got = ag.cpu().numpy().view(np.uint32)
+            results.append(("rs+ag", 2, nw, comm.device_error(), int(np.count_nonzero(got != e))))
         comm.barrier()
         comm.destroy()
         q.put((rank, results, None))
@@ -81,24 +84,23 @@ def _worker(rank, n, uid, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-def test_two_process_ncclallreduce(built):
+def _run(n, cases=None, rsag=True, timeout=240):
     import mscclpp_amd as m
 
     uid = m.Communicator.unique_id()  # root thread lives in this (parent) process
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    n = 2
-    procs = [ctx.Process(target=_worker, args=(r, n, uid, q)) for r in range(n)]
+    procs = [ctx.Process(target=_worker, args=(r, n, uid, q, cases, rsag)) for r in range(n)]
     for p in procs:
         p.start()
     got = {}
     try:
         for _ in range(n):
-            rank, res, err = q.get(timeout=240)
+            rank, res, err = q.get(timeout=timeout)
             assert err is None, err
             got[rank] = res
     except queue.Empty:
-        pytest.fail("multi-process AllReduce timed out")
+        pytest.fail(f"{n}-process AllReduce timed out")
     finally:
         for p in procs:
             p.join(timeout=30)
@@ -108,6 +110,22 @@ def test_two_process_ncclallreduce(built):
         for algo, dt, count, errc, bad in got[rank]:
             assert errc == 0, (rank, algo, dt, count, errc)
             assert bad == 0, (rank, algo, dt, count, bad)
+
+
+def test_two_process_ncclallreduce(built):
+    _run(2)
+
+
+# 4 and 8 processes sharing one device: the rank counts the 8-GPU node runs (bootstrap with 8
+# peers, 7 IPC mappings per buffer, the n = 4 / 8 slice geometries), at sizes whose launches from
+# every rank fit on the device at once (the spinning kernels of all ranks must be co-resident).
+MANY_CASES = [("allpair", 0, 4096), ("packet", 0, 1 << 17), ("packet", 1, 30001), ("fullmesh", 0, 1 << 19),
+              ("rsag", 2, 100000), ("rsag_zc", 0, 1 << 19), ("auto", 2, 1000), ("auto", 0, 1 << 16)]
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_many_process_ncclallreduce(built, n):
+    _run(n, MANY_CASES, rsag=True, timeout=300)
 
 
 def test_host_proxy_paths(built):
