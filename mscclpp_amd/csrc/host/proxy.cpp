@@ -179,6 +179,15 @@ static double nowSec() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Drain a connection stream by busy-polling hipStreamQuery.  The reference's flush is a blocking
+// stream synchronize (CudaIpcStream::sync, context.cc:37-46); the proxy thread is a dedicated
+// busy-poll core anyway (proxy.cc:42-100), and a blocking wait here measured 0.1-2 ms per flush
+// (interrupt wake-up) against a few microseconds of outstanding copies.
+static void spinSync(hipStream_t s) {
+  while (hipStreamQuery(s) == hipErrorNotReady) {
+  }
+}
+
 // Per-peer host-driven connection: a non-blocking stream (CudaIpcStream, context.cc:16-46).
 struct Conn {
   hipStream_t stream = nullptr;
@@ -198,7 +207,7 @@ class TokenWriter {
   TokenWriter& operator=(const TokenWriter&) = delete;
   void signal(uint64_t* remoteToken, hipStream_t s) {
     ++value_;
-    if (value_ % kSlots == 0) (void)hipStreamSynchronize(s);
+    if (value_ % kSlots == 0) spinSync(s);
     uint64_t* slot = &slots_[value_ % kSlots];
     *slot = value_;
     (void)hipMemcpyAsync(remoteToken, slot, sizeof(uint64_t), hipMemcpyHostToDevice, s);
@@ -394,7 +403,7 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
         writers[q]->signal((uint64_t*)peerTok[q] + rank, conns[q].stream);
       }
       if (t.fields.type & kTriggerSync) {
-        (void)hipStreamSynchronize(conns[q].stream);
+        spinSync(conns[q].stream);
         __atomic_store_n(&flushDone[q * 8], pos + 1, __ATOMIC_RELEASE);
       }
       return false;
@@ -534,7 +543,7 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
         writers[round].signal((uint64_t*)peerTok[next] + round * n + rank, conn.stream);
       }
       if (t.fields.type & kTriggerSync) {
-        (void)hipStreamSynchronize(conn.stream);
+        spinSync(conn.stream);
         __atomic_store_n(&flushDone[round * 8], pos + 1, __ATOMIC_RELEASE);
       }
       return false;
