@@ -92,10 +92,28 @@ def build_audit():
     return AUDIT_LIB
 
 
+TESTBIN = os.path.join(ROOT, "tests", "bin")
+
+
+def build_tests():
+    """C++ test programs (tests/cpp/*.cpp) linked against the product library -> tests/bin/."""
+    os.makedirs(TESTBIN, exist_ok=True)
+    hdrs = _headers()
+    outs = []
+    for src in sorted(glob.glob(os.path.join(ROOT, "tests", "cpp", "*.cpp"))):
+        exe = os.path.join(TESTBIN, os.path.splitext(os.path.basename(src))[0])
+        if _newer(exe, [src, LIB] + hdrs):
+            _run([HIPCC, "-D__HIP_PLATFORM_AMD__", "-O2", "-std=c++17", "-Wall", "-I" + INCLUDE, src, "-o", exe,
+                  "-L" + LIBDIR, "-lmscclpp_amd", "-Wl,-rpath,$ORIGIN/../../mscclpp_amd/lib"])
+        outs.append(exe)
+    return outs
+
+
 def build_all(verbose=False):
     build_oracle()
     build_library(verbose=verbose)
     build_audit()
+    build_tests()
     ref = os.path.join(ROOT, "oracle", "build_ref.sh")
     if os.path.isdir("/root/reference") and os.path.exists(ref):
         # the reference-header harness (oracle/_ref) can only be built where /root/reference exists

@@ -183,6 +183,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
       for (int r = 0; r < nranks; ++r) c->peerTokens[r] = (uint64_t*)toks[r];
       c->ensure(c->llScratch, c->llBytes, c->peerLL, (size_t)64 << 20);
     }
+    c->buildAlgorithms();
     HIPCHECK(hipDeviceSynchronize());
     c->boot->barrier();
     *comm = c.release();
@@ -269,6 +270,29 @@ ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
   return ncclSuccess;
 }
 
+// Select through the communicator's AlgorithmCollection and execute (nccl.cc:578-596): the user's
+// selector first, the built-in one as fallback; no algorithm -> ncclInvalidUsage (there is no
+// NCCL/RCCL underneath to fall back to).
+static int selectAndExecute(ncclComm_t comm, const char* collective, const void* sendbuff, void* recvbuff,
+                            size_t messageSize, size_t inBytes, size_t outBytes, ncclDataType_t datatype,
+                            ncclRedOp_t op, void* stream) {
+  using namespace mscclpp_amd;
+  static const std::unordered_map<std::string, std::vector<uint64_t>> kNoHints;
+  const std::string coll(collective);
+  const DataType dtype = dataTypeFromNccl(datatype);
+  CollectiveRequest req{comm->nranks, comm->nranks, comm->rank, sendbuff, recvbuff, messageSize,
+                        (hipStream_t)stream, coll, dtype, kNoHints};
+  auto algo = comm->algos->selectAlgorithm(req);
+  if (!algo) {
+    warn(std::string("no algorithm selected for ") + collective + " of " + std::to_string(messageSize) + " bytes");
+    return ncclInvalidUsage;
+  }
+  if (algo->type() == AlgorithmType::DSL && !comm->executor) comm->executor = std::make_shared<Executor>(comm->cxx);
+  const ReduceOp rop = op == ncclSum ? SUM : op == ncclMin ? MIN : NOP;
+  return (int)algo->execute(comm->cxx, sendbuff, recvbuff, inBytes, outBytes, dtype, rop, (hipStream_t)stream,
+                            comm->executor);
+}
+
 ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
                            ncclRedOp_t op, ncclComm_t comm, void* stream) {
   return (ncclResult_t)guarded([&] {
@@ -287,7 +311,7 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
       warn("unsupported dtype/op for AllReduce (supported: fp16, bf16, fp32, int32, uint32, fp8 e4m3/e5m2 x sum, min)");
       return (int)ncclInvalidArgument;
     }
-    return comm->allReduce(sendbuff, recvbuff, bytes, dt, o, MSCCLPP_AMD_ALGO_AUTO, 0, 0, (hipStream_t)stream);
+    return selectAndExecute(comm, "allreduce", sendbuff, recvbuff, bytes, bytes, bytes, datatype, op, stream);
   });
 }
 
@@ -305,7 +329,8 @@ ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recv
     if (!sendbuff || !recvbuff || recvcount == 0 || tb == 0) return (int)ncclInvalidArgument;
     const int dt = dtypeFromNccl(datatype), o = opFromNccl(op);
     if (dt < 0 || o < 0) return (int)ncclInvalidArgument;
-    return comm->bulkCollective(1, sendbuff, recvbuff, bytes, dt, o, MSCCLPP_AMD_ALGO_AUTO, 0, 0, (hipStream_t)stream);
+    const size_t total = bytes * (size_t)comm->nranks;  // messageSize = bytes * nRank (nccl.cc:692-697)
+    return selectAndExecute(comm, "reducescatter", sendbuff, recvbuff, total, total, bytes, datatype, op, stream);
   });
 }
 
@@ -321,10 +346,9 @@ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcoun
       return (int)ncclSuccess;
     }
     if (!sendbuff || !recvbuff || sendcount == 0 || tb == 0) return (int)ncclInvalidArgument;
-    const int dt = (tb == 2) ? MSCCLPP_AMD_F16 : MSCCLPP_AMD_F32;  // bytes are moved, not summed
     if (tb != 2 && tb != 4 && tb != 1 && tb != 8) return (int)ncclInvalidArgument;
-    return comm->bulkCollective(2, sendbuff, recvbuff, bytes, dt, MSCCLPP_AMD_SUM, MSCCLPP_AMD_ALGO_AUTO, 0, 0,
-                                (hipStream_t)stream);
+    return selectAndExecute(comm, "allgather", sendbuff, recvbuff, bytes, bytes, bytes * (size_t)comm->nranks,
+                            datatype, ncclSum, stream);
   });
 }
 

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "bootstrap.hpp"
+#include "mscclpp_amd/algorithm.hpp"
 #include "mscclpp_amd/mscclpp_amd.h"
 #include "mscclpp_amd/nccl.h"
 
@@ -81,6 +82,12 @@ int guarded(F&& f) {
   } catch (const HipError& e) {
     warn(e.what());
     return ncclUnhandledCudaError;
+  } catch (const std::invalid_argument& e) {
+    warn(e.what());
+    return ncclInvalidArgument;
+  } catch (const std::logic_error& e) {  // InvalidUsage (e.g. no selector, null executor)
+    warn(e.what());
+    return ncclInvalidUsage;
   } catch (const std::exception& e) {
     warn(e.what());
     return ncclInternalError;
@@ -173,6 +180,13 @@ struct IpcBlob {
 
 struct ncclComm {
   std::unique_ptr<Bootstrap> boot;
+  // the C++ plugin layer (algorithm.cpp): handle passed to Algorithm::execute, the collection the
+  // NCCL entry points select from (nccl.cc:176, :308-314) and the executor for DSL algorithms,
+  // created on the first DSL selection (collective: every rank selects the same algorithm)
+  std::shared_ptr<mscclpp_amd::Communicator> cxx;
+  std::unique_ptr<mscclpp_amd::AlgorithmCollection> algos;
+  std::shared_ptr<mscclpp_amd::Executor> executor;
+  void buildAlgorithms();
   int rank = 0, nranks = 1, device = 0;
   // LL scratch (two halves, packets), bulk scratch, semaphores, flags, error word
   void* llScratch = nullptr;
@@ -185,8 +199,17 @@ struct ncclComm {
   uint32_t* err = nullptr;
   std::array<void*, MSCCLPP_AMD_MAX_RANKS> peerLL{}, peerBulk{};
   std::array<uint64_t*, MSCCLPP_AMD_MAX_RANKS> peerTokens{};
-  // peer mappings opened through IPC: (peer, peer allocation base) -> mapped base here
-  std::map<std::pair<int, uint64_t>, void*> opened;
+  // peer mappings opened through IPC: (peer, peer allocation base) -> handle + mapped base here.
+  // A peer may free an allocation and get a new one at the same address; its handle then differs,
+  // and the old mapping (which would still alias the freed memory) is retired, not reused.  Retired
+  // mappings are closed with the communicator: a stale cached pointer keeps aliasing memory that
+  // stays mapped instead of faulting the GPU.
+  struct OpenedMapping {
+    hipIpcMemHandle_t handle;
+    void* mapped;
+  };
+  std::map<std::pair<int, uint64_t>, OpenedMapping> opened;
+  std::vector<void*> retired;
   // registered output buffers: local allocation base -> per-peer mapped pointers of that buffer
   std::map<std::pair<uint64_t, uint64_t>, std::array<void*, MSCCLPP_AMD_MAX_RANKS>> outRegs;
   std::mutex mu;
@@ -213,13 +236,17 @@ struct ncclComm {
       auto key = std::make_pair(r, all[r].base);
       auto it = opened.find(key);
       void* mapped = nullptr;
-      if (it == opened.end()) {
+      if (it != opened.end() && std::memcmp(&it->second.handle, &all[r].handle, sizeof(hipIpcMemHandle_t)) == 0) {
+        mapped = it->second.mapped;
+      } else {
+        if (it != opened.end()) {
+          retired.push_back(it->second.mapped);
+          opened.erase(it);
+        }
         info("rank " + std::to_string(rank) + ": opening ipc handle of rank " + std::to_string(r));
         HIPCHECK(hipIpcOpenMemHandle(&mapped, all[r].handle, hipIpcMemLazyEnablePeerAccess));
         info("rank " + std::to_string(rank) + ": opened");
-        opened[key] = mapped;
-      } else {
-        mapped = it->second;
+        opened[key] = OpenedMapping{all[r].handle, mapped};
       }
       res[r] = (char*)mapped + all[r].offset;
     }
@@ -228,8 +255,8 @@ struct ncclComm {
 
   void forgetMapping(int peer, void* mappedBase) {
     for (auto it = opened.begin(); it != opened.end(); ++it) {
-      if (it->first.first == peer && it->second == mappedBase) {
-        (void)hipIpcCloseMemHandle(it->second);
+      if (it->first.first == peer && it->second.mapped == mappedBase) {
+        (void)hipIpcCloseMemHandle(it->second.mapped);
         opened.erase(it);
         return;
       }
@@ -385,14 +412,18 @@ struct ncclComm {
 
   void destroy() {
     (void)hipDeviceSynchronize();
+    algos.reset();
+    executor.reset();
     if (boot) {
       try {
         boot->barrier();
       } catch (...) {
       }
     }
-    for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);
+    for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second.mapped);
     opened.clear();
+    for (void* p : retired) (void)hipIpcCloseMemHandle(p);
+    retired.clear();
     if (llScratch) (void)hipFree(llScratch);
     if (bulkScratch) (void)hipFree(bulkScratch);
     if (tokens) (void)hipFree(tokens);

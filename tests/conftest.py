@@ -23,4 +23,5 @@ def built():
     _build.build_oracle()
     _build.build_library()
     _build.build_audit()
+    _build.build_tests()
     return True
