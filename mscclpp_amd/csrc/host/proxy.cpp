@@ -184,6 +184,14 @@ static double nowSec() {
 // busy-poll core anyway (proxy.cc:42-100), and a blocking wait here measured 0.1-2 ms per flush
 // (interrupt wake-up) against a few microseconds of outstanding copies.
 static void spinSync(hipStream_t s) {
+  static const bool blocking = [] {
+    const char* e = std::getenv("MSCCLPP_AMD_PROXY_BLOCKING_SYNC");
+    return e && *e == '1';
+  }();
+  if (blocking) {
+    (void)hipStreamSynchronize(s);
+    return;
+  }
   while (hipStreamQuery(s) == hipErrorNotReady) {
   }
 }
@@ -582,7 +590,17 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     HIPCHECK(hipMemcpy(back.data(), buff, bytes, hipMemcpyDeviceToHost));
     bool ok = true;
     const int expected = n * (n - 1) / 2;
-    for (size_t i = 0; i < nelems && ok; ++i) ok = back[i] == expected;
+    size_t nbad = 0, firstBad = nelems;
+    for (size_t i = 0; i < nelems; ++i)
+      if (back[i] != expected && nbad++ == 0) firstBad = i;
+    ok = nbad == 0;
+    if (!ok) {
+      uint32_t e0 = 0;
+      (void)hipMemcpy(&e0, err, 4, hipMemcpyDeviceToHost);
+      warn("proxy ring allreduce rank " + std::to_string(rank) + ": " + std::to_string(nbad) + " wrong of " +
+           std::to_string(nelems) + ", first at " + std::to_string(firstBad) + " = " +
+           std::to_string(back[firstBad]) + ", device error " + std::to_string(e0));
+    }
     comm->boot->barrier();
     // benchTime: iters launches in one graph, graphLaunches replays after a barrier
     hipGraph_t graph;

@@ -112,7 +112,12 @@ __global__ void __launch_bounds__(1024) ringProxyAllReduceKernel(int* buff, cons
   size_t chunkIndex = (rank + n - 1) % n;
   size_t offset = chunkIndex * chunkNelem * sizeof(int);
   if (isComm && chunkNelem > 1) ch.fstSend.putWithSignal(offset, offset, half * sizeof(int));
-  // steps 2 .. n-1 (:753-781)
+  // steps 2 .. n-1 (:753-781).  Deviation: the reference has block 0's thread 0 trigger the put of
+  // a half-chunk right after ITS OWN share of the vectorSum that produced it, while the other blocks
+  // may still be summing that half (:765-772, :790-797, :803-811); the proxy's copy then reads a
+  // partly reduced half.  With large halves (256 MiB at 1 GiB, 2 ranks) the copy engine starts
+  // before the sum is done and the result is wrong (seen intermittently here).  A grid barrier
+  // between every vectorSum and the put of its output closes the race; nothing else changes.
   for (int step = 2; step < n; ++step) {
     if (isComm) {
       if (chunkNelem > 1) {
@@ -127,6 +132,7 @@ __global__ void __launch_bounds__(1024) ringProxyAllReduceKernel(int* buff, cons
     int* dst = (int*)((char*)buff + offset);
     const int* src = (const int*)((const char*)scratch + offset);
     ringVectorSum(dst, src, half);
+    grid_sync(gb, budget, err);  // the first half is reduced everywhere before it is sent
     if (isComm) {
       ch.fstRecv.wait();
       ch.fstSend.flush();
@@ -134,6 +140,7 @@ __global__ void __launch_bounds__(1024) ringProxyAllReduceKernel(int* buff, cons
     }
     grid_sync(gb, budget, err);
     ringVectorSum(dst + half, src + half, rest);
+    grid_sync(gb, budget, err);  // ... and the second half before the next step sends it
   }
   // step n (:783-815)
   if (isComm) {
@@ -148,6 +155,7 @@ __global__ void __launch_bounds__(1024) ringProxyAllReduceKernel(int* buff, cons
   int* dst = (int*)((char*)buff + offset);
   const int* src = (const int*)((const char*)scratch + offset);
   ringVectorSum(dst, src, half);
+  grid_sync(gb, budget, err);
   if (isComm) {
     ch.fstRecv.wait();
     ch.fstSend.flush();
@@ -155,6 +163,7 @@ __global__ void __launch_bounds__(1024) ringProxyAllReduceKernel(int* buff, cons
   }
   grid_sync(gb, budget, err);
   ringVectorSum(dst + half, src + half, rest);
+  grid_sync(gb, budget, err);
   if (isComm) {
     if (chunkNelem > 1) {
       ch.sndRecv.wait();

@@ -141,3 +141,50 @@ def test_host_proxy_paths(built):
     assert res["us_per_kernel_graph"] > 0
     for mode, r in res["portchannel_alltoall_1MiB"].items():
         assert r["correct"], (mode, r)
+
+
+def _ring_worker(rank, n, uid, q, nelems, nblocks):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "20000")
+        import torch
+
+        import mscclpp_amd as m
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        us, ok, _ = comm.proxy_ring_all_reduce(nelems, iters=1, graph_launches=1, nblocks=nblocks)
+        errc = comm.device_error()
+        comm.destroy()
+        q.put((rank, (ok, errc), None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("nblocks", [2, 24])
+def test_proxy_ring_reduced_halves_are_complete_before_put(built, nblocks):
+    """mscclpp-test allreduce1 with 128 MiB halves and few workgroups: the sum of a half takes far
+    longer than the proxy needs to start copying it, so a put triggered before every workgroup has
+    finished its share of the sum (the reference's ordering, allreduce_test.cu:765-811) sends a
+    partly reduced half.  The grid barrier before each such put must make the result exact."""
+    import mscclpp_amd as m
+
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    uid = m.Communicator.unique_id()
+    procs = [ctx.Process(target=_ring_worker, args=(r, n, uid, q, 1 << 27, nblocks)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=200)
+            assert err is None, err
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        assert got[rank] == (True, 0), (rank, got[rank])
