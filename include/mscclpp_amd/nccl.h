@@ -87,6 +87,17 @@ typedef struct ncclConfig_v21700 {
   int splitShare;
 } ncclConfig_t;
 
+#define NCCL_SPLIT_NOCOLOR -1
+
+typedef enum { ncclScalarDevice = 0, ncclScalarHostImmediate = 1 } ncclScalarResidence_t;
+
+typedef struct ncclSimInfo_v22200 {
+  size_t size;
+  unsigned int magic;
+  unsigned int version;
+  float estimatedTime;
+} ncclSimInfo_t;
+
 /* nccl.cc:187 */ ncclResult_t ncclGetVersion(int* version);
 /* nccl.cc:196 */ ncclResult_t ncclGetUniqueId(ncclUniqueId* uniqueId);
 /* nccl.cc:281 */ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank);
@@ -108,6 +119,36 @@ typedef struct ncclConfig_v21700 {
                                                  ncclDataType_t datatype, ncclRedOp_t op, ncclComm_t comm, void* stream);
 /* nccl.cc:718 */ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcount,
                                              ncclDataType_t datatype, ncclComm_t comm, void* stream);
+/* Native zero-copy pull from the root over xGMI (nccl.cc:544-605). */
+/* nccl.cc:549 */ ncclResult_t ncclBroadcast(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                                             int root, ncclComm_t comm, void* stream);
+/* nccl.cc:544 */ ncclResult_t ncclBcast(void* buff, size_t count, ncclDataType_t datatype, int root, ncclComm_t comm,
+                                         void* stream);
+/* nccl.cc:405 -- a new communicator per color over the same bootstrap, ranks ordered by key */
+/* nccl.cc:405 */ ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm,
+                                             ncclConfig_t* config);
+/* Not carried by this path: forwarded to the vendor library named by MSCCLPP_AMD_NCCL_LIB_PATH
+ * (the reference's MSCCLPP_NCCL_LIB_PATH fallback, nccl.cc:84-124, :331-346) when it is set,
+ * otherwise they return ncclInvalidUsage (one rank: a local copy where the operation defines one). */
+/* nccl.cc:533 */ ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                                          ncclRedOp_t op, int root, ncclComm_t comm, void* stream);
+/* nccl.cc:774 */ ncclResult_t ncclSend(const void* sendbuff, size_t count, ncclDataType_t datatype, int peer,
+                                        ncclComm_t comm, void* stream);
+/* nccl.cc:784 */ ncclResult_t ncclRecv(void* recvbuff, size_t count, ncclDataType_t datatype, int peer, ncclComm_t comm,
+                                        void* stream);
+/* nccl.cc:794 */ ncclResult_t ncclAllToAll(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                                            ncclComm_t comm, void* stream);
+/* nccl.cc:808 */ ncclResult_t ncclAllToAllv(const void* sendbuff, const size_t sendcounts[], const size_t sdispls[],
+                                             void* recvbuff, const size_t recvcounts[], const size_t rdispls[],
+                                             ncclDataType_t datatype, ncclComm_t comm, void* stream);
+/* nccl.cc:521 */ ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar, ncclDataType_t datatype,
+                                                        ncclScalarResidence_t residence, ncclComm_t comm);
+/* nccl.cc:527 */ ncclResult_t ncclRedOpDestroy(ncclRedOp_t op, ncclComm_t comm);
+/* nccl.cc:437 */ ncclResult_t ncclCommInitRankScalable(ncclComm_t* newcomm, int nranks, int myrank, int nId,
+                                                        ncclUniqueId* commIds, ncclConfig_t* config);
+/* nccl.cc:840 */ ncclResult_t ncclGroupSimulateEnd(ncclSimInfo_t* simInfo);
+/* nccl.cc:846 */ ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
+/* nccl.cc:852 */ ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle);
 /* nccl.cc:823 */ ncclResult_t ncclGroupStart(void);
 /* nccl.cc:832 */ ncclResult_t ncclGroupEnd(void);
 /* nccl.cc:858 */ ncclResult_t ncclMemAlloc(void** ptr, size_t size);

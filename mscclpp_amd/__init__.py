@@ -101,6 +101,9 @@ def lib():
         "mscclppAmdCollectiveLaunch": [i32, i32, ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, i32, u64, vp],
         "ncclReduceScatter": [vp, vp, sz, i32, i32, vp, vp],
         "ncclAllGather": [vp, vp, sz, i32, vp, vp],
+        "ncclBroadcast": [vp, vp, sz, i32, i32, vp, vp],
+        "ncclCommSplit": [vp, i32, i32, ctypes.POINTER(vp), vp],
+        "mscclppAmdBroadcastLaunch": [ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, u64, vp],
         "ncclGetUniqueId": [ctypes.POINTER(UniqueId)],
         "ncclCommInitRank": [ctypes.POINTER(vp), i32, UniqueId, i32],
         "ncclCommDestroy": [vp],
@@ -264,6 +267,16 @@ class InProcessRanks:
                                                 budget_ticks, stream_ptr(stream))
         check(code, "in-process collective")
 
+    def broadcast(self, sends, recvs, root, nblocks=0, nthreads=0, budget_ticks=500_000_000, stream=None):
+        """ncclBroadcast for in-process ranks: recvs[r] <- sends[root] (sends[r] read on the root only)."""
+        nbytes = recvs[0].numel() * recvs[0].element_size()
+        arr = self.views(sends, recvs)
+        for r in range(self.n):
+            arr[r].peerInput[root] = sends[root].data_ptr()
+        code = lib().mscclppAmdBroadcastLaunch(arr, self.n, self.n, nbytes, root, nblocks, nthreads, budget_ticks,
+                                               stream_ptr(stream))
+        check(code, "in-process broadcast")
+
     def errors(self):
         return [int(e[0].item()) for e in self.err]
 
@@ -346,6 +359,27 @@ class Communicator:
         check(lib().ncclAllGather(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(recv.data_ptr()), send.numel(),
                                   NCCL_DTYPES[send.dtype], self.comm, stream_ptr(stream)), "ncclAllGather")
         return recv
+
+    def broadcast(self, send, recv=None, root=0, stream=None):
+        """ncclBroadcast(send, recv, count, dtype, root, comm, stream); send is read on the root only."""
+        recv = send if recv is None else recv
+        check(lib().ncclBroadcast(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(recv.data_ptr()), recv.numel(),
+                                  NCCL_DTYPES[recv.dtype], root, self.comm, stream_ptr(stream)), "ncclBroadcast")
+        return recv
+
+    def split(self, color, key):
+        """ncclCommSplit(comm, color, key, &newcomm, NULL) -> Communicator, or None for NCCL_SPLIT_NOCOLOR."""
+        c = ctypes.c_void_p()
+        check(lib().ncclCommSplit(self.comm, color, key, ctypes.byref(c), None), "ncclCommSplit")
+        if not c.value:
+            return None
+        sub = Communicator.__new__(Communicator)
+        sub.comm = c
+        r, n = ctypes.c_int(), ctypes.c_int()
+        check(lib().ncclCommUserRank(c, ctypes.byref(r)), "ncclCommUserRank")
+        check(lib().ncclCommCount(c, ctypes.byref(n)), "ncclCommCount")
+        sub.rank, sub.nranks = r.value, n.value
+        return sub
 
     def proxy_ring_all_reduce(self, nelems, iters=20, graph_launches=15, nblocks=0):
         """mscclpp-test allreduce1: int32 ring RS+AG through the host proxy (input = rank).

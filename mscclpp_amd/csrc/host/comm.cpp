@@ -184,6 +184,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
       c->ensure(c->llScratch, c->llBytes, c->peerLL, (size_t)64 << 20);
     }
     c->buildAlgorithms();
+    initFallbackComm(c.get());  // vendor communicator for operations outside this path (nccl.cc:323-346)
     HIPCHECK(hipDeviceSynchronize());
     c->boot->barrier();
     *comm = c.release();
@@ -208,12 +209,17 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comm, int ndev, const int*) {
 
 ncclResult_t ncclCommFinalize(ncclComm_t comm) {
   if (!comm) return ncclInvalidArgument;
+  if (comm->fallback && vendorNccl()->CommFinalize) {  // nccl.cc:367-373
+    const ncclResult_t r = vendorNccl()->CommFinalize((ncclComm_t)comm->fallback);
+    if (r != ncclSuccess) return r;
+  }
   return ncclSuccess;
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (!comm) return ncclInvalidArgument;
   return (ncclResult_t)guarded([&] {
+    destroyFallbackComm(comm, false);
     comm->destroy();
     delete comm;
     return (int)ncclSuccess;
@@ -222,7 +228,12 @@ ncclResult_t ncclCommDestroy(ncclComm_t comm) {
 
 ncclResult_t ncclCommAbort(ncclComm_t comm) {
   if (!comm) return ncclSuccess;
-  return ncclCommDestroy(comm);
+  return (ncclResult_t)guarded([&] {
+    destroyFallbackComm(comm, true);
+    comm->destroy();
+    delete comm;
+    return (int)ncclSuccess;
+  });
 }
 
 const char* ncclGetErrorString(ncclResult_t result) {
@@ -243,8 +254,15 @@ const char* ncclGetLastError(ncclComm_t) { return gLastError.c_str(); }
 
 ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
   if (!comm || !asyncError) return ncclInvalidArgument;
+  // Polled by frameworks' watchdog threads: read the error word on a stream of its own, never the
+  // null stream (which would wait behind every blocking stream's queued collectives).
   uint32_t code = 0;
-  if (hipMemcpy(&code, comm->err, sizeof(code), hipMemcpyDeviceToHost) != hipSuccess) {
+  if (!comm->errStream && hipStreamCreateWithFlags(&comm->errStream, hipStreamNonBlocking) != hipSuccess) {
+    *asyncError = ncclUnhandledCudaError;
+    return ncclSuccess;
+  }
+  if (hipMemcpyAsync(&code, comm->err, sizeof(code), hipMemcpyDeviceToHost, comm->errStream) != hipSuccess ||
+      hipStreamSynchronize(comm->errStream) != hipSuccess) {
     *asyncError = ncclUnhandledCudaError;
     return ncclSuccess;
   }
@@ -289,8 +307,12 @@ static int selectAndExecute(ncclComm_t comm, const char* collective, const void*
   }
   if (algo->type() == AlgorithmType::DSL && !comm->executor) comm->executor = std::make_shared<Executor>(comm->cxx);
   const ReduceOp rop = op == ncclSum ? SUM : op == ncclMin ? MIN : NOP;
-  return (int)algo->execute(comm->cxx, sendbuff, recvbuff, inBytes, outBytes, dtype, rop, (hipStream_t)stream,
-                            comm->executor);
+  const int rc = (int)algo->execute(comm->cxx, sendbuff, recvbuff, inBytes, outBytes, dtype, rop, (hipStream_t)stream,
+                                    comm->executor);
+  if (rc != ncclSuccess)
+    warn(std::string(collective) + " via " + algo->name() + " of " + std::to_string(messageSize) +
+         " bytes failed with code " + std::to_string(rc) + " (HIP: " + hipGetErrorString(hipPeekAtLastError()) + ")");
+  return rc;
 }
 
 ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
@@ -307,6 +329,8 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     if (!sendbuff || !recvbuff || count == 0 || tb == 0) return (int)ncclInvalidArgument;  // nccl.cc:617-622
     const int dt = dtypeFromNccl(datatype);
     const int o = opFromNccl(op);
+    if (comm->fallback && (dt < 0 || o < 0 || forcedFallback("allreduce")))  // nccl.cc:628-632
+      return (int)vendorNccl()->AllReduce(sendbuff, recvbuff, count, datatype, op, (ncclComm_t)comm->fallback, stream);
     if (dt < 0 || o < 0) {
       warn("unsupported dtype/op for AllReduce (supported: fp16, bf16, fp32, int32, uint32, fp8 e4m3/e5m2 x sum, min)");
       return (int)ncclInvalidArgument;
@@ -328,6 +352,9 @@ ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recv
     }
     if (!sendbuff || !recvbuff || recvcount == 0 || tb == 0) return (int)ncclInvalidArgument;
     const int dt = dtypeFromNccl(datatype), o = opFromNccl(op);
+    if (comm->fallback && (dt < 0 || o < 0 || forcedFallback("reducescatter")))  // nccl.cc:682-686
+      return (int)vendorNccl()->ReduceScatter(sendbuff, recvbuff, recvcount, datatype, op, (ncclComm_t)comm->fallback,
+                                              stream);
     if (dt < 0 || o < 0) return (int)ncclInvalidArgument;
     const size_t total = bytes * (size_t)comm->nranks;  // messageSize = bytes * nRank (nccl.cc:692-697)
     return selectAndExecute(comm, "reducescatter", sendbuff, recvbuff, total, total, bytes, datatype, op, stream);
@@ -346,14 +373,18 @@ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcoun
       return (int)ncclSuccess;
     }
     if (!sendbuff || !recvbuff || sendcount == 0 || tb == 0) return (int)ncclInvalidArgument;
+    if (comm->fallback && (bytes % 16 || forcedFallback("allgather")))  // nccl.cc:736-739
+      return (int)vendorNccl()->AllGather(sendbuff, recvbuff, sendcount, datatype, (ncclComm_t)comm->fallback, stream);
     if (tb != 2 && tb != 4 && tb != 1 && tb != 8) return (int)ncclInvalidArgument;
     return selectAndExecute(comm, "allgather", sendbuff, recvbuff, bytes, bytes, bytes * (size_t)comm->nranks,
                             datatype, ncclSum, stream);
   });
 }
 
-ncclResult_t ncclGroupStart(void) { return ncclSuccess; }
-ncclResult_t ncclGroupEnd(void) { return ncclSuccess; }
+// Native operations run when called (a group does not defer them); with a vendor library the group
+// calls are forwarded so grouped vendor operations (send/recv) keep their semantics (nccl.cc:823-838).
+ncclResult_t ncclGroupStart(void) { return vendorNccl() ? vendorNccl()->GroupStart() : ncclSuccess; }
+ncclResult_t ncclGroupEnd(void) { return vendorNccl() ? vendorNccl()->GroupEnd() : ncclSuccess; }
 
 ncclResult_t ncclMemAlloc(void** ptr, size_t size) {
   return (ncclResult_t)guarded([&] {

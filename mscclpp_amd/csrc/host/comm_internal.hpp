@@ -27,6 +27,8 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
                          int dtype, int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
 int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
                         int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
+int launchBroadcast(const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int root, int nblocks,
+                    int nthreads, uint64_t budget, hipStream_t s);
 size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype);
 size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype);
 size_t testLLScratchRequired(int nranks, size_t bytes);
@@ -185,6 +187,10 @@ struct ncclComm {
   // created on the first DSL selection (collective: every rank selects the same algorithm)
   std::shared_ptr<mscclpp_amd::Communicator> cxx;
   std::unique_ptr<mscclpp_amd::AlgorithmCollection> algos;
+  // the vendor library's communicator for operations this path does not carry (nccl.cc:331-346),
+  // present when MSCCLPP_AMD_NCCL_LIB_PATH names librccl (nccl_compat.cpp)
+  void* fallback = nullptr;
+  hipStream_t errStream = nullptr;  // ncclCommGetAsyncError's reads
   std::shared_ptr<mscclpp_amd::Executor> executor;
   void buildAlgorithms();
   int rank = 0, nranks = 1, device = 0;
@@ -314,6 +320,43 @@ struct ncclComm {
     return res;
   }
 
+  // Broadcast: every rank all-gathers an IPC handle (root: its send buffer; others: their receive
+  // buffer, only so the call stays collective) and opens only the root's.  Done on every call: the
+  // root's buffer is not known to the other ranks in advance, so a per-buffer cache could not stay
+  // consistent across ranks.
+  int broadcast(const void* send, void* recv, size_t bytes, int root, int nblocks, int nthreads, hipStream_t stream) {
+    std::lock_guard<std::mutex> lk(mu);
+    void* mine = rank == root ? const_cast<void*>(send) : recv;
+    IpcBlob blob{};
+    void* base = nullptr;
+    size_t sz = 0;
+    HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)mine));
+    HIPCHECK(hipIpcGetMemHandle(&blob.handle, base));
+    blob.base = (uint64_t)base;
+    blob.offset = (uint64_t)((char*)mine - (char*)base);
+    blob.bytes = sz;
+    std::vector<IpcBlob> all(nranks);
+    boot->allGather(&blob, all.data(), sizeof(IpcBlob));
+    mscclppAmdRankView v = baseView(rank == root ? send : recv, recv);
+    if (rank != root) {
+      auto key = std::make_pair(root, all[root].base);
+      auto it = opened.find(key);
+      void* mapped = nullptr;
+      if (it != opened.end() && std::memcmp(&it->second.handle, &all[root].handle, sizeof(hipIpcMemHandle_t)) == 0) {
+        mapped = it->second.mapped;
+      } else {
+        if (it != opened.end()) {
+          retired.push_back(it->second.mapped);
+          opened.erase(it);
+        }
+        HIPCHECK(hipIpcOpenMemHandle(&mapped, all[root].handle, hipIpcMemLazyEnablePeerAccess));
+        opened[key] = OpenedMapping{all[root].handle, mapped};
+      }
+      v.peerInput[root] = (char*)mapped + all[root].offset;
+    }
+    return launchBroadcast(&v, 1, nranks, bytes, root, nblocks, nthreads, spinBudgetTicks(), stream);
+  }
+
   mscclppAmdRankView baseView(const void* in, void* out) {
     mscclppAmdRankView v{};
     v.input = in;
@@ -430,9 +473,46 @@ struct ncclComm {
     if (expected) (void)hipFree(expected);
     if (flags) (void)hipFree(flags);
     if (err) (void)hipFree(err);
+    if (errStream) (void)hipStreamDestroy(errStream);
+    errStream = nullptr;
     llScratch = bulkScratch = nullptr;
     tokens = expected = nullptr;
     flags = err = nullptr;
   }
 };
+
+// ---- vendor NCCL fallback (nccl_compat.cpp) --------------------------------------------------
+namespace mscclpp_amd {
+namespace host {
+struct VendorNccl {
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommFinalize)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, void*) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, void*) = nullptr;
+  ncclResult_t (*ReduceScatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, void*) = nullptr;
+  ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, void*) = nullptr;
+  ncclResult_t (*Reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t, void*) = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, void*) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, void*) = nullptr;
+  ncclResult_t (*AllToAll)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, void*) = nullptr;
+  ncclResult_t (*AllToAllv)(const void*, const size_t[], const size_t[], void*, const size_t[], const size_t[],
+                            ncclDataType_t, ncclComm_t, void*) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  ncclResult_t (*GroupSimulateEnd)(ncclSimInfo_t*) = nullptr;
+  ncclResult_t (*RedOpCreatePreMulSum)(ncclRedOp_t*, void*, ncclDataType_t, ncclScalarResidence_t, ncclComm_t) = nullptr;
+  ncclResult_t (*RedOpDestroy)(ncclRedOp_t, ncclComm_t) = nullptr;
+};
+// The vendor library named by MSCCLPP_AMD_NCCL_LIB_PATH (or MSCCLPP_NCCL_LIB_PATH), or null.
+const VendorNccl* vendorNccl();
+// MSCCLPP_AMD_FORCE_NCCL_FALLBACK_OPERATION ("all" or a comma list of allreduce, allgather,
+// reducescatter, broadcast) names `op`.
+bool forcedFallback(const char* op);
+void initFallbackComm(ncclComm* c);                 // collective over c's bootstrap
+void destroyFallbackComm(ncclComm* c, bool abort);
+}  // namespace host
+}  // namespace mscclpp_amd
 

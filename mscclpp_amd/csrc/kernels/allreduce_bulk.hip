@@ -287,6 +287,51 @@ __global__ void __launch_bounds__(512) allreduceTestK5Kernel(Views<NV> views, Bu
   block_handshake(v, nranks, rank, b, budget);
 }
 
+// ncclBroadcast (nccl.cc:549-605; the reference runs it through its algorithm collection or falls
+// back to NCCL): a zero-copy pull from the root.  Each workgroup owns one sub-range.  Entry
+// handshake: the root's send buffer is final (its producer ran earlier on the root's stream) and
+// every reader's previous use of its receive buffer is over.  Non-roots then read the root's send
+// buffer over xGMI (system-scope 16-byte loads) and store into their own receive buffer; the root
+// copies send -> recv when out of place.  Exit handshake: every reader is done with the root's
+// buffer before any rank's kernel ends, so the root may overwrite it in its next stream operation.
+template <int NV, int U>
+__global__ void __launch_bounds__(512) broadcastKernel(Views<NV> views, uint64_t bytes, uint64_t blk, int nranks,
+                                                       int root, uint64_t budget) {
+  const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
+  const int rank = v.rank;
+  const uint32_t T = blockDim.x, tid = threadIdx.x, b = blockIdx.x;
+  const uint64_t bOff = (uint64_t)b * blk;
+  block_handshake(v, nranks, rank, b, budget);
+  if (bOff < bytes) {
+    const uint64_t len = bytes - bOff < blk ? bytes - bOff : blk;
+    const uint8_t* src = (rank == root ? (const uint8_t*)v.input : (const uint8_t*)v.peerInput[root]) + bOff;
+    uint8_t* dst = (uint8_t*)v.output + bOff;
+    if (src != dst) {
+      const auto rs = make_rsrc(src);
+      const auto rd = make_rsrc(dst);
+      const uint32_t nUnits = (uint32_t)((len + 15) / 16);
+      for (uint32_t u0 = tid; u0 < nUnits; u0 += T * U) {
+        u32x4 w[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          const uint32_t u = u0 + k * T;
+          const uint32_t vb = u < nUnits ? clamp_valid(len, (uint64_t)u * 16, 16) : 0;
+          if (vb >= 16)
+            w[k] = load16<kSystem>(rs, u * 16u);
+          else if (vb)
+            w[k] = load_tail(src + (uint64_t)u * 16, vb);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          const uint32_t u = u0 + k * T;
+          if (u < nUnits) store_payload<kPlain>(rd, dst, (uint64_t)u * 16, w[k], clamp_valid(len, (uint64_t)u * 16, 16));
+        }
+      }
+    }
+  }
+  block_handshake(v, nranks, rank, b, budget);
+}
+
 static thread_local int g_launch_status = 0;
 
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks) {
@@ -445,6 +490,32 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
   MSCCLPP_AMD_DISPATCH_ALL(dtype, op, launchBulk, views, nviews, g, nranks, nblocks, nthreads, budget, s, order, mode);
   if (g_launch_status) return g_launch_status;
   return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+int launchBroadcast(const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int root, int nblocks,
+                    int nthreads, uint64_t budget, hipStream_t s) {
+  if (nblocks <= 0) {  // 256 KiB per workgroup, 8..128 workgroups
+    const uint64_t want = (bytes + (256u << 10) - 1) / (256u << 10);
+    nblocks = (int)(want < 8 ? 8 : want > 128 ? 128 : want);
+  }
+  if (nthreads <= 0) nthreads = 512;
+  if (nblocks > kMaxChannels || nthreads > 512 || nthreads % 64 || nthreads < 64) return 4;
+  if (root < 0 || root >= nranks || bytes == 0) return 4;
+  const uint64_t blk = ((bytes + nblocks - 1) / nblocks + 15) & ~15ull;
+  auto go = [&](auto kern, auto vw) {
+    if (!grid_coresident(kern, nthreads, (long)nblocks * nviews)) return 5;
+    hipLaunchKernelGGL(kern, dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, (uint64_t)bytes, blk, nranks, root,
+                       budget);
+    return hipGetLastError() == hipSuccess ? 0 : 1;
+  };
+  if (nviews == 1) {
+    Views<1> vw;
+    vw.v[0] = views[0];
+    return go(broadcastKernel<1, 4>, vw);
+  }
+  Views<kMaxRanks> vw{};
+  for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
+  return go(broadcastKernel<kMaxRanks, 4>, vw);
 }
 
 int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,

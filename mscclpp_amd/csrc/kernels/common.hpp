@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "mscclpp_amd/device.hpp"
 #include "mscclpp_amd/mscclpp_amd.h"
@@ -33,12 +34,18 @@ inline bool grid_coresident(Kernel kernel, int threads, long blocks) {
   if (kernel != cKernel || dev != cDev || threads != cThreads) {
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess) return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess) {
+      fprintf(stderr, "[mscclpp_amd WARN] occupancy query failed: %s\n", hipGetErrorString(hipGetLastError()));
+      return false;
+    }
     cKernel = kernel;
     cDev = dev;
     cThreads = threads;
     cCap = (long)per * cus;
   }
+  if (cCap < blocks)
+    fprintf(stderr, "[mscclpp_amd WARN] %ld workgroups of %d lanes cannot be co-resident (device %d holds %ld)\n",
+            blocks, threads, dev, cCap);
   return cCap >= blocks;
 }
 

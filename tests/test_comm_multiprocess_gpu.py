@@ -188,3 +188,69 @@ def test_proxy_ring_reduced_halves_are_complete_before_put(built, nblocks):
                 p.kill()
     for rank in range(n):
         assert got[rank] == (True, 0), (rank, got[rank])
+
+
+def _bcast_split_worker(rank, n, uid, q):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "5000")
+        import torch
+
+        import mscclpp_amd as m
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        out = []
+        # ncclBroadcast out of place from the last rank, then ncclBcast in place from rank 0
+        x = torch.arange(12345, dtype=torch.float32, device="cuda") * (rank + 1)
+        y = torch.zeros_like(x)
+        comm.broadcast(x, y, root=n - 1)
+        torch.cuda.synchronize()
+        out.append(bool(torch.equal(y, torch.arange(12345, dtype=torch.float32, device="cuda") * n)))
+        z = torch.full((1 << 20,), float(rank), dtype=torch.float16, device="cuda")
+        comm.broadcast(z, root=0)
+        torch.cuda.synchronize()
+        out.append(bool(torch.all(z == 0)))
+        # ncclCommSplit: everyone in one color (same group, reversed order by key), then singletons
+        sub = comm.split(0, n - 1 - rank)
+        out.append(sub.rank == n - 1 - rank and sub.nranks == n)
+        a = torch.full((4096,), float(sub.rank + 1), dtype=torch.float16, device="cuda")
+        sub.all_reduce(a)
+        torch.cuda.synchronize()
+        out.append(bool(torch.all(a == n * (n + 1) / 2)))
+        solo = comm.split(rank, 0)
+        out.append(solo.nranks == 1 and solo.rank == 0)
+        none = comm.split(-1 if rank == 0 else 5, 0)  # NCCL_SPLIT_NOCOLOR -> no communicator
+        out.append((none is None) if rank == 0 else (none is not None and none.nranks == n - 1))
+        for c in (sub, solo, none):
+            if c is not None:
+                c.destroy()
+        out.append(comm.device_error())
+        comm.destroy()
+        q.put((rank, out, None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_broadcast_and_split_two_processes(built):
+    import mscclpp_amd as m
+
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    uid = m.Communicator.unique_id()
+    procs = [ctx.Process(target=_bcast_split_worker, args=(r, n, uid, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=200)
+            assert err is None, err
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        assert got[rank] == [True, True, True, True, True, True, 0], (rank, got[rank])

@@ -60,3 +60,40 @@ def test_invalid_arguments_rejected_without_gpu(built):
     arr = (m.RankView * 1)()
     assert L.mscclppAmdAllReduceLaunch(1, arr, 1, 1, 1024, 0, 0, 0, 0, 0, None) == 4  # nranks < 2
     assert L.mscclppAmdAllReduceLaunch(1, arr, 1, 8, 1024, 9, 0, 0, 0, 0, None) == 4  # bad dtype
+
+
+def test_exports_every_nccl_symbol_torch_imports(built):
+    """Under LD_PRELOAD / LD_AUDIT the library stands in for librccl: every ncclXxx symbol that
+    libtorch_hip.so binds must resolve to it, or torch would call the vendor library with this
+    library's communicator."""
+    import glob
+    import subprocess
+
+    import torch
+
+    import mscclpp_amd as m
+
+    libs = glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib", "libtorch_hip.so"))
+    if not libs:
+        pytest.skip("no libtorch_hip.so in this torch build")
+    undef = subprocess.run(["nm", "-D", "--undefined-only", libs[0]], stdout=subprocess.PIPE, text=True).stdout
+    wanted = {ln.split()[-1].split("@")[0] for ln in undef.splitlines() if " nccl" in ln}
+    ours = subprocess.run(["nm", "-D", "--defined-only", m.LIB_PATH], stdout=subprocess.PIPE, text=True).stdout
+    have = {ln.split()[-1] for ln in ours.splitlines() if " T " in ln}
+    assert wanted, "expected torch to import NCCL symbols"
+    assert not (wanted - have), sorted(wanted - have)
+
+
+def test_vendor_fallback_absent_means_invalid_usage(built):
+    """Without MSCCLPP_AMD_NCCL_LIB_PATH, operations outside the path answer ncclInvalidUsage /
+    ncclInvalidArgument instead of crashing (no communicator or GPU needed for these checks)."""
+    import mscclpp_amd as m
+
+    L = m.lib()
+    vp = ctypes.c_void_p
+    L.ncclSend.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, vp, vp]
+    L.ncclCommRegister.argtypes = [vp, vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+    assert L.ncclSend(None, 1, 7, 0, None, None) == 4  # null communicator
+    h = vp()
+    assert L.ncclCommRegister(None, None, 0, ctypes.byref(h)) == 4
+    assert L.ncclGroupStart() == 0 and L.ncclGroupEnd() == 0
