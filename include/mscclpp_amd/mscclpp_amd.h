@@ -128,6 +128,9 @@ int mscclppAmdCommAllReduceAccum(ncclComm_t comm, const void* sendbuff, void* re
 /* Reduce-type code (MSCCLPP_AMD_*) for an ncclDataType_t and accumulation type (-1 = AUTO), or -1. */
 int mscclppAmdReduceType(int ncclDtype, int accumNcclDtype);
 int mscclppAmdCommBarrier(ncclComm_t comm);
+/* The vendor (RCCL) communicator created beside this one when MSCCLPP_AMD_NCCL_LIB_PATH is set, or
+ * NULL (no vendor library, or it refused the communicator). */
+int mscclppAmdCommVendorComm(ncclComm_t comm, void** vendorComm);
 int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear);
 int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes);
 int mscclppAmdCommFlags(ncclComm_t comm, uint32_t** flags);

@@ -291,6 +291,12 @@ ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle) {
   return ncclSuccess;
 }
 
+int mscclppAmdCommVendorComm(ncclComm_t comm, void** vendorComm) {
+  if (!comm || !vendorComm) return ncclInvalidArgument;
+  *vendorComm = comm->fallback;
+  return ncclSuccess;
+}
+
 // Broadcast for in-process ranks (parity tests): views as for mscclppAmdAllReduceLaunch; input =
 // the rank's send buffer (read on the root only), output = its receive buffer, peerInput[root] =
 // the root's send buffer.

@@ -1,0 +1,55 @@
+"""Vendor fallback (the reference's MSCCLPP_NCCL_LIB_PATH, nccl.cc:83-124, :323-346): with
+MSCCLPP_AMD_NCCL_LIB_PATH naming librccl, ncclCommInitRank also creates an RCCL communicator beside
+its own and ncclCommDestroy releases it.  One rank (RCCL refuses several ranks on one GPU); the
+forwarding of multi-rank operations needs one GPU per rank and is not exercised on this box."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+PROG = r"""
+import ctypes, sys, torch
+sys.path.insert(0, sys.argv[1])
+import mscclpp_amd as m
+torch.cuda.set_device(0)
+L = m.lib()
+L.mscclppAmdCommVendorComm.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+c = m.Communicator(0, 1, m.Communicator.unique_id())
+v = ctypes.c_void_p()
+assert L.mscclppAmdCommVendorComm(c.comm, ctypes.byref(v)) == 0
+x = torch.arange(1000, dtype=torch.float64, device="cuda")
+y = torch.zeros_like(x)
+L.ncclReduce.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_void_p, ctypes.c_void_p]
+assert L.ncclReduce(x.data_ptr(), y.data_ptr(), 1000, 8, 0, 0, c.comm, m.stream_ptr()) == 0
+torch.cuda.synchronize()
+assert torch.equal(x, y)
+c.destroy()
+print("VENDOR", bool(v.value))
+"""
+
+
+def _librccl():
+    for p in ("/opt/rocm/lib/librccl.so.1", "/opt/rocm/lib/librccl.so"):
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def test_vendor_comm_created_and_released(built):
+    lib = _librccl()
+    if lib is None:
+        pytest.skip("no librccl on this box")
+    env = dict(os.environ, MSCCLPP_AMD_NCCL_LIB_PATH=lib)
+    r = subprocess.run([sys.executable, "-c", PROG, ROOT], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "VENDOR True" in r.stdout, r.stdout[-3000:]
+    env.pop("MSCCLPP_AMD_NCCL_LIB_PATH")
+    r = subprocess.run([sys.executable, "-c", PROG, ROOT], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "VENDOR False" in r.stdout, r.stdout[-3000:]
