@@ -221,6 +221,12 @@ def _time_calls(fn, reps):
     return (time.perf_counter() - t0) / reps
 
 
+def progress(msg):
+    """Stage markers on stderr (rank 0): a long multi-GPU run keeps writing, and a stall names its stage."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def bench_multi(args):
     import torch.distributed as dist
 
@@ -255,12 +261,15 @@ def bench_multi(args):
     sel = {1: "packet", 2: "allpair", 3: "fullmesh", 4: "rsag", 5: "rsag_zc"}[m.lib().mscclppAmdSelectAlgo(n, S, 0)]
     algos = [args.algo] if args.algo else ([sel, "rsag_zc"] if sel == "fullmesh" else [sel])
     cands = []
+    shared = ndev < world  # rehearsal: ranks share a device, so every rank's grid must fit on it at once
     for a in algos:
         if a in ("fullmesh", "rsag", "rsag_zc"):
-            cands += [(a, nb_, nt_) for nb_, nt_ in ((64, 512), (128, 512), (256, 512), (128, 256), (256, 256))]
+            cands += [(a, nb_, nt_) for nb_, nt_ in ((64, 512), (128, 512), (256, 512), (128, 256), (256, 256))
+                      if not shared or nb_ * world <= 256]
         else:
             cands.append((a, 0, 0))
     tune = {}
+    progress(f"tuning {len(cands)} candidates")
     for a, nb, nt in cands:
         try:
             for _ in range(2):
@@ -270,11 +279,14 @@ def bench_multi(args):
             tune[(a, nb, nt)] = float("inf")
             if rank == 0:
                 print(f"tune {a} {nb}x{nt}: {e}", file=sys.stderr)
+    if tmax(float(comm.device_error())) != 0:  # a spin timed out somewhere: say so instead of hanging on
+        print("bench: device error after tuning; results below are suspect", file=sys.stderr)
     algo, nb, nt = min(tune, key=tune.get)
 
     def step():
         comm.all_reduce(x, out, algo=algo, nblocks=nb, nthreads=nt)
 
+    progress(f"selected {algo} {nb}x{nt}; warmup + timed region")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -332,6 +344,13 @@ def bench_multi(args):
     }
     res["roofline"]["frac"] = round(res["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
     if not args.no_extras:
+        progress("xGMI probe")
+        try:
+            probe = xgmi_probe(comm, n, dev, tmax, dist.barrier)
+            res["xgmi"]["measured"] = probe
+            res["xgmi"]["frac_of_measured_ceiling"] = round(algbw / probe["allpairs_algbw_ceiling_measured"], 4)
+        except Exception as e:  # recorded, never fatal for the headline line
+            res["xgmi"]["measured_error"] = str(e)[-300:]
         res["extras"] = bench_extras(args, comm, n, dev, tmax, dist.barrier)
     # cpu_baseline is an N=1 field (the oracle timed on rank 0 at N=1 only); at N>1 the reference's
     # host-proxy path is reported by the mscclpp-test k1 row in extras
@@ -339,6 +358,59 @@ def bench_multi(args):
     dist.barrier()
     dist.destroy_process_group()
     return res if rank == 0 else None
+
+
+def xgmi_probe(comm, n, dev, tmax, barrier, S=64 << 20):
+    """Raw xGMI ceilings measured on the node (calibrate B_link with a raw put
+    microbenchmark): the streaming copy kernel (mscclppAmdCopy, 16-byte loads/stores over all CUs)
+    with one side in IPC-mapped peer memory.  ring_put: every rank writes S into the next rank (each
+    link carries one direction); ring_get: every rank reads S from the previous rank; allpairs_put:
+    every rank writes S/(n-1) into each peer at once (one stream per peer).  Max over ranks."""
+    import mscclpp_amd as m
+
+    L = m.lib()
+    rank = comm.rank
+    src = torch.full((S,), rank & 0xFF, dtype=torch.uint8, device=dev)
+    dst = torch.empty(S, dtype=torch.uint8, device=dev)
+    pdst = comm.register_buffer(dst)
+    psrc = comm.register_buffer(src)
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    vp = ctypes.c_void_p
+
+    def timed(fn, reps=5):
+        fn()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return tmax((time.perf_counter() - t0) / reps)
+
+    sp = m.stream_ptr()
+    t_put = timed(lambda: L.mscclppAmdCopy(vp(src.data_ptr()), vp(pdst[nxt]), S, 1024, sp))
+    t_get = timed(lambda: L.mscclppAmdCopy(vp(psrc[prv]), vp(dst.data_ptr()), S, 1024, sp))
+    chunk = (S // (n - 1)) // 16 * 16
+    peers = [q for q in range(n) if q != rank]
+    streams = [torch.cuda.Stream(device=dev) for _ in peers]
+    nb = max(64, 1024 // (n - 1))
+
+    def allpairs():
+        for st in streams:
+            st.wait_stream(torch.cuda.current_stream())
+        for i, q in enumerate(peers):
+            slot = (rank - q - 1) % n  # distinct destination region per source
+            L.mscclppAmdCopy(vp(src.data_ptr() + i * chunk), vp(pdst[q] + slot * chunk), chunk, nb, m.stream_ptr(streams[i]))
+        for st in streams:
+            torch.cuda.current_stream().wait_stream(st)
+
+    t_ap = timed(allpairs)
+    barrier()
+    out = {"bytes": S, "ring_put_GBs": round(S / t_put / 1e9, 1), "ring_get_GBs": round(S / t_get / 1e9, 1),
+           "allpairs_put_out_GBs": round((n - 1) * chunk / t_ap / 1e9, 1)}
+    # all-pairs AllReduce moves 2(n-1)/n * S out of every rank: its algbw ceiling at the measured rate
+    out["allpairs_algbw_ceiling_measured"] = round(out["allpairs_put_out_GBs"] * n / (2 * (n - 1)), 1)
+    return out
 
 
 def graph_time_per_call(fn, calls=20, replays=10, sync=None):
@@ -367,6 +439,7 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
     """BASELINE configs[3] (LL latency sweep, fp16 1 KiB..1 MiB) and configs[4] (fp32 1 GiB
     RS+AG in ring order), timed the same way; failures are recorded, not raised."""
     extras = {}
+    progress("extras: LL latency sweep")
     try:
         lat = {}
         for kb in (1, 4, 16, 64, 256, 1024):
@@ -395,6 +468,7 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         extras["ll_latency_graph_us"] = glat
     except Exception as e:
         extras["ll_latency_error"] = str(e)
+    progress("extras: fp32 1 GiB rsag")
     try:
         S = 1 << 30
         xs = torch.rand(S // 4, device=dev)
@@ -407,6 +481,7 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         del xs, os_
     except Exception as e:
         extras["fp32_1GiB_rsag_error"] = str(e)
+    progress("extras: mscclpp-test kernels")
     try:
         # the mscclpp-test kernels on the sizes the reference publishes (BASELINE.md §1,
         # test/deploy/perf_ndmv4.jsonl / perf_ndmv5.jsonl), timed like common.cc:202-227
@@ -430,6 +505,7 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         # allreduce1: the int32 ring whose bytes move through PortChannels and the host proxy
         # (perf_ndmv4.jsonl:4: 1 GiB, 7701.98 us, 139.41 GB/s on 8 x A100)
         barrier()
+        comm.deregister_all()
         us, ok, _ = comm.proxy_ring_all_reduce((1 << 30) // 4, iters=3, graph_launches=2)
         us = tmax(us)
         mt["k1_1GiB"] = {"us": round(us, 1), "algbw_GBs": round((1 << 30) / us / 1e3, 2), "correct": ok,

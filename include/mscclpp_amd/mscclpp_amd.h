@@ -131,6 +131,13 @@ int mscclppAmdCommBarrier(ncclComm_t comm);
 /* The vendor (RCCL) communicator created beside this one when MSCCLPP_AMD_NCCL_LIB_PATH is set, or
  * NULL (no vendor library, or it refused the communicator). */
 int mscclppAmdCommVendorComm(ncclComm_t comm, void** vendorComm);
+/* Collective: every rank passes its matching device buffer; peers[r] receives rank r's buffer as
+ * mapped in this process (peers[rank] = ptr), MSCCLPP_AMD_MAX_RANKS entries (Communicator::
+ * registerMemory of algorithm.hpp; registerMemory + sendMemory/recvMemory in the reference). */
+int mscclppAmdCommRegisterBuffer(ncclComm_t comm, void* ptr, void** peers);
+/* Collective: close every cached mapping of peers' user buffers (scratch / semaphores stay); call it
+ * when buffers that were used with the communicator are freed. */
+int mscclppAmdCommDeregisterAll(ncclComm_t comm);
 int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear);
 int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes);
 int mscclppAmdCommFlags(ncclComm_t comm, uint32_t** flags);

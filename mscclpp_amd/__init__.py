@@ -102,6 +102,9 @@ def lib():
         "ncclReduceScatter": [vp, vp, sz, i32, i32, vp, vp],
         "ncclAllGather": [vp, vp, sz, i32, vp, vp],
         "ncclBroadcast": [vp, vp, sz, i32, i32, vp, vp],
+        "mscclppAmdCommRegisterBuffer": [vp, vp, ctypes.POINTER(vp)],
+        "mscclppAmdCommDeregisterAll": [vp],
+        "mscclppAmdCopy": [vp, vp, sz, i32, vp],
         "ncclCommSplit": [vp, i32, i32, ctypes.POINTER(vp), vp],
         "mscclppAmdBroadcastLaunch": [ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, u64, vp],
         "ncclGetUniqueId": [ctypes.POINTER(UniqueId)],
@@ -366,6 +369,16 @@ class Communicator:
         check(lib().ncclBroadcast(ctypes.c_void_p(send.data_ptr()), ctypes.c_void_p(recv.data_ptr()), recv.numel(),
                                   NCCL_DTYPES[recv.dtype], root, self.comm, stream_ptr(stream)), "ncclBroadcast")
         return recv
+
+    def register_buffer(self, t):
+        """Collective: every rank's matching buffer as mapped here (list of nranks device pointers)."""
+        arr = (ctypes.c_void_p * MAX_RANKS)()
+        check(lib().mscclppAmdCommRegisterBuffer(self.comm, ctypes.c_void_p(t.data_ptr()), arr), "register_buffer")
+        return [arr[r] for r in range(self.nranks)]
+
+    def deregister_all(self):
+        """Collective: forget every cached peer-buffer mapping (call after freeing buffers used here)."""
+        check(lib().mscclppAmdCommDeregisterAll(self.comm), "deregister_all")
 
     def split(self, color, key):
         """ncclCommSplit(comm, color, key, &newcomm, NULL) -> Communicator, or None for NCCL_SPLIT_NOCOLOR."""

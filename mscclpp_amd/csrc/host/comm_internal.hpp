@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <cstdio>
 #include <cstdlib>
@@ -355,6 +356,32 @@ struct ncclComm {
       v.peerInput[root] = (char*)mapped + all[root].offset;
     }
     return launchBroadcast(&v, 1, nranks, bytes, root, nblocks, nthreads, spinBudgetTicks(), stream);
+  }
+
+  // Drop every cached mapping of peers' user buffers (collective).  Scratch, token and flag
+  // mappings stay.  After this, the next use of any buffer registers it afresh.
+  void dropUserRegistrations() {
+    HIPCHECK(hipDeviceSynchronize());
+    boot->barrier();  // no rank still runs a kernel that uses a mapping being closed
+    std::vector<void*> keep;
+    for (int r = 0; r < nranks; ++r) {
+      keep.push_back(peerLL[r]);
+      keep.push_back(peerBulk[r]);
+      keep.push_back(peerTokens[r]);
+    }
+    for (auto it = opened.begin(); it != opened.end();) {
+      if (std::find(keep.begin(), keep.end(), it->second.mapped) == keep.end()) {
+        (void)hipIpcCloseMemHandle(it->second.mapped);
+        it = opened.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    for (void* p : retired) (void)hipIpcCloseMemHandle(p);
+    retired.clear();
+    outRegs.clear();
+    outPtrs.clear();
+    boot->barrier();
   }
 
   mscclppAmdRankView baseView(const void* in, void* out) {

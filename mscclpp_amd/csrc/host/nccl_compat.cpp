@@ -297,6 +297,24 @@ int mscclppAmdCommVendorComm(ncclComm_t comm, void** vendorComm) {
   return ncclSuccess;
 }
 
+int mscclppAmdCommRegisterBuffer(ncclComm_t comm, void* ptr, void** peers) {
+  return guarded([&] {
+    if (!comm || !ptr || !peers) return (int)ncclInvalidArgument;
+    auto v = comm->cxx->registerMemory(ptr);
+    for (int r = 0; r < MSCCLPP_AMD_MAX_RANKS; ++r) peers[r] = r < (int)v.size() ? v[(size_t)r] : nullptr;
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdCommDeregisterAll(ncclComm_t comm) {
+  return guarded([&] {
+    if (!comm) return (int)ncclInvalidArgument;
+    std::lock_guard<std::mutex> lk(comm->mu);
+    comm->dropUserRegistrations();
+    return (int)ncclSuccess;
+  });
+}
+
 // Broadcast for in-process ranks (parity tests): views as for mscclppAmdAllReduceLaunch; input =
 // the rank's send buffer (read on the root only), output = its receive buffer, peerInput[root] =
 // the root's send buffer.

@@ -196,6 +196,22 @@ static void spinSync(hipStream_t s) {
   }
 }
 
+extern "C" int mscclppAmdProxyCopy(void* dst, const void* src, size_t bytes, void* stream);
+
+// A data trigger's copy (CudaIpcConnection::write, connection.cc:138-157): hipMemcpyAsync on the
+// connection stream, as the reference does.  MSCCLPP_AMD_PROXY_COPY=kernel enqueues the CU copy
+// kernel (proxy_kernels.hip) instead, a diagnostic that separates the copy engine from the
+// mappings; not the default, because a copy kernel queued behind a spinning
+// collective on a shared hardware queue could never run.
+static hipError_t proxyCopy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  static const bool kernel = [] {
+    const char* e = std::getenv("MSCCLPP_AMD_PROXY_COPY");
+    return e && std::string(e) == "kernel";
+  }();
+  if (!kernel) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s);
+  return mscclppAmdProxyCopy(dst, src, bytes, (void*)s) == 0 ? hipSuccess : hipErrorLaunchFailure;
+}
+
 // Per-peer host-driven connection: a non-blocking stream (CudaIpcStream, context.cc:16-46).
 struct Conn {
   hipStream_t stream = nullptr;
@@ -402,10 +418,12 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
     Proxy proxy(comm->device, 512, [&](const ProxyTrigger& t, uint64_t pos) {
       const int q = (int)t.fields.semaphoreId;
       if (q < 0 || q >= n || q == rank) return false;
-      if (t.fields.type & kTriggerData)
-        (void)hipMemcpyAsync((char*)mem[t.fields.dstMemoryId] + t.fields.dstOffset,
-                             (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
-                             hipMemcpyDeviceToDevice, conns[q].stream);
+      if (t.fields.type & kTriggerData) {
+        const hipError_t e = proxyCopy((char*)mem[t.fields.dstMemoryId] + t.fields.dstOffset,
+                                       (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
+                                       conns[q].stream);
+        if (e != hipSuccess) warn("proxy copy failed: " + std::string(hipGetErrorString(e)));
+      }
       if (t.fields.type & kTriggerFlag) {
         // remote token slot of peer q for source `rank`
         writers[q]->signal((uint64_t*)peerTok[q] + rank, conns[q].stream);
@@ -519,6 +537,15 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     int* scratch = (int*)allocUncached(bytes);
     auto peerBuff = comm->exchange(buff);
     auto peerScratch = comm->exchange(scratch);
+    if (logLevel() >= 2) {
+      for (void* p : {peerBuff[next], peerScratch[next]}) {
+        void* b = nullptr;
+        size_t sz = 0;
+        const hipError_t e = hipMemGetAddressRange((hipDeviceptr_t*)&b, &sz, (hipDeviceptr_t)p);
+        info("ring: peer mapping " + std::to_string((uint64_t)p) + " -> range base " + std::to_string((uint64_t)b) +
+             " size " + std::to_string(sz) + " (" + hipGetErrorString(e) + ")");
+      }
+    }
     // tokens[round][source rank], written by the sources' proxies
     uint64_t* tok = (uint64_t*)allocUncached(2 * n * 8);
     uint64_t* expct = nullptr;
@@ -543,10 +570,15 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     Proxy proxy(comm->device, 512, [&](const ProxyTrigger& t, uint64_t pos) {  // ProxyService::handleTrigger
       const int round = (int)t.fields.semaphoreId;
       if (round < 0 || round > 1) return false;
-      if (t.fields.type & kTriggerData)
-        (void)hipMemcpyAsync((char*)mem[t.fields.dstMemoryId] + t.fields.dstOffset,
-                             (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
-                             hipMemcpyDeviceToDevice, conn.stream);
+      if (t.fields.type & kTriggerData) {
+        const hipError_t e = proxyCopy((char*)mem[t.fields.dstMemoryId] + t.fields.dstOffset,
+                                       (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
+                                       conn.stream);
+        if (e != hipSuccess)
+          warn("proxy copy failed: " + std::string(hipGetErrorString(e)) + " dst id " +
+               std::to_string(t.fields.dstMemoryId) + " off " + std::to_string(t.fields.dstOffset) + " size " +
+               std::to_string(t.fields.size));
+      }
       if (t.fields.type & kTriggerFlag) {
         writers[round].signal((uint64_t*)peerTok[next] + round * n + rank, conn.stream);
       }
@@ -597,6 +629,17 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     if (!ok) {
       uint32_t e0 = 0;
       (void)hipMemcpy(&e0, err, 4, hipMemcpyDeviceToHost);
+      // where did the peer's contribution go?  my scratch at the first bad element, my tokens
+      int sc = -1;
+      (void)hipMemcpy(&sc, scratch + firstBad, 4, hipMemcpyDeviceToHost);
+      std::vector<uint64_t> tk(2 * (size_t)n);
+      (void)hipMemcpy(tk.data(), tok, tk.size() * 8, hipMemcpyDeviceToHost);
+      std::string ts;
+      for (auto t : tk) ts += std::to_string(t) + " ";
+      warn("proxy ring allreduce rank " + std::to_string(rank) + ": scratch at first bad = " + std::to_string(sc) +
+           ", tokens [round][src] = " + ts + ", buff " + std::to_string((uint64_t)buff) + " scratch " +
+           std::to_string((uint64_t)scratch) + " peerScratch[next] " + std::to_string((uint64_t)peerScratch[next]) +
+           " peerBuff[next] " + std::to_string((uint64_t)peerBuff[next]));
       warn("proxy ring allreduce rank " + std::to_string(rank) + ": " + std::to_string(nbad) + " wrong of " +
            std::to_string(nelems) + ", first at " + std::to_string(firstBad) + " = " +
            std::to_string(back[firstBad]) + ", device error " + std::to_string(e0));

@@ -209,6 +209,39 @@ extern "C" int mscclppAmdLaunchHostOffloadKernel(int rank, int nranks, const voi
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// The host proxy's data mover (CudaIpcConnection::write, connection.cc:138-157, moves bytes with
+// cudaMemcpyAsync): a CU copy kernel the proxy thread enqueues on the connection stream.  16-byte
+// non-temporal loads, system-scope write-through stores (the destination is usually a peer's
+// IPC-mapped memory), a byte loop when the ends are not 16-byte aligned.  Stream order keeps the
+// token update enqueued after it behind the data.
+__global__ void __launch_bounds__(512) proxyCopyKernel(uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const bool aligned = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0;
+  const uint64_t body = aligned ? bytes / 16 * 16 : 0;
+  if (aligned) {
+    const uint64_t nUnits = body / 16;
+    for (uint64_t u = tid; u < nUnits; u += stride) {
+      // 4 GiB buffer windows: rebase the resource every 2^28 units
+      const uint64_t base = (u >> 28) << 32;
+      const uint32_t off = (uint32_t)((u & ((1ull << 28) - 1)) * 16);
+      store16<kSystem>(make_rsrc(dst + base), off, load16<kNonTemporal>(make_rsrc(src + base), off));
+    }
+  }
+  for (uint64_t i = body + tid; i < bytes; i += stride) dst[i] = src[i];
+}
+
+extern "C" int mscclppAmdProxyCopy(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!dst || !src) return 4;
+  if (bytes == 0) return 0;
+  const uint64_t units = (bytes + 15) / 16;
+  uint64_t nb = (units + 511) / 512;
+  if (nb > 1024) nb = 1024;
+  hipLaunchKernelGGL(proxyCopyKernel, dim3((uint32_t)nb), dim3(512), 0, (hipStream_t)stream, (uint8_t*)dst,
+                     (const uint8_t*)src, (uint64_t)bytes);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 extern "C" int mscclppAmdLaunchPortChannelPut(void* chans, int nchans, const uint64_t* dstOffs, const uint64_t* srcOffs,
                                               uint64_t chunk, int mode, void* stream) {
   if (!chans || !dstOffs || !srcOffs || nchans <= 0 || nchans > 1024) return 4;
