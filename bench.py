@@ -239,7 +239,12 @@ def bench_multi(args):
     if ndev < world:  # rehearsal on a smaller box: ranks share devices (never the case on the 8-GPU node)
         local = local % ndev
     torch.cuda.set_device(local)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a rank that stalls must turn into an error (caught per extras section) well before the driver's
+    # limit, so the JSON line is still printed: bounded bootstrap and gloo timeouts
+    os.environ.setdefault("MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S", "180")
+    import datetime
+
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=300))
     comm = m.Communicator.from_torch_dist()
     n = world
     S = args.bytes
