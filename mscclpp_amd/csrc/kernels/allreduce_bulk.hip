@@ -76,6 +76,12 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
   uint8_t* scr = (uint8_t*)v.scratch;
   constexpr int U = 8;  // units per lane per step (128 B in flight per lane in the put phase)
 
+  // AllGather writes straight into the peers' outputs: first make sure every peer's kernel is
+  // running, i.e. all earlier work on the peer's stream (which may still write that memory, e.g. a
+  // framework's freed-and-reused allocation) is done.  AllReduce / ReduceScatter reach the peers'
+  // outputs only after their reduce-scatter handshake, which already orders this.
+  if constexpr (MODE == 2) block_handshake(v, nranks, rank, b, budget);
+
   for (uint32_t ps = 0; ps < g.npasses; ++ps) {
     const uint64_t pOff = (uint64_t)ps * g.pass;          // offset inside a slice
     const uint64_t bOff = pOff + (uint64_t)b * g.blk;     // this block's sub-range start in a slice

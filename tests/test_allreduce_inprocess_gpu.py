@@ -191,3 +191,31 @@ def test_reduce_scatter_and_all_gather(built, n, dt, block):
         assert ranks.errors() == [0] * n, ("all-gather", call, ranks.error_details())
         for r in range(n):
             _cmp(_bytes(gathered[r]), exp.view(np.uint8)[: count * item], dt)
+
+
+@pytest.mark.parametrize("algo", ["packet", "allpair", "fullmesh", "rsag_zc"])
+@pytest.mark.parametrize("dt,count", [(O.I32, 1), (O.F16, 1), (O.F16, 3), (O.F32, 1), (O.BF16, 2), (O.I32, 5)])
+@pytest.mark.parametrize("op", [O.SUM, O.MIN])
+def test_tiny_buffers(built, algo, dt, count, op):
+    """1-5 element buffers (a framework's 4-byte flag all_reduce): every path, SUM and MIN."""
+    import mscclpp_amd as m
+
+    n = 2
+    code = m.ALGO_NAMES[algo]
+    nbytes = count * ITEM[dt]
+    ranks = m.InProcessRanks(n, max(m.scratch_required(code, n, nbytes, dt), 1 << 16), bulk_scratch_bytes=1 << 20)
+    for call in range(2):
+        ins = _inputs(dt, n, count, seq=call)
+        dins = [_dev(a, dt) for a in ins]
+        douts = [torch.full_like(d, 0) for d in dins]
+        try:
+            ranks.all_reduce(dins, douts, code, op=op, nblocks=2 if code in (m.ALGO_PACKET, m.ALGO_ALLPAIR) else 2,
+                             nthreads=256)
+        except RuntimeError as e:  # a path may refuse a size it cannot carry; it must not compute garbage
+            pytest.skip(f"{algo} refuses {nbytes} bytes: {e}")
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        exp = O.reduce_seq(dt, op, [np.concatenate([a.view(np.uint8), np.zeros(4, np.uint8)])[: (nbytes + 3) // 4 * 4]
+                                    for a in ins])
+        for r in range(n):
+            _cmp(_bytes(douts[r]), exp.view(np.uint8)[:nbytes], dt)

@@ -254,3 +254,68 @@ def test_broadcast_and_split_two_processes(built):
                 p.kill()
     for rank in range(n):
         assert got[rank] == [True, True, True, True, True, True, 0], (rank, got[rank])
+
+
+def _stream_order_worker(rank, n, uid, q):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "10000")
+        import torch
+
+        import mscclpp_amd as m
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        res = []
+        blk = 1 << 18
+        inp = torch.full((blk,), float(rank + 1), device="cuda")
+        out = torch.empty(n * blk, device="cuda")
+        exp = torch.cat([torch.full((blk,), float(r + 1), device="cuda") for r in range(n)])
+        ar_in = torch.full((1 << 20,), float(rank + 1), dtype=torch.float16, device="cuda")
+        ar_out = torch.empty_like(ar_in)
+        for _ in range(3):
+            # the receive buffers are still being written by this rank's own stream (a slow producer)
+            # when the collective is enqueued behind it: peers must not write into them earlier
+            torch.cuda._sleep(20_000_000)
+            out.fill_(-1.0)
+            comm.all_gather(inp, out)
+            torch.cuda._sleep(20_000_000)
+            ar_out.fill_(-1.0)
+            comm.all_reduce(ar_in, ar_out, algo="rsag_zc")
+            torch.cuda._sleep(20_000_000)
+            ar_out.fill_(-1.0)
+            comm.all_reduce(ar_in, ar_out, algo="fullmesh")
+            torch.cuda.synchronize()
+            res.append(bool(torch.equal(out, exp)) and bool(torch.all(ar_out == n * (n + 1) / 2)))
+        res.append(comm.device_error())
+        comm.destroy()
+        q.put((rank, res, None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_collectives_wait_for_the_peers_stream(built):
+    """Remote writes into a peer's receive buffer start only after the peer's earlier stream work
+    (which may still write that memory) is done: AllGather's entry handshake, and the handshakes that
+    precede the output writes of the zero-copy and fullmesh AllReduce."""
+    import mscclpp_amd as m
+
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    uid = m.Communicator.unique_id()
+    procs = [ctx.Process(target=_stream_order_worker, args=(r, n, uid, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=200)
+            assert err is None, err
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        assert got[rank] == [True, True, True, 0], (rank, got[rank])

@@ -72,9 +72,13 @@ def main():
     torch.cuda.synchronize()
     results["checks"] = checks
     results["ok"] = all(c["ok"] for c in checks)
+    for c in checks:
+        if not c["ok"]:
+            print(f"rank {rank} FAILED {c}", file=sys.stderr, flush=True)
     flags = torch.tensor([1 if results["ok"] else 0], dtype=torch.int32, device=dev)
-    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)  # a 4-byte int32 MIN through the library as well
     results["all_ranks_ok"] = bool(flags.item() == 1)
+    print(f"rank {rank} ok={results['ok']} min-reduced flag={flags.item()}", file=sys.stderr, flush=True)
     dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(results), flush=True)
