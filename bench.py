@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--bytes", type=int, default=48 << 20)
     p.add_argument("--algo", default=None,
-                   help="force an AllReduce algorithm (N>1): packet|allpair|fullmesh|rsag|rsag_zc")
+                   help="force an AllReduce algorithm (N>1): packet|allpair|fullmesh|rsag|rsag_zc|rsag_pipeline")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="N>1: skip the LL latency sweep and the fp32 1 GiB run")
@@ -264,13 +264,16 @@ def bench_multi(args):
     # zero-copy RS+AG (reads peers' inputs, writes peers' outputs) -- which one drives xGMI better
     # is measured here, on the node, not assumed.
     sel = {1: "packet", 2: "allpair", 3: "fullmesh", 4: "rsag", 5: "rsag_zc"}[m.lib().mscclppAmdSelectAlgo(n, S, 0)]
-    algos = [args.algo] if args.algo else ([sel, "rsag_zc"] if sel == "fullmesh" else [sel])
+    algos = [args.algo] if args.algo else ([sel, "rsag_zc", "rsag_pipeline"] if sel == "fullmesh" else [sel])
     cands = []
     shared = ndev < world  # rehearsal: ranks share a device, so every rank's grid must fit on it at once
     for a in algos:
         if a in ("fullmesh", "rsag", "rsag_zc"):
             cands += [(a, nb_, nt_) for nb_, nt_ in ((64, 512), (128, 512), (256, 512), (128, 256), (256, 256))
                       if not shared or nb_ * world <= 256]
+        elif a == "rsag_pipeline":  # nblocks = reduce workgroups; the launch is 2x that
+            cands += [(a, nb_, nt_) for nb_, nt_ in ((32, 512), (64, 512), (16, 512), (64, 256))
+                      if not shared or 2 * nb_ * world <= 256]
         else:
             cands.append((a, 0, 0))
     tune = {}
@@ -322,7 +325,10 @@ def bench_multi(args):
     # writes S/n own output + (n-1)/n S incoming scratch + (n-1)/n S incoming output.  rsag_zc: reads
     # S of input (own slice locally, the rest by the peers), writes S of output (own slice locally,
     # the rest by the peers).  LL paths: priced like fullmesh (their packets double the bytes).
-    hbm = 2 * S if algo == "rsag_zc" else S * (1 + 3 * (n - 1) / n + 1 / n)
+    # rsag_pipeline: reads S input + 2(n-1)/n S scratch (RS and AG regions), writes S output +
+    # 2(n-1)/n S incoming scratch
+    hbm = (2 * S if algo == "rsag_zc" else 2 * S * (1 + 2 * (n - 1) / n) if algo == "rsag_pipeline"
+           else S * (1 + 3 * (n - 1) / n + 1 / n))
     res = {
         "metric": "device-resident AllReduce algbw GB/s fp16 at 1/2/4/8 MI355X; % xGMI roofline",
         "value": round(algbw, 2),
@@ -342,7 +348,7 @@ def bench_multi(args):
         "xgmi": {"allpairs_algbw_ceiling": round(ceiling, 1), "frac": round(algbw / ceiling, 4),
                  "link_GBs_assumed": XGMI_LINK_GBS, "wire_bytes_per_rank": int(2 * (n - 1) * S / n)},
         "roofline": {"bound": "hbm", "achieved": round(hbm / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "traffic": None, "kernel": "allreduceZeroCopyKernel" if algo == "rsag_zc" else f"allreduceBulkKernel ({algo})",
+                     "unit": "GB/s", "traffic": None, "kernel": {"rsag_zc": "allreduceZeroCopyKernel", "rsag_pipeline": "allreduceRsAgPipelineKernel"}.get(algo, f"allreduceBulkKernel ({algo})"),
                      "kernel_us": round(kern_ms * 1e3, 2), "algorithmic_bytes_per_launch": int(hbm)},
         "tune_ms": {f"{k[0]}:{k[1]}x{k[2]}": round(v * 1e3, 4) for k, v in tune.items()},
         "correct": ok,

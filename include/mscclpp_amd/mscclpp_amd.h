@@ -56,6 +56,8 @@ enum {
   MSCCLPP_AMD_ALGO_RSAG = 4,     /* default_allreduce_rsag: ring-order bulk RS+AG (allreduce_rsag.cu:33-128) */
   MSCCLPP_AMD_ALGO_RSAG_ZC = 5,  /* default_allreduce_rsag_zero_copy: reads peers' inputs, writes peers' outputs,
                                     no scratch (allreduce_rsag_zero_copy.cu:41-112) */
+  MSCCLPP_AMD_ALGO_RSAG_PIPELINE = 6, /* default_allreduce_rsag_pipeline: put / reduce / recv workgroups
+                                         pipelined over a circular scratch (allreduce_rsag_pipeline.cu:85-222) */
   /* the int32 kernels of the mscclpp-test harness (test/mscclpp-test/allreduce_test.cu), by number */
   MSCCLPP_AMD_ALGO_TEST_K5 = 105, /* allreduce5 (AMD branch): in-place RS by remote reads + ring AG by gets (:959-970) */
   MSCCLPP_AMD_ALGO_TEST_K6 = 106, /* allreduce6: LL16 two-hop, harness scratch layout (:972-1034) */
@@ -80,6 +82,8 @@ typedef struct {
   int32_t rank;
   int32_t pad;
   const void* peerInput[MSCCLPP_AMD_MAX_RANKS];    /* rank q's input as mapped here (zero-copy reads) */
+  uint64_t* pipeSems;                              /* rsag_pipeline: 3 x 256 intra-launch counters, zeroed
+                                                      before each launch (stream-ordered) */
 } mscclppAmdRankView;
 
 /* ---- memory ------------------------------------------------------------------------------- */

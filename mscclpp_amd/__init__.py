@@ -20,9 +20,9 @@ F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
 # OCP fp8 reduce types: element type x accumulation type (Algorithm::execute accumDtype)
 E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32 = 5, 6, 7, 8, 9, 10
 SUM, MIN = 0, 1
-ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC = 0, 1, 2, 3, 4, 5
+ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC, ALGO_RSAG_PIPELINE = 0, 1, 2, 3, 4, 5, 6
 ALGO_TEST_K5, ALGO_TEST_K6, ALGO_TEST_K7 = 105, 106, 107  # mscclpp-test allreduce5 / 6 / 7 (int32)
-ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4, "rsag_zc": 5,
+ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4, "rsag_zc": 5, "rsag_pipeline": 6,
               "k5": ALGO_TEST_K5, "k6": ALGO_TEST_K6, "k7": ALGO_TEST_K7}
 MAX_RANKS = 8
 FLAG_SLOTS = 4096
@@ -71,6 +71,7 @@ class RankView(ctypes.Structure):
         ("rank", ctypes.c_int32),
         ("pad", ctypes.c_int32),
         ("peerInput", ctypes.c_void_p * MAX_RANKS),
+        ("pipeSems", ctypes.c_void_p),
     ]
 
 
@@ -224,6 +225,7 @@ class InProcessRanks:
         self.expected = [torch.zeros(tok_elems, dtype=torch.int64, device=dev) for _ in range(nranks)]
         self.flags = [torch.ones(FLAG_SLOTS, dtype=torch.int32, device=dev) for _ in range(nranks)]
         self.err = [torch.zeros(64, dtype=torch.int32, device=dev) for _ in range(nranks)]
+        self.pipe_sems = [torch.zeros(3 * 256, dtype=torch.int64, device=dev) for _ in range(nranks)]
 
     def views(self, inputs, outputs, bulk=False):
         arr = (RankView * self.n)()
@@ -245,6 +247,7 @@ class InProcessRanks:
             v.expected = self.expected[r].data_ptr()
             v.flags = self.flags[r].data_ptr()
             v.err = self.err[r].data_ptr()
+            v.pipeSems = self.pipe_sems[r].data_ptr()
             v.scratchBytes = sbytes
             v.rank = r
         return arr
@@ -253,7 +256,7 @@ class InProcessRanks:
                    accum=None):
         dt = reduce_code(inputs[0].dtype, accum)
         nbytes = inputs[0].numel() * inputs[0].element_size()
-        bulk = algo in (ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC, ALGO_TEST_K5)
+        bulk = algo in (ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC, ALGO_RSAG_PIPELINE, ALGO_TEST_K5)
         arr = self.views(inputs, outputs, bulk=bulk)
         code = lib().mscclppAmdAllReduceLaunch(algo, arr, self.n, self.n, nbytes, dt, op, nblocks, nthreads,
                                                budget_ticks, stream_ptr(stream))

@@ -280,6 +280,7 @@ const char* envAlgoName() {
   if (s == "fullmesh") return "default_allreduce_fullmesh";
   if (s == "rsag") return "default_allreduce_rsag";
   if (s == "rsag_zc" || s == "rsag_zero_copy") return "default_allreduce_rsag_zero_copy";
+  if (s == "rsag_pipeline") return "default_allreduce_rsag_pipeline";
   return nullptr;
 }
 
@@ -359,6 +360,7 @@ AlgorithmCollection AlgorithmCollectionBuilder::buildDefaultAlgorithms(ncclComm_
       {"default_allreduce_fullmesh", "allreduce", MSCCLPP_AMD_ALGO_FULLMESH, 0, 0, kAny},
       {"default_allreduce_rsag", "allreduce", MSCCLPP_AMD_ALGO_RSAG, 0, 0, kAny},
       {"default_allreduce_rsag_zero_copy", "allreduce", MSCCLPP_AMD_ALGO_RSAG_ZC, 0, 0, kAny},
+      {"default_allreduce_rsag_pipeline", "allreduce", MSCCLPP_AMD_ALGO_RSAG_PIPELINE, 0, 0, kAny},
       {"default_allgather_fullmesh2", "allgather", MSCCLPP_AMD_ALGO_FULLMESH, 2, 0, kAny},
       {"default_reducescatter_fullmesh", "reducescatter", MSCCLPP_AMD_ALGO_FULLMESH, 1, 0, kAny},
   };

@@ -60,6 +60,17 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
     const bool k5 = algo == MSCCLPP_AMD_ALGO_TEST_K5;
     const bool zc = algo == MSCCLPP_AMD_ALGO_RSAG_ZC || k5;  // no scratch: peers' user buffers directly
     const bool bulk = algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG || zc;
+    if (algo == MSCCLPP_AMD_ALGO_RSAG_PIPELINE) {
+      for (int i = 0; i < nviews; ++i) {
+        const mscclppAmdRankView& v = views[i];
+        if (!v.input || !v.output || !v.scratch || !v.pipeSems || !v.tokens || !v.expected || !v.err)
+          return (int)ncclInvalidArgument;
+        for (int q = 0; q < nranks; ++q)
+          if (!v.peerScratch[q] || !v.peerTokens[q]) return (int)ncclInvalidArgument;
+      }
+      return launchAllReducePipeline(views, nviews, nranks, bytes, dtype, op, nblocks, nthreads, budgetTicks,
+                                     (hipStream_t)stream);
+    }
     const bool ll = algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR ||
                     algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7;
     unsigned seen = 0;
@@ -115,6 +126,7 @@ size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype) 
   }
   if (algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7) return testLLScratchRequired(nranks, bytes);
   if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC || algo == MSCCLPP_AMD_ALGO_TEST_K5) return 0;  // peers' buffers read in place
+  if (algo == MSCCLPP_AMD_ALGO_RSAG_PIPELINE) return 2 * (size_t)nranks * 32 * 512 * 4 * 16;  // one stage, defaults
   return 0;
 }
 

@@ -28,6 +28,8 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
                          int dtype, int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
 int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,
                         int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s);
+int launchAllReducePipeline(const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype, int op,
+                            int nblocks, int nthreads, uint64_t budget, hipStream_t s);
 int launchBroadcast(const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int root, int nblocks,
                     int nthreads, uint64_t budget, hipStream_t s);
 size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype);
@@ -165,6 +167,7 @@ inline int envAlgo() {
   if (s == "fullmesh") return MSCCLPP_AMD_ALGO_FULLMESH;
   if (s == "rsag") return MSCCLPP_AMD_ALGO_RSAG;
   if (s == "rsag_zc" || s == "rsag_zero_copy") return MSCCLPP_AMD_ALGO_RSAG_ZC;
+  if (s == "rsag_pipeline") return MSCCLPP_AMD_ALGO_RSAG_PIPELINE;
   return MSCCLPP_AMD_ALGO_AUTO;
 }
 
@@ -192,6 +195,7 @@ struct ncclComm {
   // present when MSCCLPP_AMD_NCCL_LIB_PATH names librccl (nccl_compat.cpp)
   void* fallback = nullptr;
   hipStream_t errStream = nullptr;  // ncclCommGetAsyncError's reads
+  uint64_t* pipeSems = nullptr;      // rsag_pipeline's intra-launch counters (3 x 256)
   std::shared_ptr<mscclpp_amd::Executor> executor;
   void buildAlgorithms();
   int rank = 0, nranks = 1, device = 0;
@@ -437,6 +441,19 @@ struct ncclComm {
       for (int r = 0; r < nranks; ++r) v.peerOutput[r] = bufs[r];
       return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
     }
+    if (algo == MSCCLPP_AMD_ALGO_RSAG_PIPELINE) {
+      // every remote store lands in the bulk scratch: no user-buffer registration at all
+      const size_t stageCap = (size_t)1 << 30;
+      size_t need = 2 * bytes + 16 * (size_t)nranks * 64;
+      if (need > stageCap) need = stageCap;
+      ensure(bulkScratch, bulkBytes, peerBulk, need);
+      v.scratch = bulkScratch;
+      v.scratchBytes = bulkBytes;
+      for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
+      if (!pipeSems) HIPCHECK(hipMalloc((void**)&pipeSems, 3 * 256 * sizeof(uint64_t)));
+      v.pipeSems = pipeSems;
+      return launchAllReducePipeline(&v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
+    }
     if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC) {
       // zero-copy: peers' inputs and outputs are mapped once per buffer (the reference registers
       // both as remote memories, allreduce_rsag_zero_copy.cu:25-27); no scratch
@@ -501,6 +518,8 @@ struct ncclComm {
     if (flags) (void)hipFree(flags);
     if (err) (void)hipFree(err);
     if (errStream) (void)hipStreamDestroy(errStream);
+    if (pipeSems) (void)hipFree(pipeSems);
+    pipeSems = nullptr;
     errStream = nullptr;
     llScratch = bulkScratch = nullptr;
     tokens = expected = nullptr;

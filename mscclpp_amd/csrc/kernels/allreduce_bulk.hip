@@ -338,6 +338,158 @@ __global__ void __launch_bounds__(512) broadcastKernel(Views<NV> views, uint64_t
   block_handshake(v, nranks, rank, b, budget);
 }
 
+// Pipelined RS+AG (allreduceRsAgPipeline, allreduce_rsag_pipeline.cu:85-222).  Three roles run at
+// once in one launch: P = R/2 put workgroups, R reduce workgroups, V = R/2 recv workgroups.  One
+// iteration covers n slots of C = R * T * 4 units (16 B) each; slot q holds the units rank q owns.
+//   put p    : waits for a free scratch stage (credit from recv p, pipeline depth D), writes its
+//              share of every peer's slot into that peer's scratch RS region (remote 16-B stores),
+//              drains, releases reduce 2p and 2p+1.
+//   reduce b : waits for put b/2, handshakes with the peers' reduce b (their puts into my RS region
+//              are done), sums own + peers in ring order (own, r+1, ...; the reference's
+//              calVector(data, tmp), :160-166), stores the result locally and into every peer's AG
+//              region, drains, releases recv b/2.
+//   recv v   : waits for reduce 2v and 2v+1, handshakes with the peers' recv v (their reduced
+//              slots are in my AG region), copies them into the output, releases the credit.
+// Every remote store lands in communicator-owned scratch (nothing written into peers' user
+// buffers), and the iterations overlap.  Intra-launch counters live in v.pipeSems (zeroed,
+// stream-ordered, before each launch): [0, 256) recv->put credits, [256, 512) put->reduce,
+// [512, 768) reduce->recv.
+struct PipeGeom {
+  uint64_t bytes;   // buffer bytes
+  uint64_t C;       // units per slot and iteration
+  uint32_t nIters;  // iterations
+  uint32_t D;       // pipeline depth (stages in the scratch)
+  uint32_t R;       // reduce workgroups (P = V = R / 2)
+  uint32_t pad;
+};
+
+__device__ __forceinline__ void sem_release(uint64_t* c) {
+  drain_stores();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void sem_acquire(uint64_t* c, uint64_t target, uint64_t budget, uint32_t* err) {
+  if (threadIdx.x == 0) {
+    SpinGuard g(budget);
+    while (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (g.expired()) {
+        report_error(err, kErrSemaphoreTimeout);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+template <int DT, int OP, int NV>
+__global__ void __launch_bounds__(512) allreduceRsAgPipelineKernel(Views<NV> views, PipeGeom g, int nranks,
+                                                                   uint64_t budget) {
+  const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
+  const int rank = v.rank;
+  const uint32_t T = blockDim.x, tid = threadIdx.x, bid = blockIdx.x;
+  const uint32_t P = g.R / 2;
+  const uint64_t C = g.C, nC = (uint64_t)nranks * C;
+  uint64_t* credit = v.pipeSems;
+  uint64_t* toReduce = v.pipeSems + 256;
+  uint64_t* toRecv = v.pipeSems + 512;
+  const uint8_t* in = (const uint8_t*)v.input;
+  uint8_t* out = (uint8_t*)v.output;
+  uint8_t* scr = (uint8_t*)v.scratch;
+  // byte offset of (iteration, slot q) in the buffer, and of (stage, region, slot q) in the scratch
+  auto bufOff = [&](uint32_t it, int q) { return ((uint64_t)it * nC + (uint64_t)q * C) * 16; };
+  auto scrOff = [&](uint32_t it, int region, int q) {
+    return ((uint64_t)(it % g.D) * 2 * nC + (uint64_t)region * nC + (uint64_t)q * C) * 16;
+  };
+  if (bid < P) {  // ---- put
+    const uint32_t p = bid;
+    for (uint32_t it = 0; it < g.nIters; ++it) {
+      if (it >= g.D) sem_acquire(&credit[p], it - g.D + 1, budget, v.err);
+#pragma unroll 1
+      for (int k = 1; k < nranks; ++k) {
+        const int q = (rank + k) % nranks;  // (rank + peer + 1) % n (:112-113)
+        const uint64_t so = bufOff(it, q);
+        const auto rs = make_rsrc(in + so);
+        const auto rd = make_rsrc((uint8_t*)v.peerScratch[q] + scrOff(it, 0, rank));
+        u32x4 w[8];
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+          const uint32_t pos = p * T + tid + st * T * P;
+          const uint32_t vb = clamp_valid(g.bytes, so + (uint64_t)pos * 16, 16);
+          w[st] = vb >= 16 ? load16<kNonTemporal>(rs, pos * 16u) : vb ? load_tail(in + so + (uint64_t)pos * 16, vb) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+          const uint32_t pos = p * T + tid + st * T * P;
+          if (so + (uint64_t)pos * 16 < g.bytes) store16<kSystem>(rd, pos * 16u, w[st]);
+        }
+      }
+      sem_release(&toReduce[2 * p]);
+      if (tid == 0) __hip_atomic_fetch_add(&toReduce[2 * p + 1], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if (bid < P + g.R) {  // ---- reduce
+    const uint32_t b = bid - P, p = b / 2, sub = b % 2;
+    for (uint32_t it = 0; it < g.nIters; ++it) {
+      sem_acquire(&toReduce[b], it + 1, budget, v.err);
+      block_handshake(v, nranks, rank, b, budget);  // peers' puts into my RS region (these units) done
+      const uint64_t mo = bufOff(it, rank);
+      const auto rin = make_rsrc(in + mo);
+      const auto rout = make_rsrc(out + mo);
+      const auto rrs = make_rsrc(scr + scrOff(it, 0, 0));
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const uint32_t pos = p * T + tid + (sub * 4 + st) * T * P;
+        const uint32_t vb = clamp_valid(g.bytes, mo + (uint64_t)pos * 16, 16);
+        if (vb == 0) continue;
+        u32x4 acc = load_payload<kNonTemporal>(rin, in + mo, (uint64_t)pos * 16, vb);
+#pragma unroll
+        for (int k = 1; k < kMaxRanks; ++k) {
+          if (k < nranks) {
+            const int q = (rank + k) % nranks;
+            const u32x4 d = load16<kSystem>(rrs, (uint32_t)((uint64_t)q * C * 16) + pos * 16u);
+            acc = reduce4<DT, OP>(d, acc);  // calVector<T, OpType>(data, tmp)
+          }
+        }
+        store_payload<kPlain>(rout, out + mo, (uint64_t)pos * 16, acc, vb);
+#pragma unroll 1
+        for (int k = 1; k < nranks; ++k) {
+          const int q = (rank + k) % nranks;
+          store16<kSystem>(make_rsrc((uint8_t*)v.peerScratch[q] + scrOff(it, 1, rank)), pos * 16u, acc);
+        }
+      }
+      sem_release(&toRecv[b]);
+    }
+  } else {  // ---- recv
+    const uint32_t r = bid - P - g.R;
+    for (uint32_t it = 0; it < g.nIters; ++it) {
+      sem_acquire(&toRecv[2 * r], it + 1, budget, v.err);
+      sem_acquire(&toRecv[2 * r + 1], it + 1, budget, v.err);
+      block_handshake(v, nranks, rank, g.R + r, budget);  // peers' reduced slots are in my AG region
+#pragma unroll 1
+      for (int k = 1; k < nranks; ++k) {
+        const int q = (rank + k) % nranks;
+        const uint64_t oo = bufOff(it, q);
+        const auto rag = make_rsrc(scr + scrOff(it, 1, q));
+        const auto rout = make_rsrc(out + oo);
+        u32x4 w[8];
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+          const uint32_t pos = r * T + tid + st * T * P;
+          if (oo + (uint64_t)pos * 16 < g.bytes) w[st] = load16<kSystem>(rag, pos * 16u);
+        }
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+          const uint32_t pos = r * T + tid + st * T * P;
+          const uint32_t vb = clamp_valid(g.bytes, oo + (uint64_t)pos * 16, 16);
+          if (vb) store_payload<kPlain>(rout, out + oo, (uint64_t)pos * 16, w[st], vb);
+        }
+      }
+      sem_release(&credit[r]);
+    }
+  }
+}
+
 static thread_local int g_launch_status = 0;
 
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks) {
@@ -522,6 +674,72 @@ int launchBroadcast(const mscclppAmdRankView* views, int nviews, int nranks, siz
   Views<kMaxRanks> vw{};
   for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
   return go(broadcastKernel<kMaxRanks, 4>, vw);
+}
+
+template <int DT, int OP>
+static void launchPipeline(const mscclppAmdRankView* views, int nviews, const PipeGeom& g, int nranks, int nthreads,
+                           uint64_t budget, hipStream_t s) {
+  auto go = [&](auto kern, auto vw) {
+    const long blocks = (long)(g.R + g.R) * nviews;
+    if (!grid_coresident(kern, nthreads, blocks)) {
+      g_launch_status = 5;  // the roles wait on each other inside the launch: all must be resident
+      return;
+    }
+    hipLaunchKernelGGL(kern, dim3(g.R + g.R, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
+  };
+  if (nviews == 1) {
+    Views<1> vw;
+    vw.v[0] = views[0];
+    go(allreduceRsAgPipelineKernel<DT, OP, 1>, vw);
+  } else {
+    Views<kMaxRanks> vw{};
+    for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
+    go(allreduceRsAgPipelineKernel<DT, OP, kMaxRanks>, vw);
+  }
+}
+
+// R reduce workgroups (nblocks, even, 2..128; default 32) of nthreads (default 512) lanes; the
+// scratch must hold at least one stage (2 * n * C units).
+int launchAllReducePipeline(const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype, int op,
+                            int nblocks, int nthreads, uint64_t budget, hipStream_t s) {
+  if (nblocks <= 0) nblocks = 32;
+  if (nthreads <= 0) nthreads = 512;
+  if (nblocks % 2 || nblocks < 2 || nblocks > 128 || nthreads > 512 || nthreads % 64 || nthreads < 64) return 4;
+  if (dtype != kF16 && dtype != kBF16 && dtype != kF32 && dtype != kI32 && dtype != kU32) return 4;
+  PipeGeom g{};
+  g.bytes = bytes;
+  g.R = (uint32_t)nblocks;
+  g.C = (uint64_t)nblocks * nthreads * 4;
+  const uint64_t units = (bytes + 15) / 16;
+  const uint64_t perIter = (uint64_t)nranks * g.C;
+  g.nIters = (uint32_t)((units + perIter - 1) / perIter);
+  const uint64_t stage = 2 * perIter * 16;
+  for (int i = 0; i < nviews; ++i) {
+    if (!views[i].pipeSems || !views[i].scratch) return 4;
+    if (views[i].scratchBytes < stage) return 5;
+  }
+  uint64_t D = views[0].scratchBytes / stage;
+  g.D = (uint32_t)(D > g.nIters ? (g.nIters ? g.nIters : 1) : D);
+  for (int i = 0; i < nviews; ++i)
+    if (hipMemsetAsync(views[i].pipeSems, 0, 3 * 256 * sizeof(uint64_t), s) != hipSuccess) return 1;
+  g_launch_status = 0;
+  if (dtype == kF16)
+    op == kMin ? launchPipeline<kF16, kMin>(views, nviews, g, nranks, nthreads, budget, s)
+               : launchPipeline<kF16, kSum>(views, nviews, g, nranks, nthreads, budget, s);
+  else if (dtype == kBF16)
+    op == kMin ? launchPipeline<kBF16, kMin>(views, nviews, g, nranks, nthreads, budget, s)
+               : launchPipeline<kBF16, kSum>(views, nviews, g, nranks, nthreads, budget, s);
+  else if (dtype == kF32)
+    op == kMin ? launchPipeline<kF32, kMin>(views, nviews, g, nranks, nthreads, budget, s)
+               : launchPipeline<kF32, kSum>(views, nviews, g, nranks, nthreads, budget, s);
+  else if (dtype == kI32)
+    op == kMin ? launchPipeline<kI32, kMin>(views, nviews, g, nranks, nthreads, budget, s)
+               : launchPipeline<kI32, kSum>(views, nviews, g, nranks, nthreads, budget, s);
+  else
+    op == kMin ? launchPipeline<kU32, kMin>(views, nviews, g, nranks, nthreads, budget, s)
+               : launchPipeline<kU32, kSum>(views, nviews, g, nranks, nthreads, budget, s);
+  if (g_launch_status) return g_launch_status;
+  return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
 int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, int nranks, size_t bytes, int dtype,

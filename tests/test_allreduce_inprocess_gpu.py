@@ -219,3 +219,65 @@ def test_tiny_buffers(built, algo, dt, count, op):
                                     for a in ins])
         for r in range(n):
             _cmp(_bytes(douts[r]), exp.view(np.uint8)[:nbytes], dt)
+
+
+def _pipeline_expected(dt, op, ins, nbytes, n, R, T):
+    """Oracle for allreduceRsAgPipeline (allreduce_rsag_pipeline.cu:85-222): 16-byte unit u is owned
+    by slot (u mod n*C) div C (C = R*T*4 units) and summed in ring order from its owner (own,
+    owner+1, ...; calVector(data, tmp) with tmp = own first)."""
+    nw = (nbytes + 15) // 16 * 4
+    padded = []
+    for a in ins:
+        w = np.zeros(nw, np.uint32)
+        w.view(np.uint8)[:nbytes] = a.view(np.uint8)[:nbytes]
+        padded.append(w)
+    C = R * T * 4
+    owner = ((np.arange(nw) // 4) % (n * C)) // C
+    exp = np.zeros(nw, np.uint32)
+    for o in range(n):
+        order = [padded[(o + k) % n] for k in range(n)]
+        seq = O.reduce_seq(dt, op, order)
+        exp[owner == o] = seq[owner == o]
+    return exp
+
+
+@pytest.mark.parametrize("n,dt,count,R,T,stages", [
+    (2, O.F16, 1 << 16, 2, 64, 2), (4, O.F16, (1 << 18) + 7, 2, 64, 2), (8, O.F16, 1 << 19, 2, 64, 3),
+    (8, O.BF16, 100001, 4, 64, 2), (8, O.F32, 1 << 18, 2, 128, 2), (3, O.I32, 77777, 2, 64, 2),
+    (8, O.F16, 1001, 2, 64, 1), (8, O.F16, 24 << 20, 32, 512, 64)])
+def test_rsag_pipeline_bit_exact(built, n, dt, count, R, T, stages):
+    """Pipelined RS+AG: outputs bit-exact against the ring-order oracle on the kernel's interleaved
+    ownership; small workgroup counts and a scratch of only 1-3 stages force many iterations through
+    the circular scratch (credits, put/reduce/recv hand-offs); the last case is the 48 MiB bucket."""
+    import mscclpp_amd as m
+
+    nbytes = count * ITEM[dt]
+    C = R * T * 4
+    stage = 2 * n * C * 16
+    ranks = m.InProcessRanks(n, 1 << 16, bulk_scratch_bytes=stages * stage)
+    for call in range(2):
+        ins = _inputs(dt, n, count, seq=call, special=(call == 1 and dt in (O.F16, O.BF16)))
+        dins = [_dev(a, dt) for a in ins]
+        douts = [torch.full_like(d, 0) for d in dins]
+        ranks.all_reduce(dins, douts, m.ALGO_RSAG_PIPELINE, op=O.SUM, nblocks=R, nthreads=T)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        exp = _pipeline_expected(dt, O.SUM, ins, nbytes, n, R, T)
+        for r in range(n):
+            _cmp(_bytes(douts[r]), exp.view(np.uint8)[:nbytes], dt)
+
+
+def test_rsag_pipeline_min(built):
+    import mscclpp_amd as m
+
+    n, dt, count, R, T = 4, O.F16, 50000, 2, 64
+    ranks = m.InProcessRanks(n, 1 << 16, bulk_scratch_bytes=2 * 2 * n * R * T * 4 * 16)
+    ins = _inputs(dt, n, count, seq=5)
+    dins = [_dev(a, dt) for a in ins]
+    douts = [torch.full_like(d, 0) for d in dins]
+    ranks.all_reduce(dins, douts, m.ALGO_RSAG_PIPELINE, op=O.MIN, nblocks=R, nthreads=T)
+    torch.cuda.synchronize()
+    assert ranks.errors() == [0] * n
+    exp = _pipeline_expected(dt, O.MIN, ins, count * 2, n, R, T)
+    for r in range(n):
+        _cmp(_bytes(douts[r]), exp.view(np.uint8)[: count * 2], dt)

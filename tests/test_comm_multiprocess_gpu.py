@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 CASES = [  # (algo, dtype code, count)
     ("allpair", 0, 4096), ("packet", 0, 1 << 18), ("fullmesh", 0, 1 << 20), ("rsag", 2, 100000),
     ("packet", 1, 30000), ("auto", 0, 48 << 19), ("auto", 2, 1000), ("fullmesh", 1, 12345),
-    ("rsag_zc", 0, 1 << 20), ("rsag_zc", 2, 12345),
+    ("rsag_zc", 0, 1 << 20), ("rsag_zc", 2, 12345), ("rsag_pipeline", 2, 100000), ("rsag_pipeline", 2, 3 << 20),
 ]
 
 
