@@ -272,7 +272,7 @@ def bench_multi(args):
             cands += [(a, nb_, nt_) for nb_, nt_ in ((64, 512), (128, 512), (256, 512), (128, 256), (256, 256))
                       if not shared or nb_ * world <= 256]
         elif a == "rsag_pipeline":  # nblocks = reduce workgroups; the launch is 2x that
-            cands += [(a, nb_, nt_) for nb_, nt_ in ((32, 512), (64, 512), (16, 512), (64, 256))
+            cands += [(a, nb_, nt_) for nb_, nt_ in ((32, 512), (64, 512), (128, 512), (64, 256))
                       if not shared or 2 * nb_ * world <= 256]
         else:
             cands.append((a, 0, 0))
