@@ -98,11 +98,18 @@ int mscclppAmdFlagsInit(uint32_t* flags, void* stream);
 int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts, void* out, size_t bytes, int dtype, int op,
                              uint32_t* flags, int nblocks, uint64_t budgetTicks, uint32_t* err, void* stream);
 
-/* Tuning / ceiling helpers used by the benchmark (fp16 SUM): variant selects lanes-per-unit and
- * the packet cache policies; mscclppAmdCopy is a plain streaming copy (HBM ceiling). */
+/* Tuning / ceiling helpers used by the benchmark (fp16 SUM).  Variant 0 = the product kernel
+ * (partner tiles consumed one round late), 1 = the unskewed round-1 form, 2 / 3 = 4 / 1 KiB of
+ * payload per wave and round, 4 / 5 = variants 0 / 1 adding the number of first-poll misses to
+ * pollMiss[0] (diagnostic).  mscclppAmdCopy is a plain streaming copy (HBM ceiling);
+ * mscclppAmdCopyJobs runs njobs copies in ONE launch, blocksPerJob workgroups each (the xGMI probe:
+ * all peers' links driven from one kernel on one stream). */
 int mscclppAmdSelfReduceLL16Variant(const void* x, const void* y, void* pkts, void* out, size_t bytes, uint32_t* flags,
-                                    int nblocks, int variant, uint64_t budgetTicks, uint32_t* err, void* stream);
+                                    int nblocks, int variant, uint64_t budgetTicks, uint32_t* err, uint32_t* pollMiss,
+                                    void* stream);
 int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblocks, void* stream);
+int mscclppAmdCopyJobs(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs, int blocksPerJob,
+                       void* stream);
 
 /* ---- explicit-view AllReduce ------------------------------------------------------------- */
 /* Launch `algo` for `nviews` ranks of an `nranks`-rank AllReduce in ONE kernel launch (views[i]
@@ -117,8 +124,11 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
 int mscclppAmdCollectiveLaunch(int coll, int algo, const mscclppAmdRankView* views, int nviews, int nranks,
                                size_t bytes, int dtype, int op, int nblocks, int nthreads, uint64_t budgetTicks,
                                void* stream);
-/* Scratch bytes per rank (both halves) that `algo` needs for `bytes` (0 if unsupported). */
+/* Scratch bytes per rank (both halves) that `algo` needs for `bytes` (0 if unsupported).  For the
+ * pipelined RS+AG this is one stage at the default shape (32 x 512); a larger shape needs
+ * mscclppAmdScratchRequiredShape. */
 size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype);
+size_t mscclppAmdScratchRequiredShape(int algo, int nranks, size_t bytes, int dtype, int nblocks, int nthreads);
 /* Algorithm the selector picks (algorithm_selector.cc:91-139 restated for gfx950). */
 int mscclppAmdSelectAlgo(int nranks, size_t bytes, int dtype);
 

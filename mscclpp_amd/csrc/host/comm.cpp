@@ -126,8 +126,18 @@ size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype) 
   }
   if (algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7) return testLLScratchRequired(nranks, bytes);
   if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC || algo == MSCCLPP_AMD_ALGO_TEST_K5) return 0;  // peers' buffers read in place
-  if (algo == MSCCLPP_AMD_ALGO_RSAG_PIPELINE) return 2 * (size_t)nranks * 32 * 512 * 4 * 16;  // one stage, defaults
+  if (algo == MSCCLPP_AMD_ALGO_RSAG_PIPELINE) return mscclppAmdScratchRequiredShape(algo, nranks, bytes, dtype, 0, 0);
   return 0;
+}
+
+// As above for an explicit launch shape (nblocks / nthreads <= 0: the algorithm's defaults).  Only
+// the pipelined RS+AG depends on the shape: it needs at least one stage of 2 * n * (R * T * 4) 16-byte
+// units, R = nblocks reduce workgroups of T = nthreads lanes; more stages deepen the pipeline.
+size_t mscclppAmdScratchRequiredShape(int algo, int nranks, size_t bytes, int dtype, int nblocks, int nthreads) {
+  if (algo != MSCCLPP_AMD_ALGO_RSAG_PIPELINE) return mscclppAmdScratchRequired(algo, nranks, bytes, dtype);
+  if (nblocks <= 0) nblocks = 32;
+  if (nthreads <= 0) nthreads = 512;
+  return 2 * (size_t)nranks * (size_t)nblocks * (size_t)nthreads * 4 * 16;
 }
 
 // algorithm_selector.cc:91-139 for an AMD node: <= 16 KiB one-hop LL8, <= 1 MiB two-hop LL16,

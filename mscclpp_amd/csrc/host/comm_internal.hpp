@@ -406,6 +406,10 @@ struct ncclComm {
     std::lock_guard<std::mutex> lk(mu);
     if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = envAlgo();
     if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = mscclppAmdSelectAlgo(nranks, bytes, dtype);
+    // the pipelined RS+AG carries 2- and 4-byte types only; others take fullmesh, which carries all
+    if (algo == MSCCLPP_AMD_ALGO_RSAG_PIPELINE && dtype != MSCCLPP_AMD_F16 && dtype != MSCCLPP_AMD_BF16 &&
+        dtype != MSCCLPP_AMD_F32 && dtype != MSCCLPP_AMD_I32 && dtype != MSCCLPP_AMD_U32)
+      algo = MSCCLPP_AMD_ALGO_FULLMESH;
     mscclppAmdRankView v = baseView(in, out);
     if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR || algo == MSCCLPP_AMD_ALGO_TEST_K6 ||
         algo == MSCCLPP_AMD_ALGO_TEST_K7) {

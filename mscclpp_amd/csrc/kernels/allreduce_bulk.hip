@@ -17,6 +17,8 @@
 //    (s_waitcnt vmcnt(0)) before the workgroup barrier, and one lane per peer then signals with a
 //    system-scope release atomic add (MemoryDevice2DeviceSemaphore::signal, semaphore_device.hpp:84-90).
 //  * Waits are relaxed system-scope polls followed by one system-scope acquire, bounded in time.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace mscclpp_amd {
@@ -27,7 +29,9 @@ struct BulkGeom {
   uint64_t pass;        // slice bytes handled per pass (multiple of 16)
   uint64_t blk;         // bytes of a pass handled by one workgroup (multiple of 16)
   uint32_t npasses;
-  uint32_t pad;
+  uint32_t debug;       // MSCCLPP_AMD_DEBUG_SKIP_HANDSHAKE (bit 0): skip the reduce-scatter handshake.
+                        // Diagnostic only -- it makes the result wrong on purpose, so that the
+                        // benchmark's bit-exact check can be shown to catch a missing handshake.
 };
 
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -121,7 +125,7 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
           }
         }
       }
-      block_handshake(v, nranks, rank, b, budget);
+      if (!(g.debug & 1u)) block_handshake(v, nranks, rank, b, budget);
     }
 
     // ---- my slice sub-range: reduce (AR, RS), write locally, and (AR, AG) into every peer's output
@@ -487,6 +491,12 @@ __global__ void __launch_bounds__(512) allreduceRsAgPipelineKernel(Views<NV> vie
       }
       sem_release(&credit[r]);
     }
+    // Exit: every peer's recv v has copied my reduced slots out of ITS scratch before my kernel
+    // ends.  Without this a collective issued next on this communicator (fullmesh / reduce-scatter
+    // put into the peers' scratch with no entry handshake) could overwrite a peer's AG region while
+    // that peer is still copying it.  The peers' reduce workgroups are done too: their recv waited
+    // for them.  Same channel as the entry handshakes, so every rank's counters stay in step.
+    block_handshake(v, nranks, rank, g.R + r, budget);
   }
 }
 
@@ -640,6 +650,11 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
   BulkGeom g{};
   if (!bulkScratchRequired(nranks, bytes, views[0].scratchBytes, &g, nblocks)) return 5;
   const int order = (algo == MSCCLPP_AMD_ALGO_RSAG && mode != 2) ? 1 : 0;
+  static const uint32_t debug = [] {
+    const char* e = std::getenv("MSCCLPP_AMD_DEBUG_SKIP_HANDSHAKE");
+    return (e && *e == '1') ? 1u : 0u;
+  }();
+  g.debug = mode == 0 ? debug : 0u;
   if (mode == 2) {  // byte movement only: map to the f16 or f32 instantiation by element width
     dtype = elem_bytes(dtype) == 2 ? kF16 : kF32;
     op = kSum;
@@ -718,7 +733,11 @@ int launchAllReducePipeline(const mscclppAmdRankView* views, int nviews, int nra
     if (!views[i].pipeSems || !views[i].scratch) return 4;
     if (views[i].scratchBytes < stage) return 5;
   }
-  uint64_t D = views[0].scratchBytes / stage;
+  // depth from the smallest view (every rank of a communicator allocates the same scratch, so the
+  // stage offsets agree across ranks; in-process views may differ)
+  uint64_t minScratch = views[0].scratchBytes;
+  for (int i = 1; i < nviews; ++i) minScratch = views[i].scratchBytes < minScratch ? views[i].scratchBytes : minScratch;
+  uint64_t D = minScratch / stage;
   g.D = (uint32_t)(D > g.nIters ? (g.nIters ? g.nIters : 1) : D);
   for (int i = 0; i < nviews; ++i)
     if (hipMemsetAsync(views[i].pipeSems, 0, 3 * 256 * sizeof(uint64_t), s) != hipSuccess) return 1;

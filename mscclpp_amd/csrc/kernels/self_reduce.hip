@@ -3,10 +3,13 @@
 //   P = LL16(Y, flag)                 pack   (copyToPackets<LL16>, copy_device.hpp:160-171)
 //   O = X (op) unpack(P, flag)        reduce (LL16Packet::read + calVectorAccum, allreduce_packet.cu:93-108)
 //
-// One launch, two roles per workgroup.  Workgroup b packs tile t = i*G + b and then consumes the
-// tile packed by its partner b^1 in the same round, so every packet is handed from one CU to a CU
-// on a different XCD (blocks are dealt round-robin over the 8 XCDs) purely through the LL flags,
-// exactly as a peer GPU's packets arrive in the AllReduce.  Partners progress in lock-step, so the
+// One launch, two roles per workgroup.  Workgroup b packs tile t = i*G + b in round i and consumes
+// a tile packed by its partner b^1, so every packet is handed from one CU to a CU on a different
+// XCD (blocks are dealt round-robin over the 8 XCDs) purely through the LL flags, exactly as a peer
+// GPU's packets arrive in the AllReduce.  With SKEW (the default) the tile consumed in round i is
+// the one the partner packed in round i-1: it has had a whole round to land, so the first poll
+// finds its flags and no uncached 1 KiB packet line is re-read (the unskewed form consumed the
+// partner's tile of the same round and re-polled ~10 % of the packet bytes, profiles/r1f_*).  The
 // only residency requirement is that both workgroups of a pair are resident: the host keeps the
 // grid at or below 4 workgroups per CU (256 CUs).  Every spin is time-bounded.
 //
@@ -15,184 +18,31 @@
 
 namespace mscclpp_amd {
 
-template <int DT, int OP, int U, int PKT_POLICY, int LD_POLICY = kSystem>
-__global__ void __launch_bounds__(256) selfReduceLL16Kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
-                                                            uint8_t* pkts, uint8_t* __restrict__ out,
-                                                            uint64_t nunits, uint32_t* flags, uint64_t budget,
-                                                            uint32_t* err) {
-  constexpr uint32_t kThreads = 256;
-  constexpr uint64_t kTileUnits = (uint64_t)kThreads * U;
-  const uint32_t G = gridDim.x;
-  const uint32_t b = blockIdx.x;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t flag = flags[b];
-  const uint64_t ntiles = (nunits + kTileUnits - 1) / kTileUnits;
-  const uint32_t partner = b ^ 1u;
-
-  // Software pipeline per round: the X loads of the tile to consume and the Y loads of the NEXT
-  // tile to pack are in flight while this round's packets are stored and the partner's packets
-  // are polled, so every phase keeps loads outstanding.
-  u32x4 yw[U];
-  auto load_y = [&](uint64_t t) {
-    const uint64_t u0 = t * kTileUnits;
-    auto ry = make_rsrc(y + u0 * 16);
-#pragma unroll
-    for (int k = 0; k < U; ++k)
-      if (u0 + k * kThreads + tid < nunits) yw[k] = load16<kNonTemporal>(ry, (uint32_t)((k * kThreads + tid) * 16));
-  };
-  if (b < ntiles) load_y(b);
-  for (uint64_t base = 0; base < ntiles; base += G) {
-    const uint64_t t = base + b;
-    const uint64_t tp = base + partner;
-    const bool consume = partner < G && tp < ntiles;
-    u32x4 a[U];
-    if (consume) {
-      const uint64_t u0 = tp * kTileUnits;
-      auto rx = make_rsrc(x + u0 * 16);
-#pragma unroll
-      for (int k = 0; k < U; ++k)
-        if (u0 + k * kThreads + tid < nunits) a[k] = load16<kNonTemporal>(rx, (uint32_t)((k * kThreads + tid) * 16));
-    }
-    // ---- pack my tile, then prefetch the next one
-    if (t < ntiles) {
-      const uint64_t u0 = t * kTileUnits;
-      auto rp = make_rsrc(pkts + u0 * 32);
-#pragma unroll
-      for (int k = 0; k < U; ++k)
-        if (u0 + k * kThreads + tid < nunits) ll16_put_unit<PKT_POLICY>(rp, (uint32_t)((k * kThreads + tid) * 32), yw[k], flag);
-      if (t + G < ntiles) load_y(t + G);
-    }
-    // ---- consume my partner's tile
-    if (consume) {
-      const uint64_t u0 = tp * kTileUnits;
-      auto ro = make_rsrc(out + u0 * 16);
-      auto rp = make_rsrc(pkts + u0 * 32);
-      u32x4 v[U];
-      bool ok = true;
-#pragma unroll
-      for (int k = 0; k < U; ++k)
-        if (u0 + k * kThreads + tid < nunits) ok &= ll16_try_unit<LD_POLICY>(rp, (uint32_t)((k * kThreads + tid) * 32), flag, v[k]);
-      if (!ok) {
-#pragma unroll
-        for (int k = 0; k < U; ++k)
-          if (u0 + k * kThreads + tid < nunits)
-            v[k] = ll16_get_unit<LD_POLICY>(rp, (uint32_t)((k * kThreads + tid) * 32), flag, budget, err);
-      }
-#pragma unroll
-      for (int k = 0; k < U; ++k)
-        if (u0 + k * kThreads + tid < nunits)
-          store16<kNonTemporal>(ro, (uint32_t)((k * kThreads + tid) * 16), reduce4<DT, OP>(a[k], v[k]));
-    }
-  }
-  bump_flags(flags, flag);
-}
-
-// Packet-major lane mapping: lane m of a wave owns LL16 packet m, so every packet store and poll is
-// one contiguous 1 KiB wave instruction (whole 64-byte lines), and the payload side moves 8 bytes
-// per lane (512 B contiguous per instruction).  The payload-major form above writes each packet
-// line in two halves from two instructions; on gfx950 WRITE_SIZE shows those partial-line stores
-// cost a full line each (5*S written instead of 3*S).
-template <int DT, int OP, int U, int PKT_POLICY, int LD_POLICY = kSystem>
-__global__ void __launch_bounds__(256) selfReduceLL16PmKernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
-                                                              uint8_t* pkts, uint8_t* __restrict__ out,
-                                                              uint64_t npkts, uint32_t* flags, uint64_t budget,
-                                                              uint32_t* err) {
-  constexpr uint32_t kThreads = 256;
-  constexpr uint64_t kTilePkts = (uint64_t)kThreads * U;
-  const uint32_t G = gridDim.x;
-  const uint32_t b = blockIdx.x;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t flag = flags[b];
-  const uint64_t ntiles = (npkts + kTilePkts - 1) / kTilePkts;
-  const uint32_t partner = b ^ 1u;
-  u32x2 yw[U];
-  auto load_y = [&](uint64_t t) {
-    const uint64_t p0 = t * kTilePkts;
-    auto ry = make_rsrc(y + p0 * 8);
-#pragma unroll
-    for (int k = 0; k < U; ++k)
-      if (p0 + k * kThreads + tid < npkts) yw[k] = load8<kNonTemporal>(ry, (uint32_t)((k * kThreads + tid) * 8));
-  };
-  if (b < ntiles) load_y(b);
-  for (uint64_t base = 0; base < ntiles; base += G) {
-    const uint64_t t = base + b;
-    const uint64_t tp = base + partner;
-    const bool consume = partner < G && tp < ntiles;
-    u32x2 a[U];
-    if (consume) {
-      const uint64_t p0 = tp * kTilePkts;
-      auto rx = make_rsrc(x + p0 * 8);
-#pragma unroll
-      for (int k = 0; k < U; ++k)
-        if (p0 + k * kThreads + tid < npkts) a[k] = load8<kNonTemporal>(rx, (uint32_t)((k * kThreads + tid) * 8));
-    }
-    if (t < ntiles) {
-      const uint64_t p0 = t * kTilePkts;
-      auto rp = make_rsrc(pkts + p0 * 16);
-#pragma unroll
-      for (int k = 0; k < U; ++k)
-        if (p0 + k * kThreads + tid < npkts)
-          store16<PKT_POLICY>(rp, (uint32_t)((k * kThreads + tid) * 16), LL16Packet::make(yw[k].x, yw[k].y, flag));
-      if (t + G < ntiles) load_y(t + G);
-    }
-    if (consume) {
-      const uint64_t p0 = tp * kTilePkts;
-      auto ro = make_rsrc(out + p0 * 8);
-      auto rp = make_rsrc(pkts + p0 * 16);
-      u32x4 v[U];
-      bool ok = true;
-#pragma unroll
-      for (int k = 0; k < U; ++k)
-        if (p0 + k * kThreads + tid < npkts) {
-          v[k] = load16<LD_POLICY>(rp, (uint32_t)((k * kThreads + tid) * 16));
-          ok &= LL16Packet::ready(v[k], flag);
-        }
-      if (!ok) {
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-          if (p0 + k * kThreads + tid < npkts && !LL16Packet::ready(v[k], flag)) {
-            SpinGuard g(budget);
-            do {
-              v[k] = load16<LD_POLICY>(rp, (uint32_t)((k * kThreads + tid) * 16));
-              if (g.expired()) {
-                report_error(err, kErrPacketTimeout);
-                break;
-              }
-            } while (!LL16Packet::ready(v[k], flag));
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < U; ++k)
-        if (p0 + k * kThreads + tid < npkts) {
-          u32x2 r;
-          r.x = reduce_word<DT, OP>(a[k].x, v[k].x);
-          r.y = reduce_word<DT, OP>(a[k].y, v[k].z);
-          store8<kNonTemporal>(ro, (uint32_t)((k * kThreads + tid) * 8), r);
-        }
-    }
-  }
-  bump_flags(flags, flag);
-}
-
 // LDS-staged packets: the payload side moves 16 bytes per lane (one dwordx4 per wave instruction,
 // 1 KiB per wave) and the packet side stays packet-major (lane j owns packet j).  A wave turns its
 // 1 KiB of payload into 128 packets through 1 KiB of its own LDS: each lane writes its 16 bytes, then
 // reads back the 8 bytes of packet j and of packet 64 + j; the consumer runs the same swizzle in
 // reverse before the 16-byte-per-lane sum and output store.  LDS traffic per wave-tile is three
 // ds ops per side; the crossing stays inside one wave, so no barrier is needed (one wave's LDS
-// operations complete in order).
-template <int DT, int OP, int U>
+// operations complete in order).  The pack side and the consume side use separate LDS tiles, so
+// with SKEW the consume of one tile and the pack of another never share a buffer.
+//
+// COUNT: diagnostic build that adds the number of packets whose first poll missed to pollMiss[0]
+// (one atomic per wave and round), to measure the re-poll traffic the skew removes.
+template <int DT, int OP, int U, bool SKEW, bool COUNT>
 __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
                                                                uint8_t* pkts, uint8_t* __restrict__ out, uint64_t bytes,
-                                                               uint32_t* flags, uint64_t budget, uint32_t* err) {
+                                                               uint32_t* flags, uint64_t budget, uint32_t* err,
+                                                               uint32_t* pollMiss) {
   constexpr uint32_t kWaves = 4;
   constexpr uint64_t kTileBytes = (uint64_t)kWaves * U * 1024;  // payload bytes per workgroup and round
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kWaves][U][1024];
+  __shared__ __attribute__((aligned(16))) uint8_t ldsP[kWaves][U][1024];
+  __shared__ __attribute__((aligned(16))) uint8_t ldsC[kWaves][U][1024];
   const uint32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
   const uint32_t flag = flags[b];
   const uint64_t ntiles = (bytes + kTileBytes - 1) / kTileBytes;
+  const uint64_t rounds = (ntiles + G - 1) / G;
   const uint32_t partner = b ^ 1u;
   // payload byte offset of (tile, sub-tile k) for this wave: 1 KiB chunks dealt k-major over waves
   auto chunk = [&](uint64_t t, int k) { return t * kTileBytes + (uint64_t)(k * kWaves + wave) * 1024; };
@@ -205,10 +55,11 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
     }
   };
   if (b < ntiles) load_y(b);
-  for (uint64_t base = 0; base < ntiles; base += G) {
-    const uint64_t t = base + b;
-    const uint64_t tp = base + partner;
-    const bool consume = partner < G && tp < ntiles;
+  for (uint64_t i = 0; i < rounds + (SKEW ? 1 : 0); ++i) {
+    const uint64_t t = i * G + b;                          // packed this round (i < rounds)
+    const uint64_t tp = (SKEW ? i - 1 : i) * G + partner;  // consumed this round
+    const bool pack = i < rounds && t < ntiles;
+    const bool consume = (!SKEW || i > 0) && partner < G && tp < ntiles;
     u32x4 a[U];
     if (consume) {
 #pragma unroll
@@ -218,23 +69,22 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
       }
     }
     // ---- pack: payload -> LDS -> packet-major stores (packets j and 64 + j of each 1 KiB chunk)
-    if (t < ntiles) {
+    if (pack) {
 #pragma unroll
-      for (int k = 0; k < U; ++k) *(u32x4*)&lds[wave][k][lane * 16] = yw[k];
+      for (int k = 0; k < U; ++k) *(u32x4*)&ldsP[wave][k][lane * 16] = yw[k];
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const uint64_t c = chunk(t, k);
         const auto rp = make_rsrc(pkts + 2 * c);
-        const u32x2 lo = *(const u32x2*)&lds[wave][k][lane * 8];
-        const u32x2 hi = *(const u32x2*)&lds[wave][k][512 + lane * 8];
+        const u32x2 lo = *(const u32x2*)&ldsP[wave][k][lane * 8];
+        const u32x2 hi = *(const u32x2*)&ldsP[wave][k][512 + lane * 8];
         if (c + lane * 8 < bytes) store16<kSystem>(rp, lane * 16, LL16Packet::make(lo.x, lo.y, flag));
         if (c + 512 + lane * 8 < bytes) store16<kSystem>(rp, 1024 + lane * 16, LL16Packet::make(hi.x, hi.y, flag));
       }
-      __builtin_amdgcn_wave_barrier();
       if (t + G < ntiles) load_y(t + G);
     }
-    // ---- consume my partner's tile: packet-major polls -> LDS -> payload-major sum and store
+    // ---- consume a partner tile: packet-major polls -> LDS -> payload-major sum and store
     if (consume) {
       u32x4 v[2 * U];
       bool ok = true;
@@ -251,38 +101,49 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
           ok &= LL16Packet::ready(v[2 * k + 1], flag);
         }
       }
+      if constexpr (COUNT) {
+        uint32_t miss = 0;
+#pragma unroll
+        for (int i2 = 0; i2 < 2 * U; ++i2) {
+          const uint64_t c = chunk(tp, i2 / 2);
+          if (c + (i2 & 1) * 512 + lane * 8 < bytes && !LL16Packet::ready(v[i2], flag)) ++miss;
+        }
+        // wave-wide sum of the misses, one atomic per wave
+        for (int off = 32; off > 0; off >>= 1) miss += __shfl_xor(miss, off, 64);
+        if (lane == 0 && miss) __hip_atomic_fetch_add(pollMiss, miss, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (!ok) {
 #pragma unroll
-        for (int i = 0; i < 2 * U; ++i) {
-          const uint64_t c = chunk(tp, i / 2);
-          const uint32_t off = (i & 1) * 1024 + lane * 16;
-          if (c + (i & 1) * 512 + lane * 8 < bytes && !LL16Packet::ready(v[i], flag)) {
+        for (int i2 = 0; i2 < 2 * U; ++i2) {
+          const uint64_t c = chunk(tp, i2 / 2);
+          const uint32_t off = (i2 & 1) * 1024 + lane * 16;
+          if (c + (i2 & 1) * 512 + lane * 8 < bytes && !LL16Packet::ready(v[i2], flag)) {
             const auto rp = make_rsrc(pkts + 2 * c);
             SpinGuard g(budget);
             do {
-              v[i] = load16<kSystem>(rp, off);
+              v[i2] = load16<kSystem>(rp, off);
               if (g.expired()) {
                 report_error(err, kErrPacketTimeout);
                 break;
               }
-            } while (!LL16Packet::ready(v[i], flag));
+            } while (!LL16Packet::ready(v[i2], flag));
           }
         }
       }
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        *(u32x2*)&lds[wave][k][lane * 8] = u32x2{v[2 * k].x, v[2 * k].z};
-        *(u32x2*)&lds[wave][k][512 + lane * 8] = u32x2{v[2 * k + 1].x, v[2 * k + 1].z};
+        *(u32x2*)&ldsC[wave][k][lane * 8] = u32x2{v[2 * k].x, v[2 * k].z};
+        *(u32x2*)&ldsC[wave][k][512 + lane * 8] = u32x2{v[2 * k + 1].x, v[2 * k + 1].z};
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const uint64_t c = chunk(tp, k);
-        const u32x4 p = *(const u32x4*)&lds[wave][k][lane * 16];
+        const u32x4 p = *(const u32x4*)&ldsC[wave][k][lane * 16];
         if (c + lane * 16 < bytes) store16<kNonTemporal>(make_rsrc(out + c), lane * 16, reduce4<DT, OP>(a[k], p));
       }
-      __builtin_amdgcn_wave_barrier();
     }
+    __builtin_amdgcn_wave_barrier();
   }
   bump_flags(flags, flag);
 }
@@ -290,10 +151,10 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
 template <int DT, int OP>
 static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                              int nblocks, uint64_t budget, uint32_t* err, hipStream_t stream) {
-  // LDS-staged packets, 2 KiB of payload per wave and round (tools/sweep_self_reduce.py: 56.3-57.3 us
-  // at 48 MiB and 1024 workgroups vs 57.7-58.9 us for the packet-major register form, variant 13)
-  hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2>), dim3(nblocks), dim3(256), 0, stream, (const uint8_t*)x,
-                     (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err);
+  // LDS-staged packets, 2 KiB of payload per wave and round, partner tiles consumed one round late
+  hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, true, false>), dim3(nblocks), dim3(256), 0, stream,
+                     (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
+                     (uint32_t*)nullptr);
 }
 
 // Streaming copy (read S, write S) used by the benchmark to measure the achievable HBM ceiling on
@@ -315,50 +176,61 @@ __global__ void __launch_bounds__(256) copyKernel(const uint8_t* __restrict__ sr
   }
 }
 
+// Several independent copies in ONE launch: workgroups [j*B, (j+1)*B) move job j.  The xGMI probe
+// uses it so that all peers' links are driven by one kernel on one stream (one hardware queue),
+// instead of one stream per peer that the pool's GPU_MAX_HW_QUEUES=4 would serialise.  Remote
+// sides are IPC-mapped peer memory: loads and stores of the remote side are system scope.
+struct CopyJobs {
+  const uint8_t* src[MSCCLPP_AMD_MAX_RANKS * 2];
+  uint8_t* dst[MSCCLPP_AMD_MAX_RANKS * 2];
+  uint64_t units[MSCCLPP_AMD_MAX_RANKS * 2];
+};
+
+template <int U>
+__global__ void __launch_bounds__(256) copyJobsKernel(CopyJobs jobs, uint32_t blocksPerJob) {
+  const uint32_t j = blockIdx.x / blocksPerJob, jb = blockIdx.x % blocksPerJob;
+  const uint8_t* src = jobs.src[j];
+  uint8_t* dst = jobs.dst[j];
+  const uint64_t nunits = jobs.units[j];
+  const uint64_t stride = (uint64_t)blocksPerJob * 256 * U;
+  for (uint64_t u0 = (uint64_t)jb * 256 * U; u0 < nunits; u0 += stride) {
+    auto rs = make_rsrc(src + u0 * 16);
+    auto rd = make_rsrc(dst + u0 * 16);
+    u32x4 w[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (u0 + k * 256 + threadIdx.x < nunits) w[k] = load16<kSystem>(rs, (k * 256 + threadIdx.x) * 16);
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (u0 + k * 256 + threadIdx.x < nunits) store16<kSystem>(rd, (k * 256 + threadIdx.x) * 16, w[k]);
+  }
+}
+
 }  // namespace mscclpp_amd
 
 using namespace mscclpp_amd;
 
-// Tuning entry (fp16 SUM): variant selects <U, packet store policy, packet load policy>.
+// Tuning / diagnostic entry (fp16 SUM): variant 0 = the product form (skewed, 2 KiB per wave and
+// round), 1 = unskewed (round-1 form), 2 = skewed with 4 KiB per wave and round, 3 = skewed with
+// 1 KiB; 4 / 5 = variants 0 / 1 counting first-poll misses into pollMiss[0] (must not be null).
 extern "C" int mscclppAmdSelfReduceLL16Variant(const void* x, const void* y, void* pkts, void* out, size_t bytes,
                                                uint32_t* flags, int nblocks, int variant, uint64_t budgetTicks,
-                                               uint32_t* err, void* streamPtr) {
+                                               uint32_t* err, uint32_t* pollMiss, void* streamPtr) {
   hipStream_t s = (hipStream_t)streamPtr;
-  if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > kFlagSlots) return 4;
+  if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > 1024) return 4;
+  if ((variant == 4 || variant == 5) && !pollMiss) return 4;
   if (nblocks % 2) nblocks += 1;
-  const uint64_t nunits = bytes / 16;
-#define SRV(U, SP, LP)                                                                                        \
-  hipLaunchKernelGGL((selfReduceLL16Kernel<kF16, kSum, U, SP, LP>), dim3(nblocks), dim3(256), 0, s,           \
-                     (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, nunits, flags, budgetTicks, err)
+#define SRV(U, SKEW, COUNT)                                                                                       \
+  hipLaunchKernelGGL((selfReduceLL16LdsKernel<kF16, kSum, U, SKEW, COUNT>), dim3(nblocks), dim3(256), 0, s,       \
+                     (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, (uint64_t)bytes, flags, \
+                     budgetTicks, err, pollMiss)
   switch (variant) {
-    case 0: SRV(4, kAgent, kSystem); break;
-    case 1: SRV(2, kAgent, kSystem); break;
-    case 2: SRV(8, kAgent, kSystem); break;
-    case 3: SRV(4, kNonTemporal, kSystem); break;
-    case 4: SRV(4, kPlain, kSystem); break;
-    case 5: SRV(4, kAgent, kAgent); break;
-    case 6: SRV(4, kSystem, kSystem); break;
-    case 7: SRV(4, kNonTemporal, kAgent); break;
-    case 8: SRV(8, kNonTemporal, kAgent); break;
-    case 9: SRV(2, kNonTemporal, kAgent); break;
-#define SRVPM(U, SP, LP)                                                                                      \
-  hipLaunchKernelGGL((selfReduceLL16PmKernel<kF16, kSum, U, SP, LP>), dim3(nblocks), dim3(256), 0, s,         \
-                     (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes / 8, flags, budgetTicks, err)
-    case 10: SRVPM(8, kAgent, kSystem); break;
-    case 11: SRVPM(4, kAgent, kSystem); break;
-    case 12: SRVPM(16, kAgent, kSystem); break;
-    case 13: SRVPM(8, kSystem, kSystem); break;
-    case 14: SRVPM(8, kNonTemporal, kSystem); break;
-    case 15: SRVPM(8, kAgent, kAgent); break;
-#undef SRVPM
-#define SRVLDS(U)                                                                                             \
-  hipLaunchKernelGGL((selfReduceLL16LdsKernel<kF16, kSum, U>), dim3(nblocks), dim3(256), 0, s, (const uint8_t*)x, \
-                     (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, (uint64_t)bytes, flags, budgetTicks, err)
-    case 16: SRVLDS(4); break;
-    case 17: SRVLDS(8); break;
-    case 18: SRVLDS(2); break;
-    case 19: SRVLDS(1); break;
-#undef SRVLDS
+    case 0: SRV(2, true, false); break;
+    case 1: SRV(2, false, false); break;
+    case 2: SRV(4, true, false); break;
+    case 3: SRV(1, true, false); break;
+    case 4: SRV(2, true, true); break;
+    case 5: SRV(2, false, true); break;
     default: return 4;
   }
 #undef SRV
@@ -373,13 +245,30 @@ extern "C" int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblo
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+extern "C" int mscclppAmdCopyJobs(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs,
+                                  int blocksPerJob, void* streamPtr) {
+  if (!srcs || !dsts || !bytes || njobs < 1 || njobs > 2 * MSCCLPP_AMD_MAX_RANKS) return 4;
+  if (blocksPerJob <= 0) blocksPerJob = 128;
+  if ((long)blocksPerJob * njobs > 65535) return 4;
+  CopyJobs jobs{};
+  for (int j = 0; j < njobs; ++j) {
+    if (!srcs[j] || !dsts[j] || bytes[j] == 0 || bytes[j] % 16) return 4;
+    jobs.src[j] = (const uint8_t*)srcs[j];
+    jobs.dst[j] = (uint8_t*)dsts[j];
+    jobs.units[j] = bytes[j] / 16;
+  }
+  hipLaunchKernelGGL((copyJobsKernel<4>), dim3(blocksPerJob * njobs), dim3(256), 0, (hipStream_t)streamPtr, jobs,
+                     (uint32_t)blocksPerJob);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 extern "C" int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts, void* out, size_t bytes, int dtype,
                                         int op, uint32_t* flags, int nblocks, uint64_t budgetTicks, uint32_t* err,
                                         void* streamPtr) {
   hipStream_t stream = (hipStream_t)streamPtr;
   if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0) return 4;
   if (nblocks <= 0) {
-    // one 8 KiB payload tile per workgroup and round; 1024 workgroups = 4 per CU (8 KiB LDS each),
+    // one 8 KiB payload tile per workgroup and round; 1024 workgroups = 4 per CU (16 KiB LDS each),
     // all resident, so every partner pair is co-resident
     const uint64_t tiles = (bytes + 8191) / 8192;
     nblocks = (int)(tiles < 1024 ? tiles : 1024);

@@ -587,6 +587,22 @@ void oracle_allreduce_sliced(int dtype, int op, int n, const uint32_t* const* in
   }
 }
 
+/* The AllReduce result (one output buffer) when word w belongs to owner (w mod period) / chunk and
+ * is reduced by that owner in `order_kind` order:
+ *   period = n * slice, chunk = slice            contiguous slices (fullmesh kind 0, rsag kind 1)
+ *   period = n * 4C,    chunk = 4C words         allreduceRsAgPipeline's interleaved slots
+ *                                                (allreduce_rsag_pipeline.cu:104-117, C units of 16 B)
+ * With period >= nwords and slice = ceil-to-16-bytes this equals oracle_allreduce_sliced. */
+void oracle_allreduce_owned(int dtype, int op, int n, const uint32_t* const* in, uint64_t nwords,
+                            uint64_t period_words, uint64_t chunk_words, int order_kind, uint32_t* out) {
+  for (uint64_t w0 = 0; w0 < nwords; w0 += chunk_words) {
+    const int owner = (int)((w0 % period_words) / chunk_words);
+    uint64_t nw = chunk_words;
+    if (w0 + nw > nwords) nw = nwords - w0;
+    reduce_range(dtype, op, n, in, owner < n ? owner : n - 1, order_kind, w0, nw, out + w0);
+  }
+}
+
 /* ---- FIFO / ProxyTrigger (fifo_device.hpp:35-141, fifo.cc:58-78) ------------------------- */
 void oracle_trigger_encode(uint64_t type, uint32_t dstId, uint64_t dstOffset, uint32_t srcId,
                            uint64_t srcOffset, uint64_t bytes, uint32_t semaphoreId, uint64_t out[2]) {

@@ -60,6 +60,7 @@ def L():
             ("oracle_allreduce_allpairs", [i32, i32, i32, vp, u64, u32, u64, vp, vp], None),
             ("oracle_allreduce_sliced", [i32, i32, i32, vp, u64, u64, i32, vp], None),
             ("oracle_mscclpp_test_ll", [i32, vp, u64, u32, vp, vp], None),
+            ("oracle_allreduce_owned", [i32, i32, i32, vp, u64, u64, u64, i32, vp], None),
             ("oracle_trigger_encode", [u64, u32, u64, u32, u64, u64, u32, vp], None),
             ("oracle_fifo_commit_bit", [u64, u32], u64),
             ("oracle_lcg_fill", [i32, u64, i32, i32, vp], None),
@@ -161,6 +162,23 @@ def allreduce_sliced(dtype, op, inputs, nwords, slice_words, order_kind):
     outs = [np.zeros(nwords, np.uint32) for _ in range(n)]
     L().oracle_allreduce_sliced(dtype, op, n, _ptr_array(ins), nwords, slice_words, order_kind, _ptr_array(outs))
     return outs
+
+
+def allreduce_owned(dtype, op, inputs, nwords, period_words, chunk_words, order_kind):
+    """One AllReduce result buffer: word w owned by (w % period) // chunk, reduced in that owner's
+    order (0 fullmesh: owner then ascending; 1 ring: owner, owner+1, ...)."""
+    n = len(inputs)
+    ins = []
+    for a in inputs:
+        w = np.ascontiguousarray(a).view(np.uint8)
+        if w.size < nwords * 4:  # pad a ragged tail with zeros (the kernels' 16-byte units)
+            p = np.zeros(nwords * 4, np.uint8)
+            p[: w.size] = w
+            w = p
+        ins.append(w.view(np.uint32))
+    out = np.zeros(nwords, np.uint32)
+    L().oracle_allreduce_owned(dtype, op, n, _ptr_array(ins), nwords, period_words, chunk_words, order_kind, _p(out))
+    return out
 
 
 def trigger_encode(typ, dst_id, dst_off, src_id, src_off, nbytes, sem):

@@ -1,0 +1,82 @@
+"""bench.py's N-rank launcher and its input generator (CPU only; no GPU is touched).
+
+`python bench.py --gpus N` without WORLD_SIZE must start N ranks with the torch.distributed.run
+environment, and a --gpus that disagrees with WORLD_SIZE must fail.  The device
+LCG of the N>1 benchmark must generate exactly the oracle's inputs (test/torch/correctness_test.py:
+19-56), and the oracle's owner-sliced AllReduce must agree with its per-slice form."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def _bench(args, env_extra=None, timeout=120):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_launcher_spawns_n_ranks(n):
+    r = _bench(["--gpus", str(n), "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["master"] == "127.0.0.1" and int(d["port"]) > 0
+
+
+def test_gpus_world_size_mismatch_fails():
+    r = _bench(["--gpus", "8", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "disagrees" in r.stderr
+
+
+def test_failing_rank_fails_the_launch():
+    r = _bench(["--gpus", "2", "--dry-run"], {"BENCH_DRY_RUN_FAIL_RANK": "1"})
+    assert r.returncode == 3
+
+
+def test_device_lcg_matches_oracle():
+    import bench
+    import oracle_lib as O
+
+    for rank, seq in ((0, 0), (3, 1), (7, 1)):
+        t = bench.lcg_tensor(100003, rank, seq, torch.float16, "cpu")
+        ref = O.lcg(O.F16, 100003, rank, seq)
+        assert np.array_equal(t.view(torch.int16).numpy().view(np.uint16), ref)
+
+
+def test_owned_allreduce_matches_sliced():
+    import oracle_lib as O
+
+    n, count = 8, (1 << 16) + 24
+    ins = [O.lcg(O.F16, count, r, 1) for r in range(n)]
+    nbytes = count * 2
+    slice_w = ((nbytes + n - 1) // n + 15) // 16 * 4
+    nw = (nbytes + 15) // 16 * 4
+    for order in (0, 1):
+        owned = O.allreduce_owned(O.F16, O.SUM, ins, nw, n * slice_w, slice_w, order)
+        padded = []
+        for a in ins:
+            w = np.zeros(nw, np.uint32)
+            w.view(np.uint8)[:nbytes] = a.view(np.uint8)
+            padded.append(w)
+        sliced = O.allreduce_sliced(O.F16, O.SUM, padded, nw, slice_w, order)[0]
+        assert np.array_equal(owned, sliced)
+    # interleaved ownership (rsag_pipeline): unit u owned by (u mod n*C) // C, ring order from the owner
+    C = 64
+    owned = O.allreduce_owned(O.F16, O.SUM, ins, nw, n * 4 * C, 4 * C, 1)
+    padded = [np.pad(a.view(np.uint32), (0, nw - a.size // 2)) for a in ins]
+    owner = ((np.arange(nw) // 4) % (n * C)) // C
+    for o in range(n):
+        seq = O.reduce_seq(O.F16, O.SUM, [padded[(o + k) % n] for k in range(n)])
+        assert np.array_equal(owned[owner == o], seq[owner == o])

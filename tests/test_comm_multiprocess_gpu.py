@@ -319,3 +319,69 @@ def test_collectives_wait_for_the_peers_stream(built):
                 p.kill()
     for rank in range(n):
         assert got[rank] == [True, True, True, 0], (rank, got[rank])
+
+
+def _pipeline_then_worker(rank, n, uid, q):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "10000")
+        import torch
+
+        import mscclpp_amd as m
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        res = []
+        cnt = 3 << 20  # 12 MiB of int32: several pipeline iterations at every shape below
+        base = torch.arange(cnt, dtype=torch.int32, device="cuda") % 1000003
+        x = base + rank
+        exp = base * n + n * (n - 1) // 2
+        y = torch.empty_like(x)
+        blk = 1 << 18
+        rs_in = (torch.arange(n * blk, dtype=torch.int32, device="cuda") % 999) * (rank + 1)
+        rs_out = torch.empty(blk, dtype=torch.int32, device="cuda")
+        rs_exp = (torch.arange(n * blk, dtype=torch.int32, device="cuda") % 999)[rank * blk:(rank + 1) * blk] * (n * (n + 1) // 2)
+        for it in range(6):
+            nb, nt = ((32, 256), (64, 512), (2, 64))[it % 3]  # the geometry changes between calls
+            y.fill_(-1)
+            comm.all_reduce(x, y, algo="rsag_pipeline", nblocks=nb, nthreads=nt)
+            # issued at once behind it on the same communicator: puts into the peers' bulk scratch
+            comm.reduce_scatter(rs_in, rs_out)
+            ok_pipe = bool(torch.equal(y, exp))
+            y.fill_(-1)
+            comm.all_reduce(x, y, algo="fullmesh", nblocks=64 if it % 2 else 128)
+            comm.all_reduce(x, y, algo="rsag_pipeline", nblocks=nb, nthreads=nt)
+            torch.cuda.synchronize()
+            res.append(ok_pipe and bool(torch.equal(rs_out, rs_exp)) and bool(torch.equal(y, exp)))
+        res.append(comm.device_error())
+        comm.destroy()
+        q.put((rank, res, None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_pipeline_then_scratch_collectives(built):
+    """the pipelined RS+AG must not end while a peer still copies out of its
+    scratch, since the next collective on the communicator (reduce-scatter / fullmesh, which put into
+    the peers' scratch with no entry handshake, or a pipeline of another geometry) reuses it."""
+    import mscclpp_amd as m
+
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    uid = m.Communicator.unique_id()
+    procs = [ctx.Process(target=_pipeline_then_worker, args=(r, n, uid, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=200)
+            assert err is None, err
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        assert got[rank] == [True] * 6 + [0], (rank, got[rank])

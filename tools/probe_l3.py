@@ -16,9 +16,6 @@ import mscclpp_amd as m  # noqa: E402
 
 L = m.lib()
 vp = ctypes.c_void_p
-L.mscclppAmdSelfReduceLL16Variant.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int, ctypes.c_int,
-                                               ctypes.c_uint64, vp, vp]
-L.mscclppAmdCopy.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
 
 S = int(os.environ.get("BYTES", 48 << 20))
 n = S // 2
@@ -34,9 +31,10 @@ scrub = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
 s = m.stream_ptr()
 
 
-def sr(pk, variant=18, nb=1024):
+def sr(pk, variant=0, nb=1024):
     assert L.mscclppAmdSelfReduceLL16Variant(vp(x.data_ptr()), vp(y.data_ptr()), vp(pk.ptr), vp(out.data_ptr()), S,
-                                             vp(flags.data_ptr()), nb, variant, 500_000_000, vp(err.data_ptr()), s) == 0
+                                             vp(flags.data_ptr()), nb, variant, 500_000_000, vp(err.data_ptr()), None,
+                                             s) == 0
 
 
 def ev():
