@@ -30,6 +30,7 @@
 #include <utility>
 #include <vector>
 
+#include "mscclpp_amd/core.hpp"
 #include "mscclpp_amd/executor.h"
 #include "mscclpp_amd/nccl.h"
 
@@ -70,27 +71,8 @@ enum ReduceOp { SUM = 0, MIN = 3, NOP = 255 };
 // ncclDataType_t -> DataType (datatype_conversion.hpp); AUTO for types the path does not carry.
 DataType dataTypeFromNccl(ncclDataType_t t);
 
-// The communicator handed to algorithms (the reference passes std::shared_ptr<mscclpp::Communicator>).
-class Communicator {
- public:
-  explicit Communicator(ncclComm_t comm) : comm_(comm) {}
-  ncclComm_t ncclComm() const { return comm_; }
-  int rank() const;
-  int nRanks() const;
-  int nRanksPerNode() const;  // one MI355X node: == nRanks()
-  int device() const;
-  // Collective over the communicator: every rank passes its matching buffer (any pointer inside a
-  // hipMalloc'd / hipExtMallocWithFlags'd allocation).  Returns every rank's buffer as mapped in
-  // this process (entry [rank()] is `ptr`); peers' entries are IPC mappings over xGMI that device
-  // code may load from and store to.  Mappings are cached per allocation.
-  std::vector<void*> registerMemory(void* ptr);
-  // Host-side bootstrap collectives (Bootstrap::allGather / barrier).
-  void allGather(const void* sendbuf, void* recvbuf, size_t bytesPerRank);
-  void barrier();
-
- private:
-  ncclComm_t comm_;
-};
+// The communicator handed to algorithms (the reference passes std::shared_ptr<mscclpp::Communicator>)
+// is mscclpp_amd::Communicator of core.hpp.
 
 class ExecutionPlan {
  public:

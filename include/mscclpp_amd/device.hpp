@@ -34,6 +34,7 @@ enum DeviceError : uint32_t {
   kErrSemaphoreTimeout = 2,  // a semaphore wait never completed
   kErrFifoTimeout = 3,       // a FIFO push found the ring full for too long
   kErrBadGeometry = 4,       // host passed inconsistent sizes
+  kErrProxyFailure = 5,      // a host proxy's copy or token update failed (set from the host)
 };
 
 // Buffer resource over a raw pointer.  num_records = 0xFFFFFFFF: the whole 32-bit offset space is
@@ -83,6 +84,16 @@ struct SpinGuard {
     return wall_ticks() > deadline;
   }
 };
+
+// Spin budget of the reference-spelled waits that carry no budget of their own (LL16Packet::read,
+// copyFromPackets, ...): 20 s of wall clock, the library default (MSCCLPP_AMD_SPIN_TIMEOUT_MS).
+//
+// The reference's `maxSpinCount` arguments (poll_device.hpp:12-18) are accepted for source
+// compatibility and, as in the reference's release build (MSCCLPP_ASSERT_DEVICE is active only with
+// DEBUG_BUILD, assert_device.hpp), do not end a wait.  What ends a stuck wait here is the
+// wall-clock budget, in every build: the wait returns and the error word (when the handle has one)
+// records the timeout.
+constexpr uint64_t kDefaultSpinTicks = 2000000000ull;
 
 __device__ __forceinline__ void report_error(uint32_t* err, uint32_t code) {
   if (err) {

@@ -1,72 +1,51 @@
 // MemoryChannel device surface for gfx950: one-sided put / get / read / write, putPackets /
-// unpackPackets (LL16 or LL8) and signal / wait over peer memory mapped through IPC.
+// unpackPacket(s) (LL16 or LL8) and signal / wait over peer memory mapped through IPC.
 //
-// API shape follows include/mscclpp/memory_channel_device.hpp:15-224 and semaphore_device.hpp:61-135
-// (same member names, argument order and meaning); every wait takes a time budget and reports
-// timeouts through the device error word instead of asserting.  Stores into peer memory are
-// system-scope write-through; polls of local memory written by peers are system-scope loads.
-// The threaded helpers keep the reference's "thread tid of nthreads handles packets tid,
-// tid + nthreads, ..." mapping, which is packet-major: consecutive lanes move consecutive 16-byte
-// packets, so each wave instruction is one contiguous 1 KiB access.
+// Spellings, argument order and meaning follow include/mscclpp/memory_channel_device.hpp:15-224
+// (BaseMemoryChannelDeviceHandle { semaphore_ }, MemoryChannelDeviceHandle { dst_, src_,
+// packetBuffer_ }), so a kernel written against the reference compiles here after a namespace
+// change.  What differs is underneath: stores into peer memory (put, putPackets) are 16-byte
+// system-scope write-through buffer stores, loads of peer memory (get) are system-scope, and every
+// wait is bounded by the semaphore handle's wall-clock budget and reports through its error word
+// instead of spinning forever.  The threaded helpers keep the reference's "thread tid of nthreads
+// handles elements tid, tid + nthreads, ..." mapping, which is packet-major: consecutive lanes move
+// consecutive 16-byte packets, so each wave instruction is one contiguous 1 KiB access.
 #pragma once
 
-#include "packet_device.hpp"
+#include "copy_device.hpp"
+#include "semaphore_device.hpp"
 
 namespace mscclpp_amd {
 
-struct MemoryDevice2DeviceSemaphoreDeviceHandle {
-  uint64_t* inboundToken;          // local, written (added to) by the peer
-  uint64_t* remoteInboundToken;    // the peer's inboundToken as mapped here
-  uint64_t* expectedInboundToken;  // local wait counter
+// memory_channel_device.hpp:15-54
+struct BaseMemoryChannelDeviceHandle {
+  MemoryDevice2DeviceSemaphoreDeviceHandle semaphore_;
+
+  BaseMemoryChannelDeviceHandle() = default;
+  __host__ __device__ BaseMemoryChannelDeviceHandle(MemoryDevice2DeviceSemaphoreDeviceHandle semaphore)
+      : semaphore_(semaphore) {}
 
 #if defined(__HIP__)
-  // semaphore_device.hpp:84-90: prior memory operations complete before the peer sees the signal
-  __device__ __forceinline__ void signal() { add_release_sys(remoteInboundToken, 1); }
-  __device__ __forceinline__ void relaxedSignal() { add_relaxed_sys(remoteInboundToken, 1); }
-  __device__ __forceinline__ bool poll() {
-    const uint64_t want = __hip_atomic_load(expectedInboundToken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    if (ld_acquire_sys(inboundToken) >= want) {
-      __hip_atomic_fetch_add(expectedInboundToken, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return true;
-    }
-    return false;
-  }
-  __device__ __forceinline__ bool wait(uint64_t budget, uint32_t* err) {
-    const uint64_t want =
-        __hip_atomic_fetch_add(expectedInboundToken, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    SpinGuard g(budget);
-    while (ld_relaxed_sys(inboundToken) < want) {
-      if (g.expired()) {
-        report_error(err, kErrSemaphoreTimeout);
-        return false;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
-    return true;
-  }
-  __device__ __forceinline__ bool relaxedWait(uint64_t budget, uint32_t* err) {
-    const uint64_t want =
-        __hip_atomic_fetch_add(expectedInboundToken, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    SpinGuard g(budget);
-    while (ld_relaxed_sys(inboundToken) < want) {
-      if (g.expired()) {
-        report_error(err, kErrSemaphoreTimeout);
-        return false;
-      }
-    }
-    return true;
+  __device__ __forceinline__ void signal() { semaphore_.signal(); }
+  __device__ __forceinline__ void relaxedSignal() { semaphore_.relaxedSignal(); }
+  __device__ __forceinline__ bool poll() { return semaphore_.poll(); }
+  __device__ __forceinline__ void wait(int64_t maxSpinCount = 10000000) { semaphore_.wait(maxSpinCount); }
+  __device__ __forceinline__ void relaxedWait(int64_t maxSpinCount = 10000000) {
+    semaphore_.relaxedWait(maxSpinCount);
   }
 #endif
 };
 
-struct MemoryChannelDeviceHandle {
-  MemoryDevice2DeviceSemaphoreDeviceHandle semaphore_;
+// memory_channel_device.hpp:56-224
+struct MemoryChannelDeviceHandle : public BaseMemoryChannelDeviceHandle {
   void* dst_;           // peer memory (mapped here)
   void* src_;           // local memory
-  void* packetBuffer_;  // local packet buffer the peer puts packets into
-  uint64_t budget_;     // spin budget in 10 ns ticks
-  uint32_t* err_;       // device error word
+  void* packetBuffer_;  // local packet buffer the peer puts packets into (may be null)
+
+  MemoryChannelDeviceHandle() = default;
+  __host__ __device__ MemoryChannelDeviceHandle(MemoryDevice2DeviceSemaphoreDeviceHandle semaphore, void* dst,
+                                                void* src, void* packetBuffer)
+      : BaseMemoryChannelDeviceHandle(semaphore), dst_(dst), src_(src), packetBuffer_(packetBuffer) {}
 
 #if defined(__HIP__)
   template <typename T>
@@ -78,61 +57,84 @@ struct MemoryChannelDeviceHandle {
     *(reinterpret_cast<T*>(dst_) + index) = v;
   }
 
-  // Threaded copy (copy_device.hpp:34-128): 16-byte vectors then 4-byte remainder; offsets and
-  // sizes must be 4-byte aligned.  put writes peer memory write-through at system scope.
-  __device__ __forceinline__ void put(uint64_t targetOffset, uint64_t originOffset, uint64_t bytes, uint32_t tid,
-                                      uint32_t nthreads) {
-    copySys(reinterpret_cast<char*>(dst_) + targetOffset, reinterpret_cast<const char*>(src_) + originOffset, bytes,
-            tid, nthreads, true);
+  // Threaded copy local -> peer (copy_device.hpp:34-128 semantics: 4-byte head, Alignment-sized
+  // body, 4-byte tail; offsets and sizes 4-byte aligned).  The peer side is written through at
+  // system scope, 16 bytes per lane where the alignment allows; each lane's stores have completed
+  // when put returns.
+  template <int Alignment = 16, bool CopyRemainder = true>
+  __device__ __forceinline__ void put(uint64_t targetOffset, uint64_t originOffset, uint64_t originBytes,
+                                     uint32_t threadId, uint32_t numThreads) {
+    copySys<Alignment, CopyRemainder, true>(reinterpret_cast<char*>(dst_) + targetOffset,
+                                            reinterpret_cast<const char*>(src_) + originOffset, originBytes,
+                                            threadId, numThreads);
   }
-  __device__ __forceinline__ void put(uint64_t offset, uint64_t bytes, uint32_t tid, uint32_t nthreads) {
-    put(offset, offset, bytes, tid, nthreads);
+  template <int Alignment = 16, bool CopyRemainder = true>
+  __device__ __forceinline__ void put(uint64_t offset, uint64_t originBytes, uint32_t threadId, uint32_t numThreads) {
+    put<Alignment, CopyRemainder>(offset, offset, originBytes, threadId, numThreads);
   }
-  __device__ __forceinline__ void get(uint64_t targetOffset, uint64_t originOffset, uint64_t bytes, uint32_t tid,
-                                      uint32_t nthreads) {
-    copySys(reinterpret_cast<char*>(src_) + targetOffset, reinterpret_cast<const char*>(dst_) + originOffset, bytes,
-            tid, nthreads, false);
+  // Threaded copy peer -> local (the peer side is read through at system scope).
+  template <int Alignment = 16, bool CopyRemainder = true>
+  __device__ __forceinline__ void get(uint64_t targetOffset, uint64_t originOffset, uint64_t originBytes,
+                                     uint32_t threadId, uint32_t numThreads) {
+    copySys<Alignment, CopyRemainder, false>(reinterpret_cast<char*>(src_) + targetOffset,
+                                             reinterpret_cast<const char*>(dst_) + originOffset, originBytes,
+                                             threadId, numThreads);
   }
-  __device__ __forceinline__ void get(uint64_t offset, uint64_t bytes, uint32_t tid, uint32_t nthreads) {
-    get(offset, offset, bytes, tid, nthreads);
+  template <int Alignment = 16, bool CopyRemainder = true>
+  __device__ __forceinline__ void get(uint64_t offset, uint64_t originBytes, uint32_t threadId, uint32_t numThreads) {
+    get<Alignment, CopyRemainder>(offset, offset, originBytes, threadId, numThreads);
   }
 
   // putPackets<LL16>: 8 payload bytes per packet; putPackets<LL8>: 4 (memory_channel_device.hpp:154-168)
   template <typename PacketType = LL16Packet>
-  __device__ __forceinline__ void putPackets(uint64_t targetOffset, uint64_t originOffset, uint64_t bytes,
-                                             uint32_t tid, uint32_t nthreads, uint32_t flag) {
+  __device__ __forceinline__ void putPackets(uint64_t targetOffset, uint64_t originOffset, uint64_t originBytes,
+                                             uint32_t threadId, uint32_t numThreads, uint32_t flag) {
+    static_assert(sizeof(PacketType) == 16 || sizeof(PacketType) == 8, "Unsupported packet type");
     char* dst = reinterpret_cast<char*>(dst_) + targetOffset;
     const uint32_t* s = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(src_) + originOffset);
+    const auto r = make_rsrc(dst);
     if constexpr (sizeof(PacketType) == 16) {
-      const auto r = make_rsrc(dst);
-      for (uint64_t i = tid; i < bytes / 8; i += nthreads)
+      for (uint64_t i = threadId; i < originBytes / 8; i += numThreads)
         store16<kSystem>(r, (uint32_t)(i * 16), LL16Packet::make(s[2 * i], s[2 * i + 1], flag));
     } else {
-      const auto r = make_rsrc(dst);
-      for (uint64_t i = tid; i < bytes / 4; i += nthreads) store8<kSystem>(r, (uint32_t)(i * 8), u32x2{s[i], flag});
+      for (uint64_t i = threadId; i < originBytes / 4; i += numThreads)
+        store8<kSystem>(r, (uint32_t)(i * 8), u32x2{s[i], flag});
     }
   }
   template <typename PacketType = LL16Packet>
-  __device__ __forceinline__ void putPackets(uint64_t offset, uint64_t bytes, uint32_t tid, uint32_t nthreads,
-                                             uint32_t flag) {
-    putPackets<PacketType>(offset, offset, bytes, tid, nthreads, flag);
+  __device__ __forceinline__ void putPackets(uint64_t offset, uint64_t originBytes, uint32_t threadId,
+                                             uint32_t numThreads, uint32_t flag) {
+    putPackets<PacketType>(offset, offset, originBytes, threadId, numThreads, flag);
   }
-  // unpackPackets: poll the local packet buffer, write the payload into local memory (:178-215)
+
+  // One packet of the local packet buffer (memory_channel_device.hpp:178-182): uint2 for LL16,
+  // uint32_t for LL8.
   template <typename PacketType = LL16Packet>
-  __device__ __forceinline__ void unpackPackets(uint64_t targetOffset, uint64_t originOffset, uint64_t bytes,
-                                                uint32_t tid, uint32_t nthreads, uint32_t flag) {
+  __device__ __forceinline__ auto unpackPacket(uint64_t index, uint32_t flag, int64_t maxSpinCount = -1) {
+    return reinterpret_cast<const PacketType*>(packetBuffer_)[index].read(flag, maxSpinCount);
+  }
+
+  // Poll the local packet buffer, write the payload into local memory (:198-215).  Each lane
+  // polls whole packets with one 16-byte (LL16) / 8-byte (LL8) system-scope load.
+  template <typename PacketType = LL16Packet>
+  __device__ __forceinline__ void unpackPackets(uint64_t targetOffset, uint64_t originOffset, uint64_t originBytes,
+                                                uint32_t threadId, uint32_t numThreads, uint32_t flag,
+                                                int64_t maxSpinCount = -1) {
+    static_assert(sizeof(PacketType) == 16 || sizeof(PacketType) == 8, "Unsupported packet type");
+    (void)maxSpinCount;
     uint32_t* d = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(src_) + originOffset);
     const char* pk = reinterpret_cast<const char*>(packetBuffer_) + targetOffset;
     const auto r = make_rsrc(pk);
+    const uint64_t budget = semaphore_.budget ? semaphore_.budget : kDefaultSpinTicks;
     if constexpr (sizeof(PacketType) == 16) {
-      for (uint64_t i = tid; i < bytes / 8; i += nthreads) {
+      for (uint64_t i = threadId; i < originBytes / 8; i += numThreads) {
         u32x4 v = load16<kSystem>(r, (uint32_t)(i * 16));
         if (!LL16Packet::ready(v, flag)) {
-          SpinGuard g(budget_);
+          SpinGuard g(budget);
           do {
             v = load16<kSystem>(r, (uint32_t)(i * 16));
             if (g.expired()) {
-              report_error(err_, kErrPacketTimeout);
+              report_error(semaphore_.err, kErrPacketTimeout);
               break;
             }
           } while (!LL16Packet::ready(v, flag));
@@ -141,14 +143,14 @@ struct MemoryChannelDeviceHandle {
         d[2 * i + 1] = v.z;
       }
     } else {
-      for (uint64_t i = tid; i < bytes / 4; i += nthreads) {
+      for (uint64_t i = threadId; i < originBytes / 4; i += numThreads) {
         u32x2 v = load8<kSystem>(r, (uint32_t)(i * 8));
         if (v.y != flag) {
-          SpinGuard g(budget_);
+          SpinGuard g(budget);
           do {
             v = load8<kSystem>(r, (uint32_t)(i * 8));
             if (g.expired()) {
-              report_error(err_, kErrPacketTimeout);
+              report_error(semaphore_.err, kErrPacketTimeout);
               break;
             }
           } while (v.y != flag);
@@ -158,37 +160,65 @@ struct MemoryChannelDeviceHandle {
     }
   }
   template <typename PacketType = LL16Packet>
-  __device__ __forceinline__ void unpackPackets(uint64_t offset, uint64_t bytes, uint32_t tid, uint32_t nthreads,
-                                                uint32_t flag) {
-    unpackPackets<PacketType>(offset, offset, bytes, tid, nthreads, flag);
+  __device__ __forceinline__ void unpackPackets(uint64_t offset, uint64_t originBytes, uint32_t threadId,
+                                                uint32_t numThreads, uint32_t flag, int64_t maxSpinCount = -1) {
+    unpackPackets<PacketType>(offset, offset, originBytes, threadId, numThreads, flag, maxSpinCount);
   }
 
-  __device__ __forceinline__ void signal() { semaphore_.signal(); }
-  __device__ __forceinline__ void relaxedSignal() { semaphore_.relaxedSignal(); }
-  __device__ __forceinline__ bool poll() { return semaphore_.poll(); }
-  __device__ __forceinline__ void wait() { semaphore_.wait(budget_, err_); }
-  __device__ __forceinline__ void relaxedWait() { semaphore_.relaxedWait(budget_, err_); }
-
  private:
+  // Threaded copy with the remote side at system scope: 4-byte head to the first Alignment boundary
+  // of dst, Alignment-sized body (16 B: one dwordx4 per lane), 4-byte tail.
+  template <int Alignment, bool CopyRemainder, bool RemoteDst>
   __device__ __forceinline__ static void copySys(char* dst, const char* src, uint64_t bytes, uint32_t tid,
-                                                 uint32_t nthreads, bool remoteDst) {
-    const auto rd = make_rsrc(dst);
-    const auto rs = make_rsrc(src);
-    const uint64_t n16 = bytes / 16;
-    for (uint64_t i = tid; i < n16; i += nthreads) {
-      const u32x4 v = remoteDst ? load16<kPlain>(rs, (uint32_t)(i * 16)) : load16<kSystem>(rs, (uint32_t)(i * 16));
-      if (remoteDst)
-        store16<kSystem>(rd, (uint32_t)(i * 16), v);
-      else
-        store16<kPlain>(rd, (uint32_t)(i * 16), v);
+                                                 uint32_t nthreads) {
+    static_assert(Alignment == 4 || Alignment == 8 || Alignment == 16, "Unsupported alignment");
+    constexpr int kRemote = kSystem, kLocal = kPlain;
+    const uint64_t numInt = bytes / 4;
+    const uintptr_t d = reinterpret_cast<uintptr_t>(dst);
+    uint64_t head = ((d + Alignment - 1) / Alignment * Alignment - d) / 4;
+    if (head > numInt) head = numInt;
+    auto copy4 = [&](uint64_t from, uint64_t n) {
+      const auto rd = make_rsrc(dst + from * 4);
+      const auto rs = make_rsrc(src + from * 4);
+      for (uint64_t i = tid; i < n; i += nthreads) {
+        const uint32_t v = RemoteDst ? load4<kLocal>(rs, (uint32_t)(i * 4)) : load4<kRemote>(rs, (uint32_t)(i * 4));
+        if (RemoteDst)
+          store4<kRemote>(rd, (uint32_t)(i * 4), v);
+        else
+          store4<kLocal>(rd, (uint32_t)(i * 4), v);
+      }
+    };
+    if (CopyRemainder) copy4(0, head);
+    constexpr uint64_t kIntPer = Alignment / 4;
+    const uint64_t nElem = (numInt - head) / kIntPer;
+    const auto rd = make_rsrc(dst + head * 4);
+    const auto rs = make_rsrc(src + head * 4);
+    for (uint64_t i = tid; i < nElem; i += nthreads) {
+      const uint32_t off = (uint32_t)(i * Alignment);
+      if constexpr (Alignment == 16) {
+        const u32x4 v = RemoteDst ? load16<kLocal>(rs, off) : load16<kRemote>(rs, off);
+        if (RemoteDst)
+          store16<kRemote>(rd, off, v);
+        else
+          store16<kLocal>(rd, off, v);
+      } else if constexpr (Alignment == 8) {
+        const u32x2 v = RemoteDst ? load8<kLocal>(rs, off) : load8<kRemote>(rs, off);
+        if (RemoteDst)
+          store8<kRemote>(rd, off, v);
+        else
+          store8<kLocal>(rd, off, v);
+      } else {
+        const uint32_t v = RemoteDst ? load4<kLocal>(rs, off) : load4<kRemote>(rs, off);
+        if (RemoteDst)
+          store4<kRemote>(rd, off, v);
+        else
+          store4<kLocal>(rd, off, v);
+      }
     }
-    for (uint64_t i = n16 * 4 + tid; i < bytes / 4; i += nthreads) {
-      const uint32_t v = remoteDst ? load4<kPlain>(rs, (uint32_t)(i * 4)) : load4<kSystem>(rs, (uint32_t)(i * 4));
-      if (remoteDst)
-        store4<kSystem>(rd, (uint32_t)(i * 4), v);
-      else
-        store4<kPlain>(rd, (uint32_t)(i * 4), v);
-    }
+    if (CopyRemainder && kIntPer > 1) copy4(head + nElem * kIntPer, numInt - head - nElem * kIntPer);
+    // this lane's copies are complete when it returns, so a workgroup barrier followed by one
+    // lane's signal() publishes the whole workgroup's put (or its get's data to the other waves)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 #endif
 };

@@ -153,6 +153,11 @@ int mscclppAmdCommRegisterBuffer(ncclComm_t comm, void* ptr, void** peers);
  * when buffers that were used with the communicator are freed. */
 int mscclppAmdCommDeregisterAll(ncclComm_t comm);
 int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear);
+/* Registration cache state: user buffers registered (at most 64, least recently used retired
+ * beyond), IPC mappings open in this process (all communicators), mappings waiting for a device
+ * synchronize before they close.  Any pointer may be NULL. */
+int mscclppAmdCommRegistrationStats(ncclComm_t comm, size_t* userRegistrations, size_t* liveMappings,
+                                    size_t* retiredMappings);
 int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes);
 int mscclppAmdCommFlags(ncclComm_t comm, uint32_t** flags);
 /* Bootstrap all-gather of `bytes` per rank (host memory), for harnesses. */

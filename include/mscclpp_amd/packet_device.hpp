@@ -27,6 +27,11 @@ union alignas(16) LL16Packet {
   };
   u32x4 raw;
 
+  using Payload = uint2;  // packet_device.hpp:27
+
+  LL16Packet() = default;
+  __device__ __forceinline__ LL16Packet(uint2 val, uint32_t flag) : raw(make(val.x, val.y, flag)) {}
+
   __device__ __forceinline__ static u32x4 make(uint32_t v1, uint32_t v2, uint32_t flag) {
     u32x4 p;
     p.x = v1;
@@ -37,19 +42,30 @@ union alignas(16) LL16Packet {
   }
   __device__ __forceinline__ static bool ready(u32x4 p, uint32_t flag) { return p.y == flag && p.w == flag; }
 
-  // Single-packet write through a raw pointer (system scope, write-through).  Hot loops use the
-  // buffer-resource forms in PacketStream instead.
+  // Single-packet write through a raw pointer (system scope, write-through: one 16-byte store whose
+  // two 8-byte halves each carry the flag).  Hot loops use the buffer-resource forms below.
   __device__ __forceinline__ void write(uint32_t v1, uint32_t v2, uint32_t flag) {
     u32x4 p = make(v1, v2, flag);
     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(&raw), "v"(p) : "memory");
   }
-  // One poll: two relaxed system-scope 8-byte loads, as LL16Packet::readOnce.
+  __device__ __forceinline__ void write(uint64_t val, uint32_t flag) { write((uint32_t)val, (uint32_t)(val >> 32), flag); }
+  __device__ __forceinline__ void write(uint2 val, uint32_t flag) { write(val.x, val.y, flag); }
+
+  // One poll: two relaxed system-scope 8-byte loads.  Returns true when both flags match.
   __device__ __forceinline__ bool readOnce(uint32_t flag, uint32_t& v1, uint32_t& v2) const {
     const uint64_t* q = reinterpret_cast<const uint64_t*>(this);
     uint64_t lo = ld_relaxed_sys(q), hi = ld_relaxed_sys(q + 1);
     v1 = (uint32_t)lo;
     v2 = (uint32_t)hi;
     return (uint32_t)(lo >> 32) == flag && (uint32_t)(hi >> 32) == flag;
+  }
+  // The reference's helper of read() (packet_device.hpp:66-82): true while the flags do NOT match.
+  __device__ __forceinline__ bool readOnce(uint32_t flag, uint2& data) const {
+    uint32_t v1, v2;
+    const bool ok = readOnce(flag, v1, v2);
+    data.x = v1;
+    data.y = v2;
+    return !ok;
   }
   // Spin until both flags match; on timeout record kErrPacketTimeout and return zeros.
   __device__ __forceinline__ bool read(uint32_t flag, uint32_t& v1, uint32_t& v2, uint64_t budget,
@@ -64,6 +80,21 @@ union alignas(16) LL16Packet {
     }
     return true;
   }
+  // The reference's read (packet_device.hpp:88-92): the payload once both flags match.  Bounded by
+  // kDefaultSpinTicks of wall clock (maxSpinCount: see device.hpp); after a timeout it returns the
+  // last payload seen.
+  __device__ __forceinline__ uint2 read(uint32_t flag, int64_t maxSpinCount = 100000000) const {
+    (void)maxSpinCount;
+    uint32_t v1, v2;
+    SpinGuard g(kDefaultSpinTicks);
+    while (!readOnce(flag, v1, v2) && !g.expired()) {
+    }
+    uint2 d;
+    d.x = v1;
+    d.y = v2;
+    return d;
+  }
+  __device__ __forceinline__ void clear() { raw = u32x4{0, 0, 0, 0}; }
 };
 
 union alignas(8) LL8Packet {
@@ -73,18 +104,25 @@ union alignas(8) LL8Packet {
   };
   uint64_t raw;
 
+  using Payload = uint32_t;  // packet_device.hpp:108
+
+  LL8Packet() = default;
+  __device__ __forceinline__ LL8Packet(uint32_t val, uint32_t f) : raw(make(val, f)) {}
+
   __device__ __forceinline__ static uint64_t make(uint32_t v, uint32_t flag) { return ((uint64_t)flag << 32) | v; }
+  // One relaxed system-scope 8-byte store (packet_device.hpp:118-126).
   __device__ __forceinline__ void write(uint32_t v, uint32_t flag) {
     __hip_atomic_store(&raw, make(v, flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __device__ __forceinline__ bool readOnce(uint32_t flag, uint32_t& v) const {
+  // The reference's helper of read() (packet_device.hpp:132-144): true while the flag does NOT match.
+  __device__ __forceinline__ bool readOnce(uint32_t flag, uint32_t& data) const {
     uint64_t x = ld_relaxed_sys(&raw);
-    v = (uint32_t)x;
-    return (uint32_t)(x >> 32) == flag;
+    data = (uint32_t)x;
+    return (uint32_t)(x >> 32) != flag;
   }
   __device__ __forceinline__ bool read(uint32_t flag, uint32_t& v, uint64_t budget, uint32_t* err) const {
     SpinGuard g(budget);
-    while (!readOnce(flag, v)) {
+    while (readOnce(flag, v)) {
       if (g.expired()) {
         report_error(err, kErrPacketTimeout);
         v = 0;
@@ -93,7 +131,19 @@ union alignas(8) LL8Packet {
     }
     return true;
   }
+  // The reference's read (packet_device.hpp:150-154), bounded by kDefaultSpinTicks of wall clock.
+  __device__ __forceinline__ uint32_t read(uint32_t flag, int64_t maxSpinCount = 1000000) const {
+    (void)maxSpinCount;
+    uint32_t v;
+    SpinGuard g(kDefaultSpinTicks);
+    while (readOnce(flag, v) && !g.expired()) {
+    }
+    return v;
+  }
+  __device__ __forceinline__ void clear() { raw = 0; }
 };
+
+using LLPacket = LL16Packet;  // packet_device.hpp:161
 
 // ---------------------------------------------------------------------------------------------
 // Packet streams: the hot-loop forms.  A "unit" is 16 payload bytes = 2 LL16 packets (32 B) or
@@ -173,8 +223,9 @@ __device__ __forceinline__ u32x4 ll8_get_unit(__amdgpu_buffer_rsrc_t pkts, uint3
   return w;
 }
 
-// Reference-shaped threaded helpers (copy_device.hpp:156-232): thread `tid` of `nthreads`
-// handles packets tid, tid + nthreads, ...  Kept for API parity; the kernels use the unit forms.
+// Threaded helpers with an explicit spin budget and error word (the budget/error-word overloads of
+// copyToPackets / copyFromPackets, copy_device.hpp:156-232; the reference-spelled templates are in
+// copy_device.hpp): thread `tid` of `nthreads` handles packets tid, tid + nthreads, ...
 __device__ __forceinline__ void copyToPacketsLL16(void* dst, const void* src, uint64_t bytes, uint32_t tid,
                                                   uint32_t nthreads, uint32_t flag) {
   const uint32_t* s = reinterpret_cast<const uint32_t*>(src);

@@ -1,0 +1,48 @@
+// The proxy thread (include/mscclpp/proxy.hpp, src/core/proxy.cc:42-100): one host thread per
+// Proxy, bound to the CPUs of the GPU's NUMA node (proxy.cc:23-33), busy-polling the FIFO and
+// handing every trigger to a handler; the trigger is popped after the handler returns.
+#ifndef MSCCLPP_AMD_PROXY_HPP_
+#define MSCCLPP_AMD_PROXY_HPP_
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <thread>
+
+#include "mscclpp_amd/fifo.hpp"
+
+namespace mscclpp_amd {
+
+enum class ProxyHandlerResult { Continue, Stop };  // proxy.hpp:16-19
+
+class Proxy {
+ public:
+  // handler(trigger, fifoPosition): the position is what the device's push() returned
+  using Handler = std::function<ProxyHandlerResult(ProxyTrigger, uint64_t)>;
+  Proxy(Handler handler, int fifoSize = DEFAULT_FIFO_SIZE);
+  ~Proxy();
+  Proxy(const Proxy&) = delete;
+  Proxy& operator=(const Proxy&) = delete;
+  void start(bool blocking = true);  // blocking: return once the thread runs
+  void stop();
+  Fifo& fifo() { return fifo_; }
+  int numaNode() const { return numaNode_; }
+
+ private:
+  int device_ = 0;
+  Fifo fifo_;
+  Handler handler_;
+  std::thread thread_;
+  std::atomic<bool> running_{false};
+  std::atomic<bool> started_{false};
+  std::atomic<int> numaNode_{-1};
+};
+
+// The NUMA node of a GPU (sysfs of its PCI device), -1 if unknown; numaBind pins the calling
+// thread to that node's CPUs and returns the node, or -1.
+int getDeviceNumaNode(int device);
+int numaBind(int node);
+
+}  // namespace mscclpp_amd
+
+#endif  // MSCCLPP_AMD_PROXY_HPP_

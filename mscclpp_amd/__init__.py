@@ -125,6 +125,7 @@ def lib():
         "mscclppAmdCommBarrier": [vp],
         "mscclppAmdCommGetDeviceError": [vp, ctypes.POINTER(ctypes.c_uint32), i32],
         "mscclppAmdCommScratch": [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)],
+        "mscclppAmdCommRegistrationStats": [vp, ctypes.POINTER(sz), ctypes.POINTER(sz), ctypes.POINTER(sz)],
         "mscclppAmdCommFlags": [vp, ctypes.POINTER(vp)],
         "mscclppAmdCommAllGatherHost": [vp, vp, vp, sz],
         "mscclppAmdProxyRingAllReduce": [vp, sz, i32, i32, i32, ctypes.POINTER(ctypes.c_double)],
@@ -414,6 +415,13 @@ class Communicator:
         c = ctypes.c_uint32()
         check(lib().mscclppAmdCommGetDeviceError(self.comm, ctypes.byref(c), 1 if clear else 0), "device error")
         return c.value
+
+    def registration_stats(self):
+        """(user buffers registered, IPC mappings open in this process, mappings awaiting close)."""
+        a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib().mscclppAmdCommRegistrationStats(self.comm, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+              "registration stats")
+        return a.value, b.value, c.value
 
     def destroy(self):
         if self.comm:

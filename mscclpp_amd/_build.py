@@ -100,12 +100,22 @@ def build_tests():
     os.makedirs(TESTBIN, exist_ok=True)
     hdrs = _headers()
     outs = []
-    for src in sorted(glob.glob(os.path.join(ROOT, "tests", "cpp", "*.cpp"))):
+    srcs = sorted(glob.glob(os.path.join(ROOT, "tests", "cpp", "*.cpp")) +
+                  glob.glob(os.path.join(ROOT, "tests", "cpp", "*.hip")))
+
+    def one(src):
         exe = os.path.join(TESTBIN, os.path.splitext(os.path.basename(src))[0])
         if _newer(exe, [src, LIB] + hdrs):
-            _run([HIPCC, "-D__HIP_PLATFORM_AMD__", "-O2", "-std=c++17", "-Wall", "-I" + INCLUDE, src, "-o", exe,
-                  "-L" + LIBDIR, "-lmscclpp_amd", "-Wl,-rpath,$ORIGIN/../../mscclpp_amd/lib"])
-        outs.append(exe)
+            # .hip: test programs with device code of their own (kernels written against the
+            # public device headers), compiled for gfx950
+            lang = ["--offload-arch=" + ARCH, "-x", "hip"] if src.endswith(".hip") else ["-D__HIP_PLATFORM_AMD__"]
+            _run([HIPCC] + lang + ["-O2", "-std=c++17", "-Wall", "-Wno-unused-variable", "-Wno-unused-parameter",
+                                   "-I" + INCLUDE, src, "-o", exe, "-L" + LIBDIR, "-lmscclpp_amd",
+                                   "-Wl,-rpath,$ORIGIN/../../mscclpp_amd/lib"])
+        return exe
+
+    with cf.ThreadPoolExecutor(max_workers=4) as ex:
+        outs = list(ex.map(one, srcs))
     return outs
 
 

@@ -56,31 +56,6 @@ static CommResult asResult(int code) {
   return (code >= 0 && code < (int)CommResult::CommNumResults) ? (CommResult)code : CommResult::CommInternalError;
 }
 
-// ---- Communicator -----------------------------------------------------------------------------
-int Communicator::rank() const { return comm_->rank; }
-int Communicator::nRanks() const { return comm_->nranks; }
-int Communicator::nRanksPerNode() const { return comm_->nranks; }
-int Communicator::device() const { return comm_->device; }
-
-std::vector<void*> Communicator::registerMemory(void* ptr) {
-  if (!ptr) throw std::invalid_argument("registerMemory: null pointer");
-  std::vector<void*> res((size_t)comm_->nranks, nullptr);
-  if (comm_->nranks == 1) {
-    res[0] = ptr;
-    return res;
-  }
-  std::lock_guard<std::mutex> lk(comm_->mu);
-  auto peers = comm_->registerOutput(ptr);  // collective IPC exchange, cached per allocation
-  for (int r = 0; r < comm_->nranks; ++r) res[(size_t)r] = peers[(size_t)r];
-  return res;
-}
-
-void Communicator::allGather(const void* sendbuf, void* recvbuf, size_t bytesPerRank) {
-  comm_->boot->allGather(sendbuf, recvbuf, bytesPerRank);
-}
-
-void Communicator::barrier() { comm_->boot->barrier(); }
-
 // ---- ExecutionPlan / Executor (C ABI wrappers) ------------------------------------------------
 ExecutionPlan::ExecutionPlan(const std::string& planPath, int rank) {
   if (mscclppAmdExecutionPlanCreate(planPath.c_str(), rank, &plan_) != 0)

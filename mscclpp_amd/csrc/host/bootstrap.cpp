@@ -60,7 +60,19 @@ void setTimeouts(int fd, int sec) {
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
 }
 
-// Root: accept nranks ranks, then relay all-gather rounds until a rank disconnects.
+// Wire header of every message after the hello, in both directions.
+//   rank -> root: kind 1 = all-gather contribution (peer unused); kind 2 = send to `peer` with `tag`
+//   root -> rank: kind 1 = all-gather result (n contributions); kind 2 = delivery from `peer`
+struct MsgHeader {
+  uint32_t kind;
+  int32_t peer;
+  int64_t tag;
+  uint64_t len;
+};
+constexpr uint32_t kMsgAllGather = 1, kMsgP2P = 2;
+
+// Root: accept nranks ranks, then serve messages until a rank disconnects: all-gather rounds
+// complete when every rank has contributed (in order), point-to-point messages are forwarded at once.
 void rootLoop(int lfd, uint64_t nonce) {
   std::vector<int> fds;
   int nranks = -1;
@@ -98,20 +110,44 @@ void rootLoop(int lfd, uint64_t nonce) {
     ::close(lfd);
     lfd = -1;
     for (int fd : fds) setTimeouts(fd, 0);  // relay phase: ranks may stay idle indefinitely
-    // rounds: every rank sends {u64 len, data}; root replies with the concatenation
-    std::vector<char> buf;
+    std::vector<std::deque<std::vector<char>>> pending(nranks);  // all-gather contributions per rank
+    std::vector<pollfd> pfs(nranks);
     for (;;) {
-      uint64_t len = 0;
-      recvAll(fds[0], &len, sizeof(len));
-      buf.resize(len * fds.size());
-      recvAll(fds[0], buf.data(), len);
-      for (size_t r = 1; r < fds.size(); ++r) {
-        uint64_t l2 = 0;
-        recvAll(fds[r], &l2, sizeof(l2));
-        if (l2 != len) throw std::runtime_error("bootstrap root: mismatched round sizes");
-        recvAll(fds[r], buf.data() + r * len, len);
+      for (int r = 0; r < nranks; ++r) pfs[r] = pollfd{fds[r], POLLIN, 0};
+      if (::poll(pfs.data(), pfs.size(), -1) < 0) {
+        if (errno == EINTR) continue;
+        throw std::runtime_error("bootstrap root: poll failed");
       }
-      for (size_t r = 0; r < fds.size(); ++r) sendAll(fds[r], buf.data(), buf.size());
+      for (int r = 0; r < nranks; ++r) {
+        if (!(pfs[r].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+        MsgHeader h{};
+        recvAll(fds[r], &h, sizeof(h));  // throws when the rank has gone: the root ends
+        std::vector<char> body(h.len);
+        if (h.len) recvAll(fds[r], body.data(), h.len);
+        if (h.kind == kMsgP2P) {
+          if (h.peer < 0 || h.peer >= nranks) throw std::runtime_error("bootstrap root: bad destination");
+          MsgHeader out{kMsgP2P, r, h.tag, h.len};
+          sendAll(fds[h.peer], &out, sizeof(out));
+          if (h.len) sendAll(fds[h.peer], body.data(), h.len);
+        } else {
+          pending[r].push_back(std::move(body));
+        }
+      }
+      bool ready = true;
+      for (int r = 0; r < nranks; ++r) ready = ready && !pending[r].empty();
+      if (!ready) continue;
+      const uint64_t len = pending[0].front().size();
+      std::vector<char> all(len * nranks);
+      for (int r = 0; r < nranks; ++r) {
+        if (pending[r].front().size() != len) throw std::runtime_error("bootstrap root: mismatched round sizes");
+        if (len) std::memcpy(all.data() + r * len, pending[r].front().data(), len);
+        pending[r].pop_front();
+      }
+      MsgHeader out{kMsgAllGather, -1, 0, (uint64_t)all.size()};
+      for (int r = 0; r < nranks; ++r) {
+        sendAll(fds[r], &out, sizeof(out));
+        if (!all.empty()) sendAll(fds[r], all.data(), all.size());
+      }
     }
   } catch (...) {
   }
@@ -152,7 +188,7 @@ BootstrapId bootstrapCreateRoot() {
 
 bool bootstrapIdValid(const BootstrapId& id) { return std::memcmp(id.magic, "MSCAMD1", 8) == 0; }
 
-Bootstrap::Bootstrap(int rank, int nranks, const BootstrapId& id, int timeoutSec)
+TcpBootstrap::TcpBootstrap(int rank, int nranks, const BootstrapId& id, int timeoutSec)
     : rank_(rank), nranks_(nranks), fd_(-1) {
   sockaddr_in sa{};
   sa.sin_family = AF_INET;
@@ -172,24 +208,68 @@ Bootstrap::Bootstrap(int rank, int nranks, const BootstrapId& id, int timeoutSec
   sendAll(fd_, &h, sizeof(h));
 }
 
-Bootstrap::~Bootstrap() {
+TcpBootstrap::~TcpBootstrap() {
   if (fd_ >= 0) ::close(fd_);
 }
 
-void Bootstrap::allGather(const void* send, void* recv, size_t bytes) {
-  uint64_t len = bytes;
-  sendAll(fd_, &len, sizeof(len));
-  if (bytes) sendAll(fd_, send, bytes);
-  if (bytes * nranks_) recvAll(fd_, recv, bytes * nranks_);
+bool TcpBootstrap::readOne(void* agOut, size_t agBytes) {
+  MsgHeader h{};
+  recvAll(fd_, &h, sizeof(h));
+  if (h.kind == kMsgAllGather) {
+    if (h.len != agBytes) throw std::runtime_error("bootstrap: unexpected all-gather result");
+    if (agBytes) recvAll(fd_, agOut, agBytes);
+    return true;
+  }
+  std::vector<char> body(h.len);
+  if (h.len) recvAll(fd_, body.data(), h.len);
+  mailbox_[{h.peer, (int)h.tag}].push_back(std::move(body));
+  return false;
 }
 
-void Bootstrap::barrier() {
+void TcpBootstrap::allGather(const void* send, void* recv, size_t bytes) {
+  std::lock_guard<std::mutex> lk(mu_);
+  MsgHeader h{kMsgAllGather, -1, 0, (uint64_t)bytes};
+  sendAll(fd_, &h, sizeof(h));
+  if (bytes) sendAll(fd_, send, bytes);
+  while (!readOne(recv, bytes * nranks_)) {
+  }
+}
+
+void TcpBootstrap::send(const void* data, size_t bytes, int peer, int tag) {
+  if (peer < 0 || peer >= nranks_) throw std::invalid_argument("bootstrap send: bad peer");
+  std::lock_guard<std::mutex> lk(mu_);
+  MsgHeader h{kMsgP2P, peer, tag, (uint64_t)bytes};
+  sendAll(fd_, &h, sizeof(h));
+  if (bytes) sendAll(fd_, data, bytes);
+}
+
+void TcpBootstrap::recv(void* data, size_t bytes, int peer, int tag) {
+  if (peer < 0 || peer >= nranks_) throw std::invalid_argument("bootstrap recv: bad peer");
+  std::lock_guard<std::mutex> lk(mu_);
+  const auto key = std::make_pair(peer, tag);
+  for (;;) {
+    auto it = mailbox_.find(key);
+    if (it != mailbox_.end() && !it->second.empty()) {
+      std::vector<char> m = std::move(it->second.front());
+      it->second.pop_front();
+      if (m.size() != bytes)
+        throw std::runtime_error("bootstrap recv: message from rank " + std::to_string(peer) + " tag " +
+                                 std::to_string(tag) + " has " + std::to_string(m.size()) + " bytes, expected " +
+                                 std::to_string(bytes));
+      if (bytes) std::memcpy(data, m.data(), bytes);
+      return;
+    }
+    if (readOne(nullptr, 0)) throw std::runtime_error("bootstrap recv: all-gather result while receiving");
+  }
+}
+
+void TcpBootstrap::barrier() {
   char dummy = 0;
   std::vector<char> all(nranks_);
   allGather(&dummy, all.data(), 1);
 }
 
-void Bootstrap::broadcast(void* buf, size_t bytes, int root) {
+void TcpBootstrap::broadcast(void* buf, size_t bytes, int root) {
   std::vector<char> all(bytes * nranks_);
   allGather(buf, all.data(), bytes);
   std::memcpy(buf, all.data() + (size_t)root * bytes, bytes);

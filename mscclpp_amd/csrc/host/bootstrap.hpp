@@ -3,12 +3,17 @@
 // Replaces the reference's TcpBootstrap (src/core/bootstrap/bootstrap.cc:169-611): same job --
 // a 128-byte unique id names a rendezvous point, ranks exchange small blobs through it -- but a
 // simpler shape for the single-node scope: the process that creates the id runs a root thread
-// that every rank connects to (a star), and all collective exchanges (all-gather, barrier,
-// broadcast) are rounds relayed by that thread.
+// that every rank connects to (a star).  Collective exchanges (all-gather, barrier, broadcast) are
+// rounds relayed by that thread; point-to-point messages (send / recv matched by source and tag,
+// bootstrap.cc:537-560) are forwarded by it to their destination, where they wait in a mailbox until
+// received.
 #pragma once
 
 #include <cstddef>
 #include <cstdint>
+#include <deque>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -28,12 +33,12 @@ static_assert(sizeof(BootstrapId) == 128, "unique id must be 128 bytes (nccl.h:2
 BootstrapId bootstrapCreateRoot();
 bool bootstrapIdValid(const BootstrapId& id);
 
-class Bootstrap {
+class TcpBootstrap {
  public:
-  Bootstrap(int rank, int nranks, const BootstrapId& id, int timeoutSec);
-  ~Bootstrap();
-  Bootstrap(const Bootstrap&) = delete;
-  Bootstrap& operator=(const Bootstrap&) = delete;
+  TcpBootstrap(int rank, int nranks, const BootstrapId& id, int timeoutSec);
+  ~TcpBootstrap();
+  TcpBootstrap(const TcpBootstrap&) = delete;
+  TcpBootstrap& operator=(const TcpBootstrap&) = delete;
 
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }
@@ -41,11 +46,20 @@ class Bootstrap {
   void allGather(const void* send, void* recv, size_t bytes);
   void barrier();
   void broadcast(void* buf, size_t bytes, int root);
+  // Point-to-point: send never waits for the receiver; recv returns the oldest message from `peer`
+  // with `tag` (throws if its size differs from `bytes`).
+  void send(const void* data, size_t bytes, int peer, int tag);
+  void recv(void* data, size_t bytes, int peer, int tag);
 
  private:
+  // Read one message from the root; point-to-point deliveries go to the mailbox.  Returns true
+  // for an all-gather result (copied to agOut).
+  bool readOne(void* agOut, size_t agBytes);
   int rank_;
   int nranks_;
   int fd_;
+  std::mutex mu_;
+  std::map<std::pair<int, int>, std::deque<std::vector<char>>> mailbox_;
 };
 
 }  // namespace mscclpp_amd

@@ -185,7 +185,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
     HIPCHECK(hipGetDevice(&c->device));
     const char* to = std::getenv("MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S");
     info("rank " + std::to_string(rank) + ": bootstrap connect");
-    c->boot = std::make_unique<Bootstrap>(rank, nranks, id, to ? std::atoi(to) : 600);
+    c->boot = std::make_unique<TcpBootstrap>(rank, nranks, id, to ? std::atoi(to) : 600);
     info("rank " + std::to_string(rank) + ": bootstrap connected");
     const size_t tokBytes = sizeof(uint64_t) * MSCCLPP_AMD_MAX_RANKS * MSCCLPP_AMD_MAX_CHANNELS;
     c->tokens = (uint64_t*)allocUncached(tokBytes);
@@ -200,9 +200,9 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
     HIPCHECK(hipMemset(c->err, 0, 256));
     if (nranks > 1) {
       info("rank " + std::to_string(rank) + ": exchanging semaphore tokens");
-      auto toks = c->exchange(c->tokens);
+      c->peerTok = c->exchange(c->tokens);
       info("rank " + std::to_string(rank) + ": tokens mapped; allocating LL scratch");
-      for (int r = 0; r < nranks; ++r) c->peerTokens[r] = (uint64_t*)toks[r];
+      for (int r = 0; r < nranks; ++r) c->peerTokens[r] = (uint64_t*)c->peerTok[r];
       c->ensure(c->llScratch, c->llBytes, c->peerLL, (size_t)64 << 20);
     }
     c->buildAlgorithms();
@@ -468,6 +468,16 @@ int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear) {
   });
 }
 
+int mscclppAmdCommRegistrationStats(ncclComm_t comm, size_t* userRegistrations, size_t* liveMappings,
+                                    size_t* retiredMappings) {
+  if (!comm) return ncclInvalidArgument;
+  std::lock_guard<std::mutex> lk(comm->mu);
+  if (userRegistrations) *userRegistrations = comm->userRegs.size();
+  if (liveMappings) *liveMappings = liveIpcMappings();
+  if (retiredMappings) *retiredMappings = comm->retired.size();
+  return ncclSuccess;
+}
+
 int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes) {
   if (!comm || !scratch || !bytes) return ncclInvalidArgument;
   *scratch = comm->llScratch;
@@ -496,7 +506,7 @@ int mscclppAmdBootstrapCreate(int rank, int nranks, const void* uniqueId, void**
     BootstrapId id;
     std::memcpy(&id, uniqueId, sizeof(id));
     if (!bootstrapIdValid(id)) return (int)ncclInvalidArgument;
-    *handle = new Bootstrap(rank, nranks, id, 120);
+    *handle = new TcpBootstrap(rank, nranks, id, 120);
     return (int)ncclSuccess;
   });
 }
@@ -504,7 +514,7 @@ int mscclppAmdBootstrapCreate(int rank, int nranks, const void* uniqueId, void**
 int mscclppAmdBootstrapAllGather(void* handle, const void* sendbuf, void* recvbuf, size_t bytes) {
   return guarded([&] {
     if (!handle) return (int)ncclInvalidArgument;
-    static_cast<Bootstrap*>(handle)->allGather(sendbuf, recvbuf, bytes);
+    static_cast<TcpBootstrap*>(handle)->allGather(sendbuf, recvbuf, bytes);
     return (int)ncclSuccess;
   });
 }
@@ -512,13 +522,13 @@ int mscclppAmdBootstrapAllGather(void* handle, const void* sendbuf, void* recvbu
 int mscclppAmdBootstrapBarrier(void* handle) {
   return guarded([&] {
     if (!handle) return (int)ncclInvalidArgument;
-    static_cast<Bootstrap*>(handle)->barrier();
+    static_cast<TcpBootstrap*>(handle)->barrier();
     return (int)ncclSuccess;
   });
 }
 
 int mscclppAmdBootstrapDestroy(void* handle) {
-  delete static_cast<Bootstrap*>(handle);
+  delete static_cast<TcpBootstrap*>(handle);
   return ncclSuccess;
 }
 

@@ -177,6 +177,26 @@ inline int envAlgo() {
 using namespace mscclpp_amd;
 using namespace mscclpp_amd::host;
 
+namespace mscclpp_amd {
+namespace host {
+// Process-wide cache of opened IPC handles (gpu_ipc_mem.cc:193-223 keeps one for HIP too): a handle
+// is opened once per process however many owners hold it, and closed when the last owner drops
+// its reference.  Implemented in core.cpp.
+std::shared_ptr<void> openIpcHandle(const hipIpcMemHandle_t& handle);
+size_t liveIpcMappings();
+uint64_t allocationId(const void* ptr);  // HIP_POINTER_ATTRIBUTE_BUFFER_ID (0 if unknown)
+}  // namespace host
+}  // namespace mscclpp_amd
+
+// Every rank's buffer as mapped in this process, plus the references that keep the peers' mappings
+// open (entry [rank] is the local pointer and holds no reference).
+struct PeerBufs {
+  std::array<void*, MSCCLPP_AMD_MAX_RANKS> ptr{};
+  std::array<std::shared_ptr<void>, MSCCLPP_AMD_MAX_RANKS> maps{};
+  void*& operator[](int r) { return ptr[(size_t)r]; }
+  void* operator[](int r) const { return ptr[(size_t)r]; }
+};
+
 struct IpcBlob {
   hipIpcMemHandle_t handle;
   uint64_t base;    // allocation base in the owner's address space (cache key)
@@ -185,7 +205,7 @@ struct IpcBlob {
 };
 
 struct ncclComm {
-  std::unique_ptr<Bootstrap> boot;
+  std::unique_ptr<TcpBootstrap> boot;
   // the C++ plugin layer (algorithm.cpp): handle passed to Algorithm::execute, the collection the
   // NCCL entry points select from (nccl.cc:176, :308-314) and the executor for DSL algorithms,
   // created on the first DSL selection (collective: every rank selects the same algorithm)
@@ -208,25 +228,18 @@ struct ncclComm {
   uint64_t* expected = nullptr;
   uint32_t* flags = nullptr;
   uint32_t* err = nullptr;
-  std::array<void*, MSCCLPP_AMD_MAX_RANKS> peerLL{}, peerBulk{};
+  PeerBufs peerLL, peerBulk, peerTok;
   std::array<uint64_t*, MSCCLPP_AMD_MAX_RANKS> peerTokens{};
-  // peer mappings opened through IPC: (peer, peer allocation base) -> handle + mapped base here.
-  // A peer may free an allocation and get a new one at the same address; its handle then differs,
-  // and the old mapping (which would still alias the freed memory) is retired, not reused.  Retired
-  // mappings are closed with the communicator: a stale cached pointer keeps aliasing memory that
-  // stays mapped instead of faulting the GPU.
-  struct OpenedMapping {
-    hipIpcMemHandle_t handle;
-    void* mapped;
-  };
-  std::map<std::pair<int, uint64_t>, OpenedMapping> opened;
-  std::vector<void*> retired;
-  // registered output buffers: local allocation base -> per-peer mapped pointers of that buffer
-  std::map<std::pair<uint64_t, uint64_t>, std::array<void*, MSCCLPP_AMD_MAX_RANKS>> outRegs;
+  // Mappings that may still be in use by queued kernels: closed (dropped) only after a device
+  // synchronize, at the next point where that is allowed (flushRetired).
+  std::vector<std::shared_ptr<void>> retired;
   std::mutex mu;
 
-  // Exchange an IPC handle for [ptr, ptr+bytes) and return every rank's pointer as mapped here.
-  std::array<void*, MSCCLPP_AMD_MAX_RANKS> exchange(void* ptr) {
+  // Exchange an IPC handle of the allocation holding `ptr` and return every rank's pointer as mapped
+  // here (collective).  Mappings come from the process-wide cache (openIpcHandle), so a peer buffer
+  // mapped by several owners is opened once; a peer that freed an allocation and got a new one at
+  // the same address sends a new handle, which maps afresh.
+  PeerBufs exchange(void* ptr) {
     IpcBlob mine{};
     void* base = nullptr;
     size_t sz = 0;
@@ -238,51 +251,36 @@ struct ncclComm {
     mine.bytes = sz;
     std::vector<IpcBlob> all(nranks);
     boot->allGather(&mine, all.data(), sizeof(IpcBlob));
-    std::array<void*, MSCCLPP_AMD_MAX_RANKS> res{};
+    PeerBufs res;
     for (int r = 0; r < nranks; ++r) {
       if (r == rank) {
         res[r] = ptr;
         continue;
       }
-      auto key = std::make_pair(r, all[r].base);
-      auto it = opened.find(key);
-      void* mapped = nullptr;
-      if (it != opened.end() && std::memcmp(&it->second.handle, &all[r].handle, sizeof(hipIpcMemHandle_t)) == 0) {
-        mapped = it->second.mapped;
-      } else {
-        if (it != opened.end()) {
-          retired.push_back(it->second.mapped);
-          opened.erase(it);
-        }
-        info("rank " + std::to_string(rank) + ": opening ipc handle of rank " + std::to_string(r));
-        HIPCHECK(hipIpcOpenMemHandle(&mapped, all[r].handle, hipIpcMemLazyEnablePeerAccess));
-        info("rank " + std::to_string(rank) + ": opened");
-        opened[key] = OpenedMapping{all[r].handle, mapped};
-      }
-      res[r] = (char*)mapped + all[r].offset;
+      res.maps[(size_t)r] = openIpcHandle(all[r].handle);
+      res[r] = (char*)res.maps[(size_t)r].get() + all[r].offset;
     }
     return res;
   }
 
-  void forgetMapping(int peer, void* mappedBase) {
-    for (auto it = opened.begin(); it != opened.end(); ++it) {
-      if (it->first.first == peer && it->second.mapped == mappedBase) {
-        (void)hipIpcCloseMemHandle(it->second.mapped);
-        opened.erase(it);
-        return;
-      }
-    }
+  // Drop retired mappings once no queued kernel can still use them: a device synchronize, skipped
+  // (left for a later call) while `stream` is being captured into a graph.
+  void flushRetired(hipStream_t stream) {
+    if (retired.empty()) return;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (stream && hipStreamIsCapturing(stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone) return;
+    HIPCHECK(hipDeviceSynchronize());
+    retired.clear();
   }
 
   // Grow a scratch region collectively (every rank calls with the same size at the same call).
-  void ensure(void*& buf, size_t& have, std::array<void*, MSCCLPP_AMD_MAX_RANKS>& peers, size_t need) {
+  void ensure(void*& buf, size_t& have, PeerBufs& peers, size_t need) {
     if (need <= have) return;
     size_t want = have ? have : (size_t)64 << 20;
     while (want < need) want *= 2;
     HIPCHECK(hipDeviceSynchronize());
     boot->barrier();  // every rank has drained its previous use of the old buffers
-    for (int r = 0; r < nranks; ++r)
-      if (r != rank && peers[r]) forgetMapping(r, peers[r]);
+    peers = PeerBufs();  // our mappings of the peers' old buffers close here
     if (buf) HIPCHECK(hipFree(buf));
     buf = allocUncached(want);
     have = want;
@@ -291,37 +289,70 @@ struct ncclComm {
     info("rank " + std::to_string(rank) + " scratch grown to " + std::to_string(want));
   }
 
-  // Peer pointers of `out` (the bulk kernels write results straight into every peer's output,
-  // allreduce_fullmesh.cu:110-113).  Cached per local (allocation, offset) like the reference's
-  // per-buffer context cache (algorithm.cc:52-60, keyed on the local buffer only): a repeated call
-  // on the same buffer costs no host round trip.  As in the reference, every rank must pass its
+  // Peer pointers of a user buffer (the bulk kernels write results straight into every peer's
+  // output, allreduce_fullmesh.cu:110-113; zero-copy reads the peers' inputs).  Cached per local
+  // allocation like the reference's per-buffer context cache (algorithm.cc:52-60): a repeated call on
+  // the same buffer costs no host round trip.  As in the reference, every rank must pass its
   // matching buffer when a buffer is first used.
-  std::map<std::tuple<uint64_t, uint64_t, uint64_t>, std::array<void*, MSCCLPP_AMD_MAX_RANKS>> outPtrs;
+  //  * The allocation is identified by (base, size, HIP buffer id): a buffer freed and re-allocated
+  //    at the same address is a new allocation, registered afresh, and its old registration retired.
+  //  * At most kMaxUserRegs allocations stay registered; the least recently used one is retired
+  //    beyond that (every rank sees the same sequence of buffers, so every rank evicts the same).
+  //  * Retired mappings close after a device synchronize (flushRetired), never under a running kernel.
+  static constexpr size_t kMaxUserRegs = 64;
+  struct UserReg {
+    uint64_t bufferId = 0;
+    uint64_t lastUse = 0;
+    PeerBufs bases;
+    std::map<uint64_t, std::array<void*, MSCCLPP_AMD_MAX_RANKS>> byOffset;
+  };
+  std::map<std::pair<uint64_t, uint64_t>, UserReg> userRegs;
+  uint64_t useClock = 0;
 
-  std::array<void*, MSCCLPP_AMD_MAX_RANKS> registerOutput(void* out) {
+  void retireReg(std::map<std::pair<uint64_t, uint64_t>, UserReg>::iterator it) {
+    for (auto& m : it->second.bases.maps)
+      if (m) retired.push_back(std::move(m));
+    userRegs.erase(it);
+  }
+
+  std::array<void*, MSCCLPP_AMD_MAX_RANKS> registerOutput(void* out, hipStream_t stream = nullptr) {
     void* base = nullptr;
     size_t sz = 0;
     HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)out));
-    const auto pkey = std::make_tuple((uint64_t)base, (uint64_t)sz, (uint64_t)((char*)out - (char*)base));
-    auto pit = outPtrs.find(pkey);
-    if (pit != outPtrs.end()) return pit->second;
-    auto key = std::make_pair((uint64_t)base, (uint64_t)sz);
-    auto it = outRegs.find(key);
-    std::array<void*, MSCCLPP_AMD_MAX_RANKS> peersOfBase;
-    if (it == outRegs.end()) {
-      peersOfBase = exchange(base);  // collective: every rank registers its matching buffer now
-      outRegs[key] = peersOfBase;
-    } else {
-      peersOfBase = it->second;
+    const uint64_t bid = allocationId(base);
+    const auto key = std::make_pair((uint64_t)base, (uint64_t)sz);
+    auto it = userRegs.find(key);
+    if (it != userRegs.end() && it->second.bufferId != bid) {
+      retireReg(it);  // the address now belongs to another allocation
+      it = userRegs.end();
     }
-    // The offset of `out` inside its allocation must be the same on every rank for the cached
-    // mapping to be reused; exchange offsets (cheap) to check and build exact pointers.
-    uint64_t off = (uint64_t)((char*)out - (char*)base);
-    std::vector<uint64_t> offs(nranks);
-    boot->allGather(&off, offs.data(), sizeof(off));
-    std::array<void*, MSCCLPP_AMD_MAX_RANKS> res{};
-    for (int r = 0; r < nranks; ++r) res[r] = (r == rank) ? out : (char*)peersOfBase[r] + offs[r];
-    outPtrs[pkey] = res;
+    if (it == userRegs.end()) {
+      if (userRegs.size() >= kMaxUserRegs) {
+        auto lru = userRegs.begin();
+        for (auto j = userRegs.begin(); j != userRegs.end(); ++j)
+          if (j->second.lastUse < lru->second.lastUse) lru = j;
+        retireReg(lru);
+      }
+      UserReg reg;
+      reg.bufferId = bid;
+      reg.bases = exchange(base);  // collective: every rank registers its matching buffer now
+      it = userRegs.emplace(key, std::move(reg)).first;
+    }
+    UserReg& reg = it->second;
+    reg.lastUse = ++useClock;
+    const uint64_t off = (uint64_t)((char*)out - (char*)base);
+    auto pit = reg.byOffset.find(off);
+    if (pit == reg.byOffset.end()) {
+      // The offset of `out` inside its allocation may differ between ranks: exchange offsets (cheap)
+      // to build exact pointers.
+      std::vector<uint64_t> offs(nranks);
+      boot->allGather(&off, offs.data(), sizeof(off));
+      std::array<void*, MSCCLPP_AMD_MAX_RANKS> res{};
+      for (int r = 0; r < nranks; ++r) res[r] = (r == rank) ? out : (char*)reg.bases[r] + offs[r];
+      pit = reg.byOffset.emplace(off, res).first;
+    }
+    const auto res = pit->second;
+    flushRetired(stream);
     return res;
   }
 
@@ -344,47 +375,28 @@ struct ncclComm {
     boot->allGather(&blob, all.data(), sizeof(IpcBlob));
     mscclppAmdRankView v = baseView(rank == root ? send : recv, recv);
     if (rank != root) {
-      auto key = std::make_pair(root, all[root].base);
-      auto it = opened.find(key);
-      void* mapped = nullptr;
-      if (it != opened.end() && std::memcmp(&it->second.handle, &all[root].handle, sizeof(hipIpcMemHandle_t)) == 0) {
-        mapped = it->second.mapped;
-      } else {
-        if (it != opened.end()) {
-          retired.push_back(it->second.mapped);
-          opened.erase(it);
-        }
-        HIPCHECK(hipIpcOpenMemHandle(&mapped, all[root].handle, hipIpcMemLazyEnablePeerAccess));
-        opened[key] = OpenedMapping{all[root].handle, mapped};
-      }
-      v.peerInput[root] = (char*)mapped + all[root].offset;
+      // the mapping stays referenced until a later broadcast from the same root replaces it (and
+      // is then retired: the kernel below may still be queued)
+      auto m = openIpcHandle(all[root].handle);
+      auto& slot = bcastMaps[(size_t)root];
+      if (slot && slot != m) retired.push_back(std::move(slot));
+      slot = m;
+      v.peerInput[root] = (char*)m.get() + all[root].offset;
     }
-    return launchBroadcast(&v, 1, nranks, bytes, root, nblocks, nthreads, spinBudgetTicks(), stream);
+    const int rc = launchBroadcast(&v, 1, nranks, bytes, root, nblocks, nthreads, spinBudgetTicks(), stream);
+    flushRetired(stream);
+    return rc;
   }
+  std::array<std::shared_ptr<void>, MSCCLPP_AMD_MAX_RANKS> bcastMaps;
 
   // Drop every cached mapping of peers' user buffers (collective).  Scratch, token and flag
   // mappings stay.  After this, the next use of any buffer registers it afresh.
   void dropUserRegistrations() {
     HIPCHECK(hipDeviceSynchronize());
     boot->barrier();  // no rank still runs a kernel that uses a mapping being closed
-    std::vector<void*> keep;
-    for (int r = 0; r < nranks; ++r) {
-      keep.push_back(peerLL[r]);
-      keep.push_back(peerBulk[r]);
-      keep.push_back(peerTokens[r]);
-    }
-    for (auto it = opened.begin(); it != opened.end();) {
-      if (std::find(keep.begin(), keep.end(), it->second.mapped) == keep.end()) {
-        (void)hipIpcCloseMemHandle(it->second.mapped);
-        it = opened.erase(it);
-      } else {
-        ++it;
-      }
-    }
-    for (void* p : retired) (void)hipIpcCloseMemHandle(p);
+    while (!userRegs.empty()) retireReg(userRegs.begin());
+    for (auto& m : bcastMaps) m.reset();
     retired.clear();
-    outRegs.clear();
-    outPtrs.clear();
     boot->barrier();
   }
 
@@ -432,7 +444,7 @@ struct ncclComm {
       v.scratch = bulkScratch;
       v.scratchBytes = bulkBytes;
       for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
-      auto outs = registerOutput(out);
+      auto outs = registerOutput(out, stream);
       for (int r = 0; r < nranks; ++r) v.peerOutput[r] = outs[r];
       return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
     }
@@ -441,7 +453,7 @@ struct ncclComm {
         warn("mscclpp-test kernel 5 runs in place (sendbuff == recvbuff)");
         return ncclInvalidUsage;
       }
-      auto bufs = registerOutput(out);
+      auto bufs = registerOutput(out, stream);
       for (int r = 0; r < nranks; ++r) v.peerOutput[r] = bufs[r];
       return launchAllReduceBulk(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
     }
@@ -461,8 +473,8 @@ struct ncclComm {
     if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC) {
       // zero-copy: peers' inputs and outputs are mapped once per buffer (the reference registers
       // both as remote memories, allreduce_rsag_zero_copy.cu:25-27); no scratch
-      auto outs = registerOutput(out);
-      auto ins = registerOutput(const_cast<void*>(in));
+      auto outs = registerOutput(out, stream);
+      auto ins = registerOutput(const_cast<void*>(in), stream);
       for (int r = 0; r < nranks; ++r) {
         v.peerOutput[r] = outs[r];
         v.peerInput[r] = ins[r];
@@ -491,7 +503,7 @@ struct ncclComm {
     v.scratchBytes = bulkBytes;
     for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
     if (mode == 2) {
-      auto outs = registerOutput(out);
+      auto outs = registerOutput(out, stream);
       for (int r = 0; r < nranks; ++r) v.peerOutput[r] = outs[r];
     } else {
       for (int r = 0; r < nranks; ++r) v.peerOutput[r] = out;  // unused by ReduceScatter
@@ -511,9 +523,9 @@ struct ncclComm {
       } catch (...) {
       }
     }
-    for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second.mapped);
-    opened.clear();
-    for (void* p : retired) (void)hipIpcCloseMemHandle(p);
+    userRegs.clear();
+    for (auto& m : bcastMaps) m.reset();
+    peerLL = peerBulk = peerTok = PeerBufs();
     retired.clear();
     if (llScratch) (void)hipFree(llScratch);
     if (bulkScratch) (void)hipFree(bulkScratch);

@@ -1,0 +1,507 @@
+// Host core API (include/mscclpp_amd/core.hpp): bootstrap wrapper, registered memory, connections,
+// semaphores and the Communicator's connect / send / recv / buildSemaphore, plus the process-wide IPC
+// mapping cache every owner of a peer mapping goes through.
+//
+// Reference behaviour restated (not translated):
+//   RegisteredMemory serialize / deserialize   src/core/registered_memory.cc:35-145 (CudaIpc part)
+//   IPC open cache                             src/core/gpu_ipc_mem.cc:193-223
+//   CudaIpcConnection write / updateAndSync /
+//   flush                                      src/core/connection.cc:85-195, context.cc:16-46
+//   Communicator connect / sendMemory /
+//   recvMemory / buildSemaphore                src/core/communicator.cc:86-173
+//   SemaphoreStub / Semaphore                  src/core/semaphore.cc:32-116
+#include <unistd.h>
+
+#include <chrono>
+#include <unordered_map>
+
+#include "comm_internal.hpp"
+#include "mscclpp_amd/core.hpp"
+#include "mscclpp_amd/gpu_utils.hpp"
+#include "mscclpp_amd/memory_channel.hpp"
+#include "mscclpp_amd/semaphore.hpp"
+
+namespace mscclpp_amd {
+namespace host {
+
+namespace {
+struct HandleKey {
+  hipIpcMemHandle_t h;
+  bool operator==(const HandleKey& o) const { return std::memcmp(&h, &o.h, sizeof(h)) == 0; }
+};
+struct HandleKeyHash {
+  size_t operator()(const HandleKey& k) const {
+    const unsigned char* p = reinterpret_cast<const unsigned char*>(&k.h);
+    size_t x = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(k.h); ++i) x = (x ^ p[i]) * 1099511628211ull;
+    return x;
+  }
+};
+std::mutex gIpcMu;
+std::unordered_map<HandleKey, std::weak_ptr<void>, HandleKeyHash> gIpcOpen;
+}  // namespace
+
+std::shared_ptr<void> openIpcHandle(const hipIpcMemHandle_t& handle) {
+  std::lock_guard<std::mutex> lk(gIpcMu);
+  HandleKey key{handle};
+  auto it = gIpcOpen.find(key);
+  if (it != gIpcOpen.end()) {
+    if (auto p = it->second.lock()) return p;
+    gIpcOpen.erase(it);
+  }
+  void* mapped = nullptr;
+  HIPCHECK(hipIpcOpenMemHandle(&mapped, handle, hipIpcMemLazyEnablePeerAccess));
+  std::shared_ptr<void> p(mapped, [key](void* q) {
+    {
+      std::lock_guard<std::mutex> lk2(gIpcMu);
+      auto j = gIpcOpen.find(key);
+      if (j != gIpcOpen.end() && j->second.expired()) gIpcOpen.erase(j);
+    }
+    const hipError_t e = hipIpcCloseMemHandle(q);
+    if (e != hipSuccess) warn(std::string("hipIpcCloseMemHandle: ") + hipGetErrorString(e));
+  });
+  gIpcOpen[key] = p;
+  return p;
+}
+
+size_t liveIpcMappings() {
+  std::lock_guard<std::mutex> lk(gIpcMu);
+  size_t n = 0;
+  for (auto& kv : gIpcOpen) n += kv.second.expired() ? 0 : 1;
+  return n;
+}
+
+uint64_t allocationId(const void* ptr) {
+  unsigned long long id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)ptr) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (uint64_t)id;
+}
+
+}  // namespace host
+
+// ---- Bootstrap ------------------------------------------------------------------------------------
+void Bootstrap::send(const std::vector<char>& data, int peer, int tag) {
+  uint64_t n = data.size();
+  send(&n, sizeof(n), peer, tag);
+  if (n) send(const_cast<char*>(data.data()), (int)n, peer, tag);
+}
+
+void Bootstrap::recv(std::vector<char>& data, int peer, int tag) {
+  uint64_t n = 0;
+  recv(&n, sizeof(n), peer, tag);
+  data.resize(n);
+  if (n) recv(data.data(), (int)n, peer, tag);
+}
+
+namespace {
+// The communicator's TCP bootstrap behind the Bootstrap interface (core.hpp:29-110).
+class CommBootstrap : public Bootstrap {
+ public:
+  explicit CommBootstrap(ncclComm_t c) : c_(c) {}
+  int getRank() const override { return c_->rank; }
+  int getNranks() const override { return c_->nranks; }
+  int getNranksPerNode() const override { return c_->nranks; }
+  void send(void* data, int size, int peer, int tag) override { c_->boot->send(data, (size_t)size, peer, tag); }
+  void recv(void* data, int size, int peer, int tag) override { c_->boot->recv(data, (size_t)size, peer, tag); }
+  void allGather(void* allData, int size) override {
+    std::vector<char> mine((char*)allData + (size_t)c_->rank * size, (char*)allData + (size_t)(c_->rank + 1) * size);
+    c_->boot->allGather(mine.data(), allData, (size_t)size);
+  }
+  void barrier() override { c_->boot->barrier(); }
+  using Bootstrap::recv;
+  using Bootstrap::send;
+
+ private:
+  ncclComm_t c_;
+};
+
+// Bootstrap tag spaces of the exchanges below, so that a user's memory tag 0 and connection tag 0
+// never match each other's messages.
+int memTag(int tag) { return tag * 4 + 0; }
+int connTag(int tag) { return tag * 4 + 1; }
+int semTag(int tag) { return tag * 4 + 2; }
+
+constexpr uint32_t kMemMagic = 0x4d524d41;  // "AMRM"
+}  // namespace
+
+// ---- RegisteredMemory -------------------------------------------------------------------------------
+struct RegisteredMemory::Impl {
+  void* data = nullptr;      // usable here
+  uint64_t original = 0;     // owner's pointer
+  uint64_t size = 0;
+  TransportFlags transports;
+  int rank = -1;
+  int32_t pid = 0;
+  hipIpcMemHandle_t handle{};
+  uint64_t offset = 0;       // original - allocation base
+  std::shared_ptr<void> map;  // the IPC mapping (received from another process)
+};
+
+namespace {
+struct MemWire {
+  uint32_t magic;
+  int32_t rank;
+  int32_t pid;
+  uint32_t transports;
+  uint64_t original;
+  uint64_t size;
+  uint64_t offset;
+  hipIpcMemHandle_t handle;
+};
+}  // namespace
+
+void* RegisteredMemory::data() const { return pimpl_ ? pimpl_->data : nullptr; }
+void* RegisteredMemory::originalDataPtr() const { return pimpl_ ? (void*)pimpl_->original : nullptr; }
+size_t RegisteredMemory::size() const { return pimpl_ ? (size_t)pimpl_->size : 0; }
+TransportFlags RegisteredMemory::transports() const { return pimpl_ ? pimpl_->transports : TransportFlags(); }
+int RegisteredMemory::rank() const { return pimpl_ ? pimpl_->rank : -1; }
+
+std::vector<char> RegisteredMemory::serialize() const {
+  if (!pimpl_) throw Error("serialize: empty RegisteredMemory", ErrorCode::InvalidUsage);
+  MemWire w{};
+  w.magic = kMemMagic;
+  w.rank = pimpl_->rank;
+  w.pid = pimpl_->pid;
+  w.transports = pimpl_->transports.has(Transport::CudaIpc) ? 1u : 0u;
+  w.original = pimpl_->original;
+  w.size = pimpl_->size;
+  w.offset = pimpl_->offset;
+  w.handle = pimpl_->handle;
+  return std::vector<char>((char*)&w, (char*)&w + sizeof(w));
+}
+
+RegisteredMemory RegisteredMemory::deserialize(const std::vector<char>& data) {
+  MemWire w{};
+  if (data.size() != sizeof(w)) throw Error("deserialize: not a RegisteredMemory", ErrorCode::InvalidUsage);
+  std::memcpy(&w, data.data(), sizeof(w));
+  if (w.magic != kMemMagic) throw Error("deserialize: not a RegisteredMemory", ErrorCode::InvalidUsage);
+  auto impl = std::make_shared<Impl>();
+  impl->original = w.original;
+  impl->size = w.size;
+  impl->transports = w.transports ? TransportFlags(Transport::CudaIpc) : TransportFlags();
+  impl->rank = w.rank;
+  impl->pid = w.pid;
+  impl->handle = w.handle;
+  impl->offset = w.offset;
+  if (w.pid == (int32_t)getpid()) {
+    impl->data = (void*)w.original;  // same process (in-process ranks): the pointer is usable as is
+  } else {
+    try {
+      impl->map = host::openIpcHandle(w.handle);
+    } catch (const host::HipError& e) {
+      throw Error(std::string("RegisteredMemory::deserialize: ") + e.what(), ErrorCode::SystemError);
+    }
+    impl->data = (char*)impl->map.get() + w.offset;
+  }
+  return RegisteredMemory(impl);
+}
+
+// ---- Connection --------------------------------------------------------------------------------------
+// CudaIpcConnection (connection.cc:85-195): copies on a non-blocking stream of this GPU.  Token
+// values of updateAndSync are staged in a pinned ring, one slot per value (HIP reads a pinned source
+// when the copy runs, not when it is queued, so one shared word could publish a later value early);
+// a slot is reused only after a stream synchronize retired the copies of the previous lap.
+struct Connection::Impl {
+  int remoteRank = -1;
+  int tag = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t* slots = nullptr;
+  uint64_t nvals = 0;
+  static constexpr uint64_t kSlots = 1024;
+  ~Impl() {
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+    if (slots) (void)hipHostFree(slots);
+  }
+  void drain(int64_t timeoutUsec) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipStreamQuery(stream);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady)
+        throw Error(std::string("Connection::flush: ") + hipGetErrorString(e), ErrorCode::SystemError);
+      if (timeoutUsec >= 0 &&
+          std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >
+              timeoutUsec)
+        throw Error("Connection::flush timed out", ErrorCode::Timeout);
+    }
+  }
+};
+
+void Connection::write(RegisteredMemory dst, uint64_t dstOffset, RegisteredMemory src, uint64_t srcOffset,
+                       uint64_t size) {
+  if (!pimpl_) throw Error("write on an empty Connection", ErrorCode::InvalidUsage);
+  if (dstOffset + size > dst.size() || srcOffset + size > src.size())
+    throw Error("Connection::write out of the registered range", ErrorCode::InvalidUsage);
+  if (size == 0) return;
+  const hipError_t e = hipMemcpyAsync((char*)dst.data() + dstOffset, (char*)src.data() + srcOffset, size,
+                                      hipMemcpyDeviceToDevice, pimpl_->stream);
+  if (e != hipSuccess) throw Error(std::string("Connection::write: ") + hipGetErrorString(e), ErrorCode::SystemError);
+}
+
+void Connection::updateAndSync(RegisteredMemory dst, uint64_t dstOffset, uint64_t* src, uint64_t newValue) {
+  if (!pimpl_) throw Error("updateAndSync on an empty Connection", ErrorCode::InvalidUsage);
+  if (dstOffset + sizeof(uint64_t) > dst.size())
+    throw Error("Connection::updateAndSync out of the registered range", ErrorCode::InvalidUsage);
+  if (src) *src = newValue;
+  Impl& c = *pimpl_;
+  ++c.nvals;
+  if (c.nvals % Impl::kSlots == 0) c.drain(-1);
+  uint64_t* slot = &c.slots[c.nvals % Impl::kSlots];
+  *slot = newValue;
+  const hipError_t e =
+      hipMemcpyAsync((char*)dst.data() + dstOffset, slot, sizeof(uint64_t), hipMemcpyHostToDevice, c.stream);
+  if (e != hipSuccess)
+    throw Error(std::string("Connection::updateAndSync: ") + hipGetErrorString(e), ErrorCode::SystemError);
+}
+
+void Connection::flush(int64_t timeoutUsec) {
+  if (!pimpl_) throw Error("flush on an empty Connection", ErrorCode::InvalidUsage);
+  pimpl_->drain(timeoutUsec);
+}
+
+Transport Connection::transport() const { return Transport::CudaIpc; }
+Transport Connection::remoteTransport() const { return Transport::CudaIpc; }
+int Connection::remoteRank() const { return pimpl_ ? pimpl_->remoteRank : -1; }
+int Connection::tag() const { return pimpl_ ? pimpl_->tag : -1; }
+hipStream_t Connection::stream() const { return pimpl_ ? pimpl_->stream : nullptr; }
+
+// ---- Semaphore ---------------------------------------------------------------------------------------
+struct Semaphore::Impl {
+  Connection connection;
+  RegisteredMemory local;   // my token (the peer signals into it)
+  RegisteredMemory remote;  // the peer's token as mapped here
+  std::shared_ptr<void> tokenAlloc;  // keeps my token's allocation alive
+  uint64_t budget = 0;
+  uint32_t* err = nullptr;
+};
+
+Connection& Semaphore::connection() { return pimpl_->connection; }
+const Connection& Semaphore::connection() const { return pimpl_->connection; }
+const RegisteredMemory& Semaphore::localMemory() const { return pimpl_->local; }
+const RegisteredMemory& Semaphore::remoteMemory() const { return pimpl_->remote; }
+
+// ---- Communicator ---------------------------------------------------------------------------------------
+Communicator::Communicator(ncclComm_t comm) : comm_(comm) {
+  if (!comm) throw Error("Communicator: null ncclComm_t", ErrorCode::InvalidUsage);
+}
+
+Communicator::~Communicator() {
+  if (owned_ && comm_) (void)ncclCommDestroy(comm_);
+}
+
+std::shared_ptr<Communicator> Communicator::create(int rank, int nranks, const ncclUniqueId& id) {
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&c, nranks, id, rank);
+  if (r != ncclSuccess)
+    throw Error(std::string("ncclCommInitRank: ") + ncclGetErrorString(r) + ": " + ncclGetLastError(nullptr),
+                ErrorCode::SystemError);
+  auto p = std::make_shared<Communicator>(c);
+  p->owned_ = true;
+  return p;
+}
+
+int Communicator::rank() const { return comm_->rank; }
+int Communicator::nRanks() const { return comm_->nranks; }
+int Communicator::nRanksPerNode() const { return comm_->nranks; }
+int Communicator::device() const { return comm_->device; }
+uint32_t* Communicator::deviceErrorWord() const { return comm_->err; }
+uint64_t Communicator::spinBudget() const { return host::spinBudgetTicks(); }
+
+std::shared_ptr<Bootstrap> Communicator::bootstrap() {
+  if (!bootstrap_) bootstrap_ = std::make_shared<CommBootstrap>(comm_);
+  return bootstrap_;
+}
+
+RegisteredMemory Communicator::registerMemory(void* ptr, size_t size, TransportFlags transports) {
+  if (!ptr || size == 0) throw Error("registerMemory: null or empty buffer", ErrorCode::InvalidUsage);
+  auto impl = std::make_shared<RegisteredMemory::Impl>();
+  impl->data = ptr;
+  impl->original = (uint64_t)ptr;
+  impl->size = size;
+  impl->transports = transports;
+  impl->rank = comm_->rank;
+  impl->pid = (int32_t)getpid();
+  if (transports.has(Transport::CudaIpc)) {
+    void* base = nullptr;
+    size_t range = 0;
+    hipError_t e = hipMemGetAddressRange((hipDeviceptr_t*)&base, &range, (hipDeviceptr_t)ptr);
+    if (e == hipSuccess && (char*)ptr + size > (char*)base + range) e = hipErrorInvalidValue;
+    if (e == hipSuccess) e = hipIpcGetMemHandle(&impl->handle, base);
+    if (e != hipSuccess)
+      throw Error(std::string("registerMemory: not a device allocation (") + hipGetErrorString(e) + ")",
+                  ErrorCode::InvalidUsage);
+    impl->offset = (uint64_t)((char*)ptr - (char*)base);
+  }
+  return RegisteredMemory(impl);
+}
+
+void Communicator::sendMemory(RegisteredMemory memory, int remoteRank, int tag) {
+  bootstrap()->send(memory.serialize(), remoteRank, memTag(tag));
+}
+
+std::shared_future<RegisteredMemory> Communicator::recvMemory(int remoteRank, int tag) {
+  auto boot = bootstrap();
+  return std::async(std::launch::deferred, [boot, remoteRank, tag] {
+           std::vector<char> data;
+           boot->recv(data, remoteRank, memTag(tag));
+           return RegisteredMemory::deserialize(data);
+         }).share();
+}
+
+namespace {
+struct EndpointWire {
+  int32_t rank;
+  int32_t pid;
+  int32_t device;
+  int32_t transport;
+};
+}  // namespace
+
+std::shared_future<Connection> Communicator::connect(const EndpointConfig& localConfig, int remoteRank, int tag) {
+  if (localConfig.transport != Transport::CudaIpc)
+    throw Error("connect: one MI355X node carries CudaIpc connections only", ErrorCode::InvalidUsage);
+  if (remoteRank < 0 || remoteRank >= comm_->nranks)
+    throw Error("connect: bad remote rank", ErrorCode::InvalidUsage);
+  EndpointWire mine{comm_->rank, (int32_t)getpid(), comm_->device, (int32_t)Transport::CudaIpc};
+  auto boot = bootstrap();
+  boot->send(&mine, (int)sizeof(mine), remoteRank, connTag(tag));
+  const int device = comm_->device;
+  return std::async(std::launch::deferred, [boot, remoteRank, tag, device] {
+           EndpointWire peer{};
+           boot->recv(&peer, (int)sizeof(peer), remoteRank, connTag(tag));
+           if (peer.transport != (int32_t)Transport::CudaIpc)
+             throw Error("connect: the peer offered another transport", ErrorCode::InvalidUsage);
+           auto impl = std::make_shared<Connection::Impl>();
+           impl->remoteRank = remoteRank;
+           impl->tag = tag;
+           impl->device = device;
+           int cur = 0;
+           gpuCheck(hipGetDevice(&cur), "hipGetDevice");
+           gpuCheck(hipSetDevice(device), "hipSetDevice");
+           gpuCheck(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+           gpuCheck(hipHostMalloc((void**)&impl->slots, Connection::Impl::kSlots * sizeof(uint64_t),
+                                  hipHostMallocDefault),
+                    "hipHostMalloc");
+           gpuCheck(hipSetDevice(cur), "hipSetDevice");
+           return Connection(impl);
+         }).share();
+}
+
+int Communicator::remoteRankOf(const Connection& connection) { return connection.remoteRank(); }
+int Communicator::tagOf(const Connection& connection) { return connection.tag(); }
+
+std::shared_future<Semaphore> Communicator::buildSemaphore(const Connection& connection, int remoteRank, int tag) {
+  if (!connection.valid()) throw Error("buildSemaphore: empty connection", ErrorCode::InvalidUsage);
+  // my token: 8 bytes of uncached device memory (semaphore.cc:32-43), registered and sent
+  void* tok = host::allocUncached(64);
+  std::shared_ptr<void> tokAlloc(tok, [](void* p) { (void)hipFree(p); });
+  RegisteredMemory local = registerMemory(tok, sizeof(uint64_t), Transport::CudaIpc);
+  auto boot = bootstrap();
+  boot->send(local.serialize(), remoteRank, semTag(tag));
+  const uint64_t budget = host::spinBudgetTicks();
+  uint32_t* err = comm_->err;
+  return std::async(std::launch::deferred, [boot, remoteRank, tag, connection, local, tokAlloc, budget, err] {
+           std::vector<char> data;
+           boot->recv(data, remoteRank, semTag(tag));
+           auto impl = std::make_shared<Semaphore::Impl>();
+           impl->connection = connection;
+           impl->local = local;
+           impl->remote = RegisteredMemory::deserialize(data);
+           impl->tokenAlloc = tokAlloc;
+           impl->budget = budget;
+           impl->err = err;
+           return Semaphore(impl);
+         }).share();
+}
+
+std::vector<void*> Communicator::registerMemory(void* ptr) {
+  if (!ptr) throw std::invalid_argument("registerMemory: null pointer");
+  std::vector<void*> res((size_t)comm_->nranks, nullptr);
+  if (comm_->nranks == 1) {
+    res[0] = ptr;
+    return res;
+  }
+  std::lock_guard<std::mutex> lk(comm_->mu);
+  auto peers = comm_->registerOutput(ptr);  // collective IPC exchange, cached per allocation
+  for (int r = 0; r < comm_->nranks; ++r) res[(size_t)r] = peers[(size_t)r];
+  return res;
+}
+
+void Communicator::allGather(const void* sendbuf, void* recvbuf, size_t bytesPerRank) {
+  comm_->boot->allGather(sendbuf, recvbuf, bytesPerRank);
+}
+
+void Communicator::barrier() { comm_->boot->barrier(); }
+
+// ---- semaphores (semaphore.hpp; semaphore.cc:118-238) ---------------------------------------------
+Host2DeviceSemaphore::Host2DeviceSemaphore(const Semaphore& semaphore, uint64_t budget, uint32_t* err)
+    : semaphore_(semaphore) {
+  if (!semaphore.valid()) throw Error("Host2DeviceSemaphore: empty Semaphore", ErrorCode::InvalidUsage);
+  gpuCheck(hipMalloc((void**)&expectedInboundToken_, sizeof(uint64_t)), "hipMalloc");
+  gpuCheck(hipMemset(expectedInboundToken_, 0, sizeof(uint64_t)), "hipMemset");
+  budget_ = budget ? budget : semaphore.pimpl()->budget;
+  err_ = err ? err : semaphore.pimpl()->err;
+}
+
+Host2DeviceSemaphore::Host2DeviceSemaphore(Communicator& communicator, const Connection& connection)
+    : Host2DeviceSemaphore(communicator.buildSemaphore(connection, connection.remoteRank(), connection.tag()).get()) {}
+
+Host2DeviceSemaphore::~Host2DeviceSemaphore() {
+  if (expectedInboundToken_) (void)hipFree(expectedInboundToken_);
+}
+
+Connection& Host2DeviceSemaphore::connection() { return semaphore_.connection(); }
+
+void Host2DeviceSemaphore::signal() {
+  semaphore_.connection().updateAndSync(semaphore_.remoteMemory(), 0, &outbound_, outbound_ + 1);
+}
+
+Host2DeviceSemaphore::DeviceHandle Host2DeviceSemaphore::deviceHandle() const {
+  DeviceHandle h{};
+  h.inboundToken = (uint64_t*)semaphore_.localMemory().data();
+  h.expectedInboundToken = expectedInboundToken_;
+  h.budget = budget_;
+  h.err = err_;
+  return h;
+}
+
+MemoryDevice2DeviceSemaphore::MemoryDevice2DeviceSemaphore(const Semaphore& semaphore, uint64_t budget, uint32_t* err)
+    : semaphore_(semaphore) {
+  if (!semaphore.valid()) throw Error("MemoryDevice2DeviceSemaphore: empty Semaphore", ErrorCode::InvalidUsage);
+  gpuCheck(hipMalloc((void**)&expectedInboundToken_, sizeof(uint64_t)), "hipMalloc");
+  gpuCheck(hipMemset(expectedInboundToken_, 0, sizeof(uint64_t)), "hipMemset");
+  budget_ = budget ? budget : semaphore.pimpl()->budget;
+  err_ = err ? err : semaphore.pimpl()->err;
+}
+
+MemoryDevice2DeviceSemaphore::MemoryDevice2DeviceSemaphore(Communicator& communicator, const Connection& connection)
+    : MemoryDevice2DeviceSemaphore(
+          communicator.buildSemaphore(connection, connection.remoteRank(), connection.tag()).get()) {}
+
+MemoryDevice2DeviceSemaphore::~MemoryDevice2DeviceSemaphore() {
+  if (expectedInboundToken_) (void)hipFree(expectedInboundToken_);
+}
+
+Connection& MemoryDevice2DeviceSemaphore::connection() { return semaphore_.connection(); }
+
+MemoryDevice2DeviceSemaphore::DeviceHandle MemoryDevice2DeviceSemaphore::deviceHandle() const {
+  DeviceHandle h{};
+  h.inboundToken = (uint64_t*)semaphore_.localMemory().data();
+  h.remoteInboundToken = (uint64_t*)semaphore_.remoteMemory().data();
+  h.expectedInboundToken = expectedInboundToken_;
+  h.budget = budget_;
+  h.err = err_;
+  return h;
+}
+
+BaseMemoryChannel::BaseMemoryChannel(const Semaphore& semaphore)
+    : semaphore_(std::make_shared<MemoryDevice2DeviceSemaphore>(semaphore)) {}
+
+}  // namespace mscclpp_amd

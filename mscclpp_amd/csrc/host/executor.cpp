@@ -431,7 +431,7 @@ struct mscclppAmdExecutor {
   ncclComm* comm = nullptr;
   uint64_t* tokens = nullptr;    // inbound [kMaxRanks][kMaxTags], uncached
   uint64_t* expected = nullptr;  // [kMaxRanks][kMaxTags]
-  std::array<void*, MSCCLPP_AMD_MAX_RANKS> peerTokens{};
+  PeerBufs peerTokens;
   ex::Syncer* syncers = nullptr;
   uint32_t* err = nullptr;
   uint32_t flag = 0;  // Executor::Impl::launchKernel's flag: +1 per execution
@@ -444,7 +444,7 @@ struct mscclppAmdExecutor {
   struct Context {
     void* scratch = nullptr;
     uint64_t scratchBytes = 0, scratchChunk = 0;
-    std::array<void*, MSCCLPP_AMD_MAX_RANKS> peerScratch{}, peerIn{}, peerOut{};
+    PeerBufs peerScratch, peerIn, peerOut;
     ex::Sem* sems = nullptr;
     std::map<std::pair<uint64_t, uint64_t>, DevicePlan> plans;
   };
@@ -470,8 +470,7 @@ struct mscclppAmdExecutor {
     comm->boot->barrier();  // no rank still runs a kernel on these buffers
     for (auto& kv : contexts) {
       Context& c = kv.second;
-      for (int r = 0; r < comm->nranks; ++r)
-        if (r != comm->rank && c.peerScratch[r]) comm->forgetMapping(r, c.peerScratch[r]);
+      c.peerScratch = c.peerIn = c.peerOut = PeerBufs();  // our mappings of the peers' buffers close
     }
     comm->boot->barrier();  // every rank closed its mappings of our scratch before it is freed
     for (auto& kv : contexts) {
@@ -485,8 +484,7 @@ struct mscclppAmdExecutor {
 
   void destroy() {
     dropContexts();
-    for (int r = 0; r < comm->nranks; ++r)
-      if (r != comm->rank && peerTokens[r]) comm->forgetMapping(r, peerTokens[r]);
+    peerTokens = PeerBufs();
     comm->boot->barrier();
     (void)hipFree(tokens);
     (void)hipFree(expected);

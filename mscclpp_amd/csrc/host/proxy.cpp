@@ -1,14 +1,11 @@
-// Host-proxy transport: trigger FIFO (host side), proxy thread, ProxyService and the two harnesses
-// built on them (the config-1 host-offload AllGather and a PortChannel all-to-all).
-//
-// Reference behaviour:
-//   Fifo::poll / pop                 src/core/fifo.cc:58-78 (commit bit = lap parity, cleared on read)
-//   Proxy::start loop                src/core/proxy.cc:42-100 (busy poll, handler, pop; NUMA bind :23-33)
-//   ProxyService::handleTrigger      src/core/port_channel.cc:117-154 (Data -> write, Flag -> signal,
-//                                    Sync -> flush then publish flushDonePos)
-//   CudaIpcConnection::write/flush   src/core/connection.cc:138-195 (hipMemcpyAsync on a per-connection
-//                                    stream; updateAndSync = H2D copy of the outbound token)
-//   MyProxyService / main timing     test/allgather_test_host_offloading.cu:81-330
+// The proxy-path harnesses of the reference's tests on this library:
+//   mscclppAmdHostOffloadAllGather   test/allgather_test_host_offloading.cu:81-330 (its own proxy
+//                                    handler, as the test's MyProxyService)
+//   mscclppAmdPortChannelAllToAll    PortChannels built with the public host API + ProxyService
+//   mscclppAmdProxyRingAllReduce     test/mscclpp-test/allreduce_test.cu:730-839 (allreduce1)
+// The FIFO, proxy thread and ProxyService themselves are in channels.cpp (include/mscclpp_amd/
+// {fifo,proxy,port_channel}.hpp).  Copy and token-update failures on a proxy thread are checked and
+// reported (the result's correctness flag and a warning), never dropped.
 #include <sched.h>
 
 #include <atomic>
@@ -19,7 +16,7 @@
 #include <thread>
 
 #include "comm_internal.hpp"
-#include "mscclpp_amd/port_channel_device.hpp"
+#include "mscclpp_amd/port_channel.hpp"
 
 extern "C" int mscclppAmdLaunchHostOffloadKernel(int rank, int nranks, const void* fifoHandle, void* semHandles,
                                                  int handleIndex, uint64_t budget, uint32_t* err, void* stream);
@@ -31,149 +28,6 @@ extern "C" int mscclppAmdLaunchPortChannelPut(void* chans, int nchans, const uin
 
 namespace mscclpp_amd {
 namespace host {
-
-// ---- NUMA: pin the proxy thread to the CPUs of the GPU's NUMA node (proxy.cc:23-33) ----------
-static int deviceNumaNode(int device) {
-  char bus[64] = {0};
-  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return -1;
-  std::string id(bus);
-  for (auto& ch : id) ch = (char)std::tolower(ch);
-  std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
-  int node = -1;
-  if (f) f >> node;
-  return node;
-}
-
-static int bindToNumaNode(int node) {
-  if (node < 0) return -1;
-  std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
-  std::string list;
-  if (!f || !std::getline(f, list)) return -1;
-  cpu_set_t set;
-  CPU_ZERO(&set);
-  int count = 0;
-  std::stringstream ss(list);
-  std::string part;
-  while (std::getline(ss, part, ',')) {
-    int a = 0, b = 0;
-    if (sscanf(part.c_str(), "%d-%d", &a, &b) == 2) {
-      for (int c = a; c <= b; ++c, ++count) CPU_SET(c, &set);
-    } else if (sscanf(part.c_str(), "%d", &a) == 1) {
-      CPU_SET(a, &set);
-      ++count;
-    }
-  }
-  if (count == 0) return -1;
-  return sched_setaffinity(0, sizeof(set), &set) == 0 ? node : -1;
-}
-
-// ---- FIFO (host side) --------------------------------------------------------------------------
-class Fifo {
- public:
-  explicit Fifo(int size) : size_(size) {
-    if (size <= 0 || (size & (size - 1))) throw std::invalid_argument("FIFO size must be a power of two");
-    while ((1 << shift_) < size) ++shift_;
-    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-    HIPCHECK(hipHostMalloc((void**)&triggers_, sizeof(ProxyTrigger) * size, fl));
-    std::memset((void*)triggers_, 0, sizeof(ProxyTrigger) * size);
-    HIPCHECK(hipHostMalloc((void**)&tail_, 64, fl));
-    std::memset((void*)tail_, 0, 64);
-    HIPCHECK(hipHostGetDevicePointer((void**)&dTriggers_, (void*)triggers_, 0));
-    HIPCHECK(hipHostGetDevicePointer((void**)&dTail_, (void*)tail_, 0));
-    HIPCHECK(hipMalloc((void**)&head_, 64));
-    HIPCHECK(hipMemset(head_, 0, 64));
-    HIPCHECK(hipMalloc((void**)&tailCache_, 64));
-    HIPCHECK(hipMemset(tailCache_, 0, 64));
-  }
-  ~Fifo() {
-    (void)hipHostFree((void*)triggers_);
-    (void)hipHostFree((void*)tail_);
-    (void)hipFree(head_);
-    (void)hipFree(tailCache_);
-  }
-  // fifo.cc:58-73: accept the slot only when its commit bit carries this lap's parity.
-  bool poll(ProxyTrigger& t) {
-    const uint64_t cur = *tail_;
-    ProxyTrigger* slot = &triggers_[cur & (uint64_t)(size_ - 1)];
-    const uint64_t snd = __atomic_load_n(&slot->snd, __ATOMIC_ACQUIRE);
-    const uint64_t parity = ((cur >> shift_) & 1ull) ^ 1ull;
-    if ((snd >> 63) != parity) return false;
-    t.snd = snd & ~(1ull << 63);
-    t.fst = __atomic_load_n(&slot->fst, __ATOMIC_RELAXED);
-    return true;
-  }
-  void pop() { __atomic_store_n(tail_, *tail_ + 1, __ATOMIC_RELEASE); }  // fifo.cc:75-78
-  uint64_t tail() const { return *tail_; }
-  FifoDeviceHandle deviceHandle() const {
-    FifoDeviceHandle h{};
-    h.triggers = dTriggers_;
-    h.head = head_;
-    h.tail = dTail_;
-    h.tailCache = tailCache_;
-    h.size = size_;
-    h.sizeMask = (uint64_t)size_ - 1;
-    h.sizeShift = (uint64_t)shift_;
-    return h;
-  }
-
- private:
-  int size_;
-  int shift_ = 0;
-  ProxyTrigger* triggers_ = nullptr;
-  ProxyTrigger* dTriggers_ = nullptr;
-  uint64_t* tail_ = nullptr;
-  uint64_t* dTail_ = nullptr;
-  uint64_t* head_ = nullptr;
-  uint64_t* tailCache_ = nullptr;
-};
-
-// ---- proxy thread ------------------------------------------------------------------------------
-class Proxy {
- public:
-  using Handler = std::function<bool(const ProxyTrigger&, uint64_t pos)>;  // true = stop
-  Proxy(int device, int fifoSize, Handler h) : device_(device), fifo_(fifoSize), handler_(std::move(h)) {}
-  ~Proxy() { stop(); }
-  void start() {
-    running_.store(true, std::memory_order_release);
-    th_ = std::thread([this] {
-      (void)hipSetDevice(device_);
-      numaNode_ = bindToNumaNode(deviceNumaNode(device_));
-      hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-      (void)hipThreadExchangeStreamCaptureMode(&mode);  // never capture in a proxy thread
-      started_.store(true, std::memory_order_release);
-      ProxyTrigger t;
-      int runCnt = 4096;
-      for (;;) {
-        if (runCnt-- == 0) {
-          runCnt = 4096;
-          if (!running_.load(std::memory_order_acquire)) break;
-        }
-        if (!fifo_.poll(t)) continue;
-        const bool stop = handler_(t, fifo_.tail());
-        fifo_.pop();
-        if (stop) break;
-      }
-    });
-    while (!started_.load(std::memory_order_acquire)) std::this_thread::sleep_for(std::chrono::microseconds(50));
-  }
-  void stop() {
-    if (th_.joinable()) {
-      running_.store(false, std::memory_order_release);
-      th_.join();
-    }
-  }
-  Fifo& fifo() { return fifo_; }
-  int numaNode() const { return numaNode_; }
-
- private:
-  int device_;
-  Fifo fifo_;
-  Handler handler_;
-  std::thread th_;
-  std::atomic<bool> running_{false};
-  std::atomic<bool> started_{false};
-  int numaNode_ = -1;
-};
 
 static double nowSec() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -234,7 +88,8 @@ class TokenWriter {
     if (value_ % kSlots == 0) spinSync(s);
     uint64_t* slot = &slots_[value_ % kSlots];
     *slot = value_;
-    (void)hipMemcpyAsync(remoteToken, slot, sizeof(uint64_t), hipMemcpyHostToDevice, s);
+    const hipError_t e = hipMemcpyAsync(remoteToken, slot, sizeof(uint64_t), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) throw HipError(e, "proxy token update (hipMemcpyAsync H2D)");
   }
 
  private:
@@ -288,18 +143,24 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
     HIPCHECK(hipMalloc((void**)&err, 64));
     HIPCHECK(hipMemset(err, 0, 64));
     // MyProxyService::handleTrigger (:135-155)
-    Proxy proxy(comm->device, 512, [&](const ProxyTrigger& t, uint64_t) {
+    std::string proxyFailure;  // first copy / token failure on the proxy thread
+    Proxy proxy([&](ProxyTrigger t, uint64_t) {
       if (t.fst > 0) {
         const int set = t.fst == 1 ? 0 : 1;
-        for (int k = 1; k < n; ++k) {
-          const int nghr = (rank + k) % n;
-          (void)hipMemcpyAsync((char*)peers[nghr] + rank * perRank, (char*)data + rank * perRank, perRank,
-                               hipMemcpyDeviceToDevice, conns[nghr].stream);
-          writers[set * n + nghr]->signal((uint64_t*)peerTok[nghr] + set * n + rank, conns[nghr].stream);
+        try {
+          for (int k = 1; k < n; ++k) {
+            const int nghr = (rank + k) % n;
+            const hipError_t e = hipMemcpyAsync((char*)peers[nghr] + rank * perRank, (char*)data + rank * perRank,
+                                                perRank, hipMemcpyDeviceToDevice, conns[nghr].stream);
+            if (e != hipSuccess) throw HipError(e, "proxy data copy (hipMemcpyAsync D2D)");
+            writers[set * n + nghr]->signal((uint64_t*)peerTok[nghr] + set * n + rank, conns[nghr].stream);
+          }
+        } catch (const std::exception& ex) {
+          if (proxyFailure.empty()) proxyFailure = ex.what();
         }
       }
-      return false;
-    });
+      return ProxyHandlerResult::Continue;
+    }, 512);
     proxy.start();
     FifoDeviceHandle fh = proxy.fifo().deviceHandle();
     hipStream_t st;
@@ -350,7 +211,8 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
     comm->boot->barrier();
     uint32_t e = 0;
     HIPCHECK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost));
-    out[2] = (ok && e == 0) ? 1.0 : 0.0;
+    if (!proxyFailure.empty()) warn("host offload proxy: " + proxyFailure);
+    out[2] = (ok && e == 0 && proxyFailure.empty()) ? 1.0 : 0.0;
     out[3] = (double)proxy.numaNode();
     proxy.stop();
     for (int r = 0; r < n; ++r)
@@ -362,11 +224,8 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
     (void)hipGraphDestroy(graph);
     (void)hipStreamDestroy(st);
     comm->boot->barrier();  // peers no longer touch my data / tokens
-    for (int r = 0; r < n; ++r)
-      if (r != rank) {  // peers free these buffers now: drop the cached mappings
-        comm->forgetMapping(r, peers[r]);
-        comm->forgetMapping(r, peerTok[r]);
-      }
+    peers = PeerBufs();     // peers free these buffers now: close our mappings of them
+    peerTok = PeerBufs();
     (void)hipFree(err);
     (void)hipFree(dh);
     (void)hipFree(tok);
@@ -377,7 +236,10 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
 }
 
 // =============================================================================================
-// Harness 2: PortChannel all-to-all through ProxyService (port_channel.cc:117-178)
+// Harness 2: PortChannel all-to-all through the general ProxyService (port_channel.cc:117-178),
+// built with the public host API the way a user kernel's channels are: Communicator::connect +
+// registerMemory / sendMemory / recvMemory + ProxyService::buildAndAddSemaphore / addMemory /
+// portChannel, device handles copied to the GPU.
 // =============================================================================================
 extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int mode, int iters, double* out) {
   return guarded([&] {
@@ -392,124 +254,78 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
     std::vector<uint32_t> h(bytes / 4);
     for (size_t i = 0; i < h.size(); ++i) h[i] = (uint32_t)(rank * 0x01000000u + i);  // src chunk q for peer q
     HIPCHECK(hipMemcpy(src, h.data(), bytes, hipMemcpyHostToDevice));
-    auto peerDst = comm->exchange(dst);
-    // MemoryId 0 = my src; 1 + q = peer q's dst.  One semaphore (and channel) per peer.
-    std::vector<void*> mem(1 + n);
-    mem[0] = src;
-    for (int q = 0; q < n; ++q) mem[1 + q] = peerDst[q];
-    uint64_t *tok = nullptr, *expct = nullptr, *flushDone = nullptr, *dFlushDone = nullptr;
-    HIPCHECK(hipMalloc((void**)&tok, n * 8));
-    HIPCHECK(hipMemset(tok, 0, n * 8));
-    HIPCHECK(hipMalloc((void**)&expct, n * 8));
-    HIPCHECK(hipMemset(expct, 0, n * 8));
-    auto peerTok = comm->exchange(tok);
-    std::vector<std::unique_ptr<TokenWriter>> writers(n);
-    for (auto& w : writers) w = std::make_unique<TokenWriter>();
-    HIPCHECK(hipHostMalloc((void**)&flushDone, n * 64, hipHostMallocMapped | hipHostMallocCoherent));
-    std::memset(flushDone, 0, n * 64);
-    HIPCHECK(hipHostGetDevicePointer((void**)&dFlushDone, flushDone, 0));
-    std::vector<Conn> conns(n);
-    for (int q = 0; q < n; ++q)
-      if (q != rank) HIPCHECK(hipStreamCreateWithFlags(&conns[q].stream, hipStreamNonBlocking));
-    uint32_t* err = nullptr;
-    HIPCHECK(hipMalloc((void**)&err, 64));
-    HIPCHECK(hipMemset(err, 0, 64));
-    // semaphoreId = peer index
-    Proxy proxy(comm->device, 512, [&](const ProxyTrigger& t, uint64_t pos) {
-      const int q = (int)t.fields.semaphoreId;
-      if (q < 0 || q >= n || q == rank) return false;
-      if (t.fields.type & kTriggerData) {
-        const hipError_t e = proxyCopy((char*)mem[t.fields.dstMemoryId] + t.fields.dstOffset,
-                                       (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
-                                       conns[q].stream);
-        if (e != hipSuccess) warn("proxy copy failed: " + std::string(hipGetErrorString(e)));
-      }
-      if (t.fields.type & kTriggerFlag) {
-        // remote token slot of peer q for source `rank`
-        writers[q]->signal((uint64_t*)peerTok[q] + rank, conns[q].stream);
-      }
-      if (t.fields.type & kTriggerSync) {
-        spinSync(conns[q].stream);
-        __atomic_store_n(&flushDone[q * 8], pos + 1, __ATOMIC_RELEASE);
-      }
-      return false;
-    });
-    proxy.start();
-    std::vector<PortChannelDeviceHandle> ch;
-    for (int q = 0; q < n; ++q) {
-      if (q == rank) continue;
-      PortChannelDeviceHandle c{};
-      c.semaphoreId = (uint32_t)q;
-      c.dst = (uint32_t)(1 + q);
-      c.src = 0;
-      c.semaphore = {tok + q, expct + q};
-      c.fifo = proxy.fifo().deviceHandle();
-      c.flushDonePos = dFlushDone + q * 8;
-      c.budget = spinBudgetTicks();
-      c.err = err;
-      ch.push_back(c);
-    }
-    // channel c (peer q) moves my src chunk q to offset rank*chunk of q's dst
-    std::vector<uint64_t> offs;
-    for (int q = 0; q < n; ++q)
-      if (q != rank) offs.push_back((uint64_t)rank * chunk);
-    for (int q = 0; q < n; ++q)
-      if (q != rank) offs.push_back((uint64_t)q * chunk);
-    uint64_t* dOffs = nullptr;
-    HIPCHECK(hipMalloc((void**)&dOffs, offs.size() * 8));
-    HIPCHECK(hipMemcpy(dOffs, offs.data(), offs.size() * 8, hipMemcpyHostToDevice));
-    PortChannelDeviceHandle* dch = nullptr;
-    HIPCHECK(hipMalloc((void**)&dch, ch.size() * sizeof(ch[0])));
-    HIPCHECK(hipMemcpy(dch, ch.data(), ch.size() * sizeof(ch[0]), hipMemcpyHostToDevice));
-    hipStream_t st;
-    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    comm->boot->barrier();
-    double t0 = nowSec();
-    for (int i = 0; i < iters; ++i) {
-      if (mscclppAmdLaunchPortChannelPut(dch, (int)ch.size(), dOffs, dOffs + ch.size(), chunk, mode, st))
-        throw std::runtime_error("launch");
-    }
-    HIPCHECK(hipStreamSynchronize(st));
-    double t1 = nowSec();
-    comm->boot->barrier();
-    out[0] = (t1 - t0) * 1e6 / iters;
-    // check: peer p's chunk addressed to me (its src chunk `rank`) sits at offset p*chunk of my dst
-    std::vector<uint32_t> back(bytes / 4);
-    HIPCHECK(hipMemcpy(back.data(), dst, bytes, hipMemcpyDeviceToHost));
+    double t0 = 0, t1 = 0;
     bool ok = true;
-    for (int p = 0; p < n && ok; ++p) {
-      if (p == rank) continue;
-      for (size_t i = 0; i < chunk / 4; ++i) {
-        const size_t srcElem = (size_t)rank * (chunk / 4) + i;
-        if (back[(size_t)p * (chunk / 4) + i] != (uint32_t)(p * 0x01000000u + srcElem)) {
-          ok = false;
-          break;
+    uint32_t e = 0;
+    int numa = -1;
+    {
+      Communicator cx(comm);
+      ProxyService proxy;
+      std::vector<std::shared_future<Connection>> cf;
+      std::vector<int> peers;
+      RegisteredMemory srcMem = cx.registerMemory(src, bytes, Transport::CudaIpc);
+      RegisteredMemory dstMem = cx.registerMemory(dst, bytes, Transport::CudaIpc);
+      std::vector<std::shared_future<RegisteredMemory>> remote;
+      for (int q = 0; q < n; ++q) {
+        if (q == rank) continue;
+        peers.push_back(q);
+        cf.push_back(cx.connect(Transport::CudaIpc, q));
+        cx.sendMemory(dstMem, q);
+        remote.push_back(cx.recvMemory(q));
+      }
+      const MemoryId srcId = proxy.addMemory(srcMem);
+      std::vector<PortChannelDeviceHandle> ch;
+      for (size_t i = 0; i < peers.size(); ++i) {
+        const SemaphoreId sid = proxy.buildAndAddSemaphore(cx, cf[i].get());
+        const MemoryId dstId = proxy.addMemory(remote[i].get());
+        ch.push_back(proxy.portChannel(sid, dstId, srcId).deviceHandle());
+      }
+      proxy.startProxy(true);
+      // channel c (peer q) moves my src chunk q to offset rank*chunk of q's dst
+      std::vector<uint64_t> offs;
+      for (int q : peers) offs.push_back((uint64_t)rank * chunk);
+      for (int q : peers) offs.push_back((uint64_t)q * chunk);
+      uint64_t* dOffs = nullptr;
+      HIPCHECK(hipMalloc((void**)&dOffs, offs.size() * 8));
+      HIPCHECK(hipMemcpy(dOffs, offs.data(), offs.size() * 8, hipMemcpyHostToDevice));
+      PortChannelDeviceHandle* dch = nullptr;
+      HIPCHECK(hipMalloc((void**)&dch, ch.size() * sizeof(ch[0])));
+      HIPCHECK(hipMemcpy(dch, ch.data(), ch.size() * sizeof(ch[0]), hipMemcpyHostToDevice));
+      hipStream_t st;
+      HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      comm->boot->barrier();
+      t0 = nowSec();
+      for (int i = 0; i < iters; ++i) {
+        if (mscclppAmdLaunchPortChannelPut(dch, (int)ch.size(), dOffs, dOffs + ch.size(), chunk, mode, st))
+          throw std::runtime_error("launch");
+      }
+      HIPCHECK(hipStreamSynchronize(st));
+      t1 = nowSec();
+      comm->boot->barrier();
+      // check: peer p's chunk addressed to me (its src chunk `rank`) sits at offset p*chunk of my dst
+      std::vector<uint32_t> back(bytes / 4);
+      HIPCHECK(hipMemcpy(back.data(), dst, bytes, hipMemcpyDeviceToHost));
+      for (int p = 0; p < n && ok; ++p) {
+        if (p == rank) continue;
+        for (size_t i = 0; i < chunk / 4; ++i) {
+          const size_t srcElem = (size_t)rank * (chunk / 4) + i;
+          if (back[(size_t)p * (chunk / 4) + i] != (uint32_t)(p * 0x01000000u + srcElem)) {
+            ok = false;
+            break;
+          }
         }
       }
+      HIPCHECK(hipMemcpy(&e, comm->err, 4, hipMemcpyDeviceToHost));
+      numa = proxy.proxyNumaNode();
+      proxy.stopProxy();
+      (void)hipStreamDestroy(st);
+      (void)hipFree(dOffs);
+      (void)hipFree(dch);
+      comm->boot->barrier();  // every peer is done with my buffers before the mappings close
     }
-    uint32_t e = 0;
-    HIPCHECK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost));
+    out[0] = (t1 - t0) * 1e6 / iters;
     out[1] = (ok && e == 0) ? 1.0 : 0.0;
-    out[2] = (double)proxy.numaNode();
-    proxy.stop();
-    for (int q = 0; q < n; ++q)
-      if (conns[q].stream) {
-        (void)hipStreamSynchronize(conns[q].stream);
-        (void)hipStreamDestroy(conns[q].stream);
-      }
-    (void)hipStreamDestroy(st);
-    comm->boot->barrier();
-    for (int q = 0; q < n; ++q)
-      if (q != rank) {
-        comm->forgetMapping(q, peerDst[q]);
-        comm->forgetMapping(q, peerTok[q]);
-      }
-    (void)hipFree(dOffs);
-    (void)hipFree(dch);
-    (void)hipFree(err);
-    (void)hipHostFree(flushDone);
-    (void)hipFree(tok);
-    (void)hipFree(expct);
+    out[2] = (double)numa;
     (void)hipFree(src);
     (void)hipFree(dst);
     return (int)ncclSuccess;
@@ -567,43 +383,46 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     HIPCHECK(hipStreamCreateWithFlags(&conn.stream, hipStreamNonBlocking));
     // MemoryId 0 = my buffer, 1 = next's scratch, 2 = next's buffer; semaphoreId = round
     void* mem[3] = {buff, peerScratch[next], peerBuff[next]};
-    Proxy proxy(comm->device, 512, [&](const ProxyTrigger& t, uint64_t pos) {  // ProxyService::handleTrigger
+    std::string proxyFailure;  // first copy / token failure on the proxy thread
+    Proxy proxy([&](ProxyTrigger t, uint64_t pos) {  // ProxyService::handleTrigger
       const int round = (int)t.fields.semaphoreId;
-      if (round < 0 || round > 1) return false;
+      if (round < 0 || round > 1) return ProxyHandlerResult::Continue;
       if (t.fields.type & kTriggerData) {
         const hipError_t e = proxyCopy((char*)mem[t.fields.dstMemoryId] + t.fields.dstOffset,
                                        (char*)mem[t.fields.srcMemoryId] + t.fields.srcOffset, t.fields.size,
                                        conn.stream);
-        if (e != hipSuccess)
-          warn("proxy copy failed: " + std::string(hipGetErrorString(e)) + " dst id " +
-               std::to_string(t.fields.dstMemoryId) + " off " + std::to_string(t.fields.dstOffset) + " size " +
-               std::to_string(t.fields.size));
+        if (e != hipSuccess && proxyFailure.empty())
+          proxyFailure = "proxy copy failed: " + std::string(hipGetErrorString(e)) + " dst id " +
+                         std::to_string(t.fields.dstMemoryId) + " off " + std::to_string(t.fields.dstOffset) +
+                         " size " + std::to_string(t.fields.size);
       }
       if (t.fields.type & kTriggerFlag) {
-        writers[round].signal((uint64_t*)peerTok[next] + round * n + rank, conn.stream);
+        try {
+          writers[round].signal((uint64_t*)peerTok[next] + round * n + rank, conn.stream);
+        } catch (const std::exception& ex) {
+          if (proxyFailure.empty()) proxyFailure = ex.what();
+        }
       }
       if (t.fields.type & kTriggerSync) {
         spinSync(conn.stream);
         __atomic_store_n(&flushDone[round * 8], pos + 1, __ATOMIC_RELEASE);
       }
-      return false;
-    });
+      return ProxyHandlerResult::Continue;
+    }, 512);
     proxy.start();
     const uint64_t budget = spinBudgetTicks();
     PortChannelDeviceHandle ch[4] = {};
     for (int round = 0; round < 2; ++round) {
       PortChannelDeviceHandle& snd = ch[round * 2];      // to next
       PortChannelDeviceHandle& rcv = ch[round * 2 + 1];  // from prev: only its semaphore is used
-      snd.semaphoreId = (uint32_t)round;
-      snd.src = 0;
-      snd.dst = (uint32_t)(1 + round);
-      snd.fifo = proxy.fifo().deviceHandle();
-      snd.flushDonePos = dFlushDone + round * 8;
-      snd.budget = budget;
-      snd.err = err;
-      snd.semaphore = {tok + round * n + next, expct + round * n + next};
+      snd.semaphoreId_ = (uint32_t)round;
+      snd.src_ = 0;
+      snd.dst_ = (uint32_t)(1 + round);
+      snd.fifo_ = proxy.fifo().deviceHandle(budget, err);
+      snd.flushDonePos_ = dFlushDone + round * 8;
+      snd.semaphore_ = {tok + round * n + next, expct + round * n + next, budget, err};
       rcv = snd;
-      rcv.semaphore = {tok + round * n + prev, expct + round * n + prev};
+      rcv.semaphore_ = {tok + round * n + prev, expct + round * n + prev, budget, err};
     }
     hipStream_t st;
     HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -661,7 +480,8 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     uint32_t e = 0;
     HIPCHECK(hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost));
     out[0] = (t1 - t0) * 1e6 / iters / graphLaunches;
-    out[1] = (ok && e == 0) ? 1.0 : 0.0;
+    if (!proxyFailure.empty()) warn("ring proxy: " + proxyFailure);
+    out[1] = (ok && e == 0 && proxyFailure.empty()) ? 1.0 : 0.0;
     out[2] = (double)proxy.numaNode();
     proxy.stop();
     (void)hipStreamSynchronize(conn.stream);
@@ -670,12 +490,7 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     (void)hipGraphDestroy(graph);
     (void)hipStreamDestroy(st);
     comm->boot->barrier();  // peers no longer touch my buffers / tokens
-    for (int r = 0; r < n; ++r)
-      if (r != rank) {
-        comm->forgetMapping(r, peerBuff[r]);
-        comm->forgetMapping(r, peerScratch[r]);
-        comm->forgetMapping(r, peerTok[r]);
-      }
+    peerBuff = peerScratch = peerTok = PeerBufs();
     (void)hipFree(gb);
     (void)hipFree(err);
     (void)hipHostFree(flushDone);

@@ -103,13 +103,11 @@ extern "C" int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int
     MemoryChannelDeviceHandle h[2];
     for (int r = 0; r < 2; ++r) {
       const int p = 1 - r;
-      h[r].semaphore_ = {tok + r, tok + p, exp + r};
+      h[r].semaphore_ = {tok + r, tok + p, exp + r, 200000000ull /* 2 s */, err};
       // packet modes: dst_ = peer's packet buffer; mode 2: dst_ = peer's data buffer
       h[r].dst_ = mode <= 1 ? pk[p] : (void*)b[p];
       h[r].src_ = b[r];
       h[r].packetBuffer_ = pk[r];
-      h[r].budget_ = 200000000ull;  // 2 s
-      h[r].err_ = err;
     }
     CK(hipMalloc((void**)&dch, sizeof(h)));
     CK(hipMemcpy(dch, h, sizeof(h), hipMemcpyHostToDevice));

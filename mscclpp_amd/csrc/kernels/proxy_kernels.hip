@@ -14,14 +14,21 @@ namespace mscclpp_amd {
 __global__ void hostOffloadKernel(int rank, FifoDeviceHandle fifo, Host2DeviceSemaphoreDeviceHandle* handles,
                                   int handleIndex, uint64_t budget, uint32_t* err) {
   const int tid = threadIdx.x;
+  fifo.budget = budget;
+  fifo.err = err;
   __syncthreads();
   if (tid == 0) {
     ProxyTrigger t;
     t.fst = (uint64_t)handleIndex;
     t.snd = 0;
-    fifo.push(t, budget, err);
+    fifo.push(t);
   }
-  if (tid != rank) handles[tid].wait(budget, err);
+  if (tid != rank) {
+    Host2DeviceSemaphoreDeviceHandle h = handles[tid];
+    h.budget = budget;
+    h.err = err;
+    h.wait();
+  }
 }
 
 // mode 0: put + signal per chunk; 1: putWithSignal; 2: putWithSignalAndFlush; then wait for the

@@ -385,3 +385,71 @@ def test_pipeline_then_scratch_collectives(built):
                 p.kill()
     for rank in range(n):
         assert got[rank] == [True] * 6 + [0], (rank, got[rank])
+
+
+def _churn_worker(rank, n, uid, q):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "10000")
+        import torch
+
+        import mscclpp_amd as m
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        L = m.lib()
+        import ctypes
+
+        bad, peak = 0, 0
+        for it in range(1000):
+            # a fresh device allocation per iteration, freed right after: hipMalloc hands the same
+            # address back again and again, each time a new allocation (new IPC handle)
+            p = ctypes.c_void_p()
+            m.check(L.mscclppAmdMalloc(ctypes.byref(p), 1 << 20), "malloc")
+            t = m.device_view(p.value, 1 << 20).view(torch.float32)
+            t.fill_(float(rank + it))
+            comm.all_reduce(t, t, algo="fullmesh" if it % 2 else "rsag_zc")
+            torch.cuda.synchronize()
+            exp = float(sum(r + it for r in range(n)))
+            bad += int((t != exp).sum().item())
+            regs, maps, retired = comm.registration_stats()
+            peak = max(peak, regs)
+            del t
+            m.check(L.mscclppAmdFree(p), "free")
+        regs, maps, retired = comm.registration_stats()
+        err = comm.device_error()
+        comm.destroy()
+        q.put((rank, (bad, peak, maps, err), None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_registration_churn_stays_bounded_and_exact(built):
+    """1000 freshly allocated buffers through the zero-copy and fullmesh
+    AllReduce (which register the user's buffers) stay exact without any explicit deregistration,
+    and the registration cache stays bounded (a buffer re-allocated at the same address is a new
+    registration; at most 64 stay registered)."""
+    import mscclpp_amd as m
+
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    uid = m.Communicator.unique_id()
+    procs = [ctx.Process(target=_churn_worker, args=(r, n, uid, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=240)
+            assert err is None, err
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        bad, peak, maps, err = got[rank]
+        assert bad == 0 and err == 0, (rank, got[rank])
+        assert peak <= 64, (rank, got[rank])
+        assert maps <= 80, (rank, got[rank])

@@ -1,0 +1,52 @@
+"""The host channel API and the reference's device spellings:
+
+* tests/cpp/test_fifo.hip -- the FIFO known-answer tests of test/unit/fifo_tests.cu:15-162 on the
+  device FIFO with the host poller (10k pushes fst = snd = i, zero triggers, lap-wrap parity with the
+  commit bit cleared, rejection of a non-power-of-two size);
+* tests/cpp/test_channels.hip -- two processes building MemoryChannels and PortChannels with
+  Communicator::connect / registerMemory / sendMemory / recvMemory / MemoryDevice2DeviceSemaphore /
+  ProxyService, driven by kernels written with the reference's spellings (LL8/LL16 packet ping-pong
+  of test/mp_unit/memory_channel_tests.cu:246-325, unpackPacket, put/get ping-pong, the proxy LL
+  ping-pong of port_channel_tests.cu:337-446 with copyToPackets / copyFromPackets);
+* tests/cpp/test_customized_allgather.hip -- the reference's plugin example
+  (examples/customized-collective-algorithm/customized_allgather.cu) with PortChannels through
+  ProxyService, reached through ncclAllGather, direct and graph-captured, exact."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "bin")
+
+
+def _run(name, args, timeout):
+    env = dict(os.environ, MSCCLPP_AMD_SPIN_TIMEOUT_MS="10000")
+    r = subprocess.run([os.path.join(BIN, name)] + args, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=timeout, env=env)
+    assert r.returncode == 0, r.stdout[-4000:]
+    return r.stdout
+
+
+def test_fifo_rejects_non_power_of_two(built):
+    assert "reject OK" in _run("test_fifo", ["cpu"], 60)
+
+
+@pytest.mark.gpu
+def test_fifo_known_answers_on_device(built):
+    out = _run("test_fifo", ["gpu"], 120)
+    for part in ("reject OK", "fifo OK", "zero OK", "wrap OK", "gpu OK"):
+        assert part in out, out
+
+
+@pytest.mark.gpu
+def test_memory_and_port_channels_reference_spellings(built):
+    out = _run("test_channels", ["gpu", str(1 << 20)], 200)
+    assert "gpu OK" in out and "rank 0 OK" in out and "rank 1 OK" in out, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 4])
+def test_customized_allgather_port_channels(built, n):
+    out = _run("test_customized_allgather", ["gpu", str(n), str(1 << 18)], 200)
+    assert "gpu OK" in out and all(f"rank {r} OK" in out for r in range(n)), out
