@@ -239,6 +239,10 @@ def progress(msg):
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+FULL_NAMES = {"packet": "default_allreduce_packet", "allpair": "default_allreduce_allpair_packet",
+              "fullmesh": "default_allreduce_fullmesh", "rsag": "default_allreduce_rsag",
+              "rsag_zc": "default_allreduce_rsag_zero_copy", "rsag_pipeline": "default_allreduce_rsag_pipeline"}
+
 SCALING_NOTE = ("n_gpus=1 measures BASELINE configs[1] (the 1-GPU LL16 pack+sum+unpack of a 48 MiB fp16 bucket, "
                 "S / kernel-step time); n_gpus>1 measures configs[2] (AllReduce algbw S / t of a 48 MiB fp16 bucket per "
                 "rank over xGMI).  Different workloads: the 1 -> N ratio is not the scaling efficiency of one workload.")
@@ -502,6 +506,13 @@ def bench_multi(args):
         "correct": ok,
         "correct_bitexact": bitexact,
     }
+    # the winner in the tuned-config format of python/mscclpp_benchmark/tuning_config.py, to be loaded
+    # with MSCCLPP_AMD_TUNED_CONFIG (or merged into the built-in table, host/tuning.cpp)
+    res["tuned_config"] = {"version": 1, "profiles": [{"sku": torch.cuda.get_device_name(dev), "scale": n,
+                                                       "collectives": {"allreduce": [
+                                                           {"message_size": S, "algorithm": FULL_NAMES[algo],
+                                                            "nblocks": nb, "nthreads": nt,
+                                                            "time_us": round(t * 1e6, 2)}]}}]}
     mc = probe.get("allpairs_algbw_ceiling_measured")
     if mc:
         res["xgmi"]["frac_of_measured_ceiling"] = round(algbw / mc, 4)
@@ -599,6 +610,11 @@ def graph_time_per_call(fn, calls=20, replays=10, sync=None):
     return _time_calls(g.replay, replays) / calls
 
 
+def ndev_shared(n):
+    """True in a rehearsal where n ranks share fewer devices (grids must then fit together)."""
+    return torch.cuda.device_count() < n
+
+
 def bench_extras(args, comm, n, dev, tmax, barrier):
     """BASELINE configs[3] (LL latency sweep, fp16 1 KiB..1 MiB) and configs[4] (fp32 1 GiB
     RS+AG in ring order), timed the same way; failures are recorded, not raised."""
@@ -632,6 +648,33 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         extras["ll_latency_graph_us"] = glat
     except Exception as e:
         extras["ll_latency_error"] = str(e)
+    progress("extras: bulk size sweep")
+    try:
+        # per message size, the best of the bulk algorithms at two shapes each (fp16): the data for
+        # the tuned-config table (host/tuning.cpp) above the LL range
+        sweep = {}
+        big = torch.rand((256 << 20) // 2, device=dev).half()
+        bout = torch.empty_like(big)
+        for mb in (2, 4, 8, 16, 32, 64, 128, 256):
+            xs, os_ = big[: (mb << 20) // 2], bout[: (mb << 20) // 2]
+            row = {}
+            for a, nb_, nt_ in (("fullmesh", 64, 512), ("fullmesh", 128, 512), ("rsag_zc", 64, 512),
+                                ("rsag_zc", 128, 512), ("rsag_pipeline", 32, 512), ("rsag_pipeline", 64, 512)):
+                if ndev_shared(n) and nb_ * (2 if a == "rsag_pipeline" else 1) * n > 256:
+                    continue
+                try:
+                    for _ in range(2):
+                        comm.all_reduce(xs, os_, algo=a, nblocks=nb_, nthreads=nt_)
+                    row[f"{a}:{nb_}x{nt_}"] = round(tmax(_time_calls(
+                        lambda: comm.all_reduce(xs, os_, algo=a, nblocks=nb_, nthreads=nt_), 5)) * 1e6, 1)
+                except Exception as e:  # noqa: BLE001
+                    row[f"{a}:{nb_}x{nt_}"] = str(e)[:80]
+            best = min((v, k) for k, v in row.items() if isinstance(v, float))
+            sweep[f"{mb}MiB"] = {"us": row, "best": best[1], "algbw_GBs": round((mb << 20) / best[0] / 1e3, 1)}
+        extras["bulk_size_sweep"] = sweep
+        del big, bout
+    except Exception as e:
+        extras["bulk_size_sweep_error"] = str(e)[-300:]
     progress("extras: fp32 1 GiB rsag")
     try:
         S = 1 << 30

@@ -129,8 +129,17 @@ int mscclppAmdCollectiveLaunch(int coll, int algo, const mscclppAmdRankView* vie
  * mscclppAmdScratchRequiredShape. */
 size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype);
 size_t mscclppAmdScratchRequiredShape(int algo, int nranks, size_t bytes, int dtype, int nblocks, int nthreads);
-/* Algorithm the selector picks (algorithm_selector.cc:91-139 restated for gfx950). */
+/* Algorithm the selector picks: the tuned-config store's entry for this SKU, rank count and size
+ * (built-in table = algorithm_selector.cc:91-139, AMD branch), MSCCLPP_AMD_ALGO_*. */
 int mscclppAmdSelectAlgo(int nranks, size_t bytes, int dtype);
+/* Tuned-config store (the JSON format of python/mscclpp_benchmark/tuning_config.py): load a file
+ * whose profiles take precedence over the built-in table (as MSCCLPP_AMD_TUNED_CONFIG=<path> does at
+ * start-up), and query the entry for a collective ("allreduce", "allgather", "reducescatter") of
+ * `bytes` on `nranks` ranks: algorithm name and launch shape (0 = default).  Query returns 5 when no
+ * entry applies. */
+int mscclppAmdTunedConfigLoad(const char* path);
+int mscclppAmdTunedConfig(const char* collective, int nranks, size_t bytes, char* algorithm, size_t algorithmLen,
+                          int* nblocks, int* nthreads);
 
 /* ---- communicator extensions -------------------------------------------------------------- */
 int mscclppAmdCommAllReduce(ncclComm_t comm, const void* sendbuff, void* recvbuff, size_t count, int ncclDtype,

@@ -99,6 +99,9 @@ def lib():
         "mscclppAmdSelfReduceLL16": [vp, vp, vp, vp, sz, i32, i32, vp, i32, u64, vp, vp],
         "mscclppAmdAllReduceLaunch": [i32, ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, i32, u64, vp],
         "mscclppAmdSelectAlgo": [i32, sz, i32],
+        "mscclppAmdTunedConfigLoad": [ctypes.c_char_p],
+        "mscclppAmdTunedConfig": [ctypes.c_char_p, i32, sz, ctypes.c_char_p, sz, ctypes.POINTER(i32),
+                                  ctypes.POINTER(i32)],
         "mscclppAmdCollectiveLaunch": [i32, i32, ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, i32, u64, vp],
         "ncclReduceScatter": [vp, vp, sz, i32, i32, vp, vp],
         "ncclAllGather": [vp, vp, sz, i32, vp, vp],
@@ -202,6 +205,21 @@ def self_reduce_ll16(x, y, pkts_ptr, out, flags, err, op=SUM, nblocks=0, budget_
         ctypes.c_void_p(out.data_ptr()), nbytes, reduce_code(x.dtype, accum), op, ctypes.c_void_p(flags.data_ptr()),
         nblocks, budget_ticks or 200_000_000, ctypes.c_void_p(err.data_ptr()), stream_ptr(stream))
     check(code, "self_reduce_ll16")
+
+
+def tuned_config(collective, nranks, nbytes):
+    """(algorithm name, nblocks, nthreads) the tuned-config store picks, or None."""
+    name = ctypes.create_string_buffer(128)
+    nb, nt = ctypes.c_int(), ctypes.c_int()
+    rc = lib().mscclppAmdTunedConfig(collective.encode(), nranks, nbytes, name, 128, ctypes.byref(nb), ctypes.byref(nt))
+    if rc == 5:
+        return None
+    check(rc, "tuned config")
+    return name.value.decode(), nb.value, nt.value
+
+
+def load_tuned_config(path):
+    check(lib().mscclppAmdTunedConfigLoad(os.fsencode(path)), f"tuned config {path}")
 
 
 def scratch_required(algo, nranks, nbytes, dtype_code):

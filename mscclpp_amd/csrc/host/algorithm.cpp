@@ -215,10 +215,21 @@ struct BuiltinCtx {
 // handle to it and the key is the buffer pair (algorithm.cc:52-60).
 std::shared_ptr<Algorithm> builtin(ncclComm* comm, const std::string& name, const std::string& collective, int code,
                                    int coll, size_t minBytes, size_t maxBytes) {
-  auto kernel = [code, coll](const std::shared_ptr<void> ctx, const void* in, void* out, size_t inSize, size_t outSize,
-                             DataType dtype, ReduceOp op, hipStream_t stream, int nBlocks, int nThreads,
-                             const std::unordered_map<std::string, uintptr_t>&, DataType accum) -> CommResult {
+  auto kernel = [code, coll, name, collective](const std::shared_ptr<void> ctx, const void* in, void* out,
+                                               size_t inSize, size_t outSize, DataType dtype, ReduceOp op,
+                                               hipStream_t stream, int nBlocks, int nThreads,
+                                               const std::unordered_map<std::string, uintptr_t>&,
+                                               DataType accum) -> CommResult {
     ncclComm* c = std::static_pointer_cast<BuiltinCtx>(ctx)->comm;
+    if (nBlocks <= 0 && nThreads <= 0) {  // the tuned launch shape of this algorithm, if any
+      std::string tuned;
+      int nb = 0, nt = 0;
+      const size_t msg = inSize;  // the request's messageSize for all three (nccl.cc:586, :697, :748)
+      if (tunedConfig(collective, c->nranks, msg, tuned, nb, nt) && tuned == name) {
+        nBlocks = nb;
+        nThreads = nt;
+      }
+    }
     if (coll == 2) {  // AllGather moves bytes: the element type only sets the unit
       if (inSize == 0 || outSize != inSize * (size_t)c->nranks) return CommResult::CommInvalidArgument;
       return asResult(c->bulkCollective(2, in, out, inSize, MSCCLPP_AMD_F32, MSCCLPP_AMD_SUM, code, nBlocks,
@@ -270,12 +281,19 @@ std::shared_ptr<Algorithm> lookup(const AlgoMapByCollective& m, const std::strin
 
 std::shared_ptr<Algorithm> defaultAlgoSelector(const AlgoMapByCollective& algoMap, const CollectiveRequest& request) {
   if (request.nRanksPerNode != request.worldSize) return nullptr;  // multi-node: not this path (:163-175)
-  if (request.collective == "allreduce") {
+  if (request.collective == "allreduce")
     if (const char* forced = envAlgoName()) return lookup(algoMap, "allreduce", forced);
-    const char* name = request.messageSize <= ((size_t)1 << 14)   ? "default_allreduce_allpair_packet"
-                       : request.messageSize <= ((size_t)1 << 20) ? "default_allreduce_packet"
-                                                                  : "default_allreduce_fullmesh";
-    return lookup(algoMap, "allreduce", name);
+  // the tuned-config store (tuning.cpp): user profiles for this SKU / rank count, then the built-in
+  // table restating the AMD thresholds of algorithm_selector.cc:107-131
+  std::string name;
+  int nb = 0, nt = 0;
+  if (tunedConfig(request.collective, request.worldSize, request.messageSize, name, nb, nt))
+    if (auto a = lookup(algoMap, request.collective, name.c_str())) return a;
+  if (request.collective == "allreduce") {
+    const char* def = request.messageSize <= ((size_t)1 << 14)   ? "default_allreduce_allpair_packet"
+                      : request.messageSize <= ((size_t)1 << 20) ? "default_allreduce_packet"
+                                                                 : "default_allreduce_fullmesh";
+    return lookup(algoMap, "allreduce", def);
   }
   if (request.collective == "allgather") return lookup(algoMap, "allgather", "default_allgather_fullmesh2");
   if (request.collective == "reducescatter")

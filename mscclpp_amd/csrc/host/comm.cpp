@@ -140,11 +140,20 @@ size_t mscclppAmdScratchRequiredShape(int algo, int nranks, size_t bytes, int dt
   return 2 * (size_t)nranks * (size_t)nblocks * (size_t)nthreads * 4 * 16;
 }
 
-// algorithm_selector.cc:91-139 for an AMD node: <= 16 KiB one-hop LL8, <= 1 MiB two-hop LL16,
-// larger buckets the bulk all-pairs path.
+// The tuned-config store (tuning.cpp): the built-in table is algorithm_selector.cc:91-139 for an
+// AMD node (<= 16 KiB one-hop LL8, <= 1 MiB two-hop LL16, larger buckets the bulk all-pairs path);
+// MSCCLPP_AMD_TUNED_CONFIG / mscclppAmdTunedConfigLoad profiles for this SKU and rank count come first.
 int mscclppAmdSelectAlgo(int nranks, size_t bytes, int dtype) {
-  (void)nranks;
   (void)dtype;
+  std::string name;
+  int nb = 0, nt = 0;
+  try {
+    if (tunedConfig("allreduce", nranks, bytes, name, nb, nt)) {
+      const int code = algoCodeOf(name);
+      if (code > 0) return code;
+    }
+  } catch (...) {
+  }
   if (bytes <= ((size_t)1 << 14)) return MSCCLPP_AMD_ALGO_ALLPAIR;
   if (bytes <= ((size_t)1 << 20)) return MSCCLPP_AMD_ALGO_PACKET;
   return MSCCLPP_AMD_ALGO_FULLMESH;

@@ -185,6 +185,11 @@ namespace host {
 std::shared_ptr<void> openIpcHandle(const hipIpcMemHandle_t& handle);
 size_t liveIpcMappings();
 uint64_t allocationId(const void* ptr);  // HIP_POINTER_ATTRIBUTE_BUFFER_ID (0 if unknown)
+// Tuned configuration (tuning.cpp) for a collective of `bytes` on `nranks` ranks of this device's
+// SKU: the algorithm name and launch shape (0 = the algorithm's default); false if none.
+bool tunedConfig(const std::string& collective, int nranks, uint64_t bytes, std::string& algorithm, int& nblocks,
+                 int& nthreads);
+int algoCodeOf(const std::string& name);  // MSCCLPP_AMD_ALGO_* of a default_allreduce_* name, or -1
 }  // namespace host
 }  // namespace mscclpp_amd
 
@@ -400,6 +405,18 @@ struct ncclComm {
     boot->barrier();
   }
 
+  // The tuned launch shape of `algo` for this message, when the caller left the shape open and the
+  // tuned entry names the same algorithm.
+  void applyTunedShape(const char* coll, int algo, size_t bytes, int& nblocks, int& nthreads) {
+    if (nblocks > 0 || nthreads > 0) return;
+    std::string name;
+    int nb = 0, nt = 0;
+    if (tunedConfig(coll, nranks, bytes, name, nb, nt) && algoCodeOf(name) == algo) {
+      nblocks = nb;
+      nthreads = nt;
+    }
+  }
+
   mscclppAmdRankView baseView(const void* in, void* out) {
     mscclppAmdRankView v{};
     v.input = in;
@@ -417,7 +434,10 @@ struct ncclComm {
                 hipStream_t stream) {
     std::lock_guard<std::mutex> lk(mu);
     if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = envAlgo();
-    if (algo == MSCCLPP_AMD_ALGO_AUTO) algo = mscclppAmdSelectAlgo(nranks, bytes, dtype);
+    if (algo == MSCCLPP_AMD_ALGO_AUTO) {
+      algo = mscclppAmdSelectAlgo(nranks, bytes, dtype);
+      applyTunedShape("allreduce", algo, bytes, nblocks, nthreads);
+    }
     // the pipelined RS+AG carries 2- and 4-byte types only; others take fullmesh, which carries all
     if (algo == MSCCLPP_AMD_ALGO_RSAG_PIPELINE && dtype != MSCCLPP_AMD_F16 && dtype != MSCCLPP_AMD_BF16 &&
         dtype != MSCCLPP_AMD_F32 && dtype != MSCCLPP_AMD_I32 && dtype != MSCCLPP_AMD_U32)

@@ -32,6 +32,16 @@ CASES_4 = [
     ("allreduce_rres_n4.json", "f32", 1 << 15, "LL16", 2),
     ("allreduce_put_n4.json", "f16", 1 << 14, "LL16", 2),
 ]
+# the reference's own 2-rank plans (test/execution-files, committed as fixtures under plans/ref/):
+# the LL packet AllReduce (ppkt / respkt / upkt, double scratch) and the memory-channel AllReduce
+# (rres + signal / wait, 16 chunks per rank)
+CASES_REF = [
+    ("ref/allreduce_packet.json", "f16", 1 << 16, "LL16", 3),
+    ("ref/allreduce_packet.json", "bf16", 1 << 12, "LL8", 2),
+    ("ref/allreduce_packet.json", "f32", 1 << 14, "LL16", 2),
+    ("ref/allreduce.json", "f16", 1 << 19, "LL16", 3),
+    ("ref/allreduce.json", "f32", 1 << 16, "LL16", 2),
+]
 DT = {"f16": 0, "bf16": 1, "f32": 2}
 
 
@@ -134,3 +144,8 @@ def test_executor_two_ranks(built):
 
 def test_executor_four_ranks(built):
     _compare(4, CASES_4, _run(4, CASES_4))
+
+
+def test_executor_reference_plans(built):
+    """The reference's own execution plans, two ranks, bit-exact against the oracle's simulation."""
+    _compare(2, CASES_REF, _run(2, CASES_REF))

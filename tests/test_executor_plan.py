@@ -16,6 +16,10 @@ import executor_oracle as E  # noqa: E402
 
 GENERATED = sorted(f for f in os.listdir(PLANS) if f.endswith(".json"))
 REF_PLANS = "/root/reference/test/execution-files"
+# The reference's own plan files (test/execution-files/allreduce*.json), committed as data fixtures
+# (sha256 in tests/golden/plans/ref/SOURCE.txt) so that the GPU box, which has no /root/reference,
+# can run them too.
+REF_FIXTURES = os.path.join(PLANS, "ref")
 
 
 def _nranks(doc):
@@ -48,11 +52,21 @@ def test_lowering_matches_oracle(built, fname):
     _check_plan(built, os.path.join(PLANS, fname))
 
 
-@pytest.mark.skipif(not os.path.isdir(REF_PLANS), reason="reference plans only exist in the build container")
 @pytest.mark.parametrize("fname", ["allreduce_packet.json", "allreduce.json"])
 def test_lowering_of_reference_plans(built, fname):
-    """The reference's own plan files, read where they lie (never copied into this repo)."""
-    _check_plan(built, os.path.join(REF_PLANS, fname))
+    """The reference's own plan files (the committed fixtures; where /root/reference exists, they
+    must still be byte-identical to the files there)."""
+    path = os.path.join(REF_FIXTURES, fname)
+    if os.path.isdir(REF_PLANS):
+        with open(path, "rb") as a, open(os.path.join(REF_PLANS, fname), "rb") as b:
+            assert a.read() == b.read()
+    _check_plan(built, path)
+
+
+@pytest.mark.parametrize("fname", ["allreduce_packet.json", "allreduce.json"])
+@pytest.mark.parametrize("dtype", ["i32", "u32"])
+def test_oracle_known_answer_reference_plans(fname, dtype):
+    test_oracle_known_answer(os.path.join("ref", fname), dtype)
 
 
 @pytest.mark.parametrize("fname", GENERATED)
