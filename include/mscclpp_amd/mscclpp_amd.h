@@ -167,6 +167,11 @@ int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear);
  * synchronize before they close.  Any pointer may be NULL. */
 int mscclppAmdCommRegistrationStats(ncclComm_t comm, size_t* userRegistrations, size_t* liveMappings,
                                     size_t* retiredMappings);
+/* Host all-gathers made by user-buffer registration so far: one per newly registered allocation,
+ * one per new buffer offset inside a registered allocation (none when the communicator runs with
+ * MSCCLPP_NCCL_SYMMETRIC_MEMORY, env.hpp:101-107, which *symmetricMemory reports). */
+int mscclppAmdCommRegistrationExchanges(ncclComm_t comm, uint64_t* allocationExchanges, uint64_t* offsetExchanges,
+                                        int* symmetricMemory);
 int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes);
 int mscclppAmdCommFlags(ncclComm_t comm, uint32_t** flags);
 /* Bootstrap all-gather of `bytes` per rank (host memory), for harnesses. */

@@ -129,6 +129,8 @@ def lib():
         "mscclppAmdCommGetDeviceError": [vp, ctypes.POINTER(ctypes.c_uint32), i32],
         "mscclppAmdCommScratch": [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)],
         "mscclppAmdCommRegistrationStats": [vp, ctypes.POINTER(sz), ctypes.POINTER(sz), ctypes.POINTER(sz)],
+        "mscclppAmdCommRegistrationExchanges": [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                                ctypes.POINTER(ctypes.c_int)],
         "mscclppAmdCommFlags": [vp, ctypes.POINTER(vp)],
         "mscclppAmdCommAllGatherHost": [vp, vp, vp, sz],
         "mscclppAmdProxyRingAllReduce": [vp, sz, i32, i32, i32, ctypes.POINTER(ctypes.c_double)],
@@ -440,6 +442,13 @@ class Communicator:
         check(lib().mscclppAmdCommRegistrationStats(self.comm, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
               "registration stats")
         return a.value, b.value, c.value
+
+    def registration_exchanges(self):
+        """(allocation exchanges, offset exchanges, symmetric memory on) of user-buffer registration."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        check(lib().mscclppAmdCommRegistrationExchanges(self.comm, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+              "registration exchanges")
+        return a.value, b.value, bool(c.value)
 
     def destroy(self):
         if self.comm:

@@ -487,6 +487,16 @@ int mscclppAmdCommRegistrationStats(ncclComm_t comm, size_t* userRegistrations, 
   return ncclSuccess;
 }
 
+int mscclppAmdCommRegistrationExchanges(ncclComm_t comm, uint64_t* allocationExchanges, uint64_t* offsetExchanges,
+                                        int* symmetricMemory) {
+  if (!comm) return ncclInvalidArgument;
+  std::lock_guard<std::mutex> lk(comm->mu);
+  if (allocationExchanges) *allocationExchanges = comm->allocExchanges;
+  if (offsetExchanges) *offsetExchanges = comm->offsetExchanges;
+  if (symmetricMemory) *symmetricMemory = comm->symmetricMemory ? 1 : 0;
+  return ncclSuccess;
+}
+
 int mscclppAmdCommScratch(ncclComm_t comm, void** scratch, size_t* bytes) {
   if (!comm || !scratch || !bytes) return ncclInvalidArgument;
   *scratch = comm->llScratch;

@@ -158,6 +158,17 @@ inline int opFromNccl(ncclRedOp_t op) {
   return -1;
 }
 
+// MSCCLPP_NCCL_SYMMETRIC_MEMORY (env.hpp:101-107, env.cpp:67; any value but "0" is true): every rank
+// allocates its communication buffers symmetrically, so a buffer sits at the same offset inside its
+// allocation on every rank.  Registration then needs no host exchange for a new buffer inside an
+// allocation that is already registered (the reference caches one context per allocation in that
+// mode and passes the offset to the kernel, allreduce_fullmesh.cu:206-208, :248-257).
+inline bool envSymmetricMemory() {
+  const char* e = std::getenv("MSCCLPP_AMD_NCCL_SYMMETRIC_MEMORY");
+  if (!e) e = std::getenv("MSCCLPP_NCCL_SYMMETRIC_MEMORY");
+  return e && std::string(e) != "0";
+}
+
 inline int envAlgo() {
   const char* e = std::getenv("MSCCLPP_AMD_ALGO");
   if (!e) return MSCCLPP_AMD_ALGO_AUTO;
@@ -313,6 +324,9 @@ struct ncclComm {
   };
   std::map<std::pair<uint64_t, uint64_t>, UserReg> userRegs;
   uint64_t useClock = 0;
+  bool symmetricMemory = envSymmetricMemory();
+  // host all-gathers the registration path made: allocations exchanged, offsets exchanged
+  uint64_t allocExchanges = 0, offsetExchanges = 0;
 
   void retireReg(std::map<std::pair<uint64_t, uint64_t>, UserReg>::iterator it) {
     for (auto& m : it->second.bases.maps)
@@ -341,6 +355,7 @@ struct ncclComm {
       UserReg reg;
       reg.bufferId = bid;
       reg.bases = exchange(base);  // collective: every rank registers its matching buffer now
+      ++allocExchanges;
       it = userRegs.emplace(key, std::move(reg)).first;
     }
     UserReg& reg = it->second;
@@ -349,9 +364,13 @@ struct ncclComm {
     auto pit = reg.byOffset.find(off);
     if (pit == reg.byOffset.end()) {
       // The offset of `out` inside its allocation may differ between ranks: exchange offsets (cheap)
-      // to build exact pointers.
-      std::vector<uint64_t> offs(nranks);
-      boot->allGather(&off, offs.data(), sizeof(off));
+      // to build exact pointers -- unless the application declared symmetric allocation, where it
+      // is the same on every rank and this call stays local.
+      std::vector<uint64_t> offs(nranks, off);
+      if (!symmetricMemory) {
+        boot->allGather(&off, offs.data(), sizeof(off));
+        ++offsetExchanges;
+      }
       std::array<void*, MSCCLPP_AMD_MAX_RANKS> res{};
       for (int r = 0; r < nranks; ++r) res[r] = (r == rank) ? out : (char*)reg.bases[r] + offs[r];
       pit = reg.byOffset.emplace(off, res).first;

@@ -453,3 +453,80 @@ def test_registration_churn_stays_bounded_and_exact(built):
         assert bad == 0 and err == 0, (rank, got[rank])
         assert peak <= 64, (rank, got[rank])
         assert maps <= 80, (rank, got[rank])
+
+
+def _symmetric_worker(rank, n, uid, symmetric, q):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "10000")
+        if symmetric:
+            os.environ["MSCCLPP_NCCL_SYMMETRIC_MEMORY"] = "1"
+        else:
+            os.environ.pop("MSCCLPP_NCCL_SYMMETRIC_MEMORY", None)
+        os.environ.pop("MSCCLPP_AMD_NCCL_SYMMETRIC_MEMORY", None)
+        import ctypes
+
+        import torch
+
+        import mscclpp_amd as m
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        L = m.lib()
+        nslots, slot = 16, 1 << 19  # 16 sub-buffers of 512 KiB in one 8 MiB allocation
+        p = ctypes.c_void_p()
+        m.check(L.mscclppAmdMalloc(ctypes.byref(p), nslots * slot), "malloc")
+        whole = m.device_view(p.value, nslots * slot).view(torch.float32)
+        whole.fill_(-1.0)
+        per = slot // 4
+        bad = 0
+        for rnd in range(2):
+            for k in range(nslots):
+                t = whole[k * per:(k + 1) * per]
+                t.fill_(float(rank * 100 + k + rnd))
+                comm.all_reduce(t, t, algo="fullmesh" if (k + rnd) % 2 else "rsag_zc")
+            torch.cuda.synchronize()
+            for k in range(nslots):
+                exp = float(sum(r * 100 + k + rnd for r in range(n)))
+                bad += int((whole[k * per:(k + 1) * per] != exp).sum().item())
+        allocs, offs, sym = comm.registration_exchanges()
+        err = comm.device_error()
+        del whole
+        comm.destroy()
+        m.check(L.mscclppAmdFree(p), "free")
+        q.put((rank, (bad, allocs, offs, sym, err), None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("symmetric", [True, False])
+def test_symmetric_memory_registration(built, symmetric):
+    """MSCCLPP_NCCL_SYMMETRIC_MEMORY (env.hpp:101-107): buffers at the same offset of one allocation
+    on every rank.  16 sub-buffers of one allocation through fullmesh and zero-copy AllReduce (both
+    register the user's buffers): exact either way; the allocation is exchanged once, and new offsets
+    cost one host all-gather each only without the symmetric declaration."""
+    import mscclpp_amd as m
+
+    n = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    uid = m.Communicator.unique_id()
+    procs = [ctx.Process(target=_symmetric_worker, args=(r, n, uid, symmetric, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=180)
+            assert err is None, err
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        bad, allocs, offs, sym, err = got[rank]
+        assert bad == 0 and err == 0, (rank, got[rank])
+        assert sym == symmetric
+        assert allocs == 1, (rank, got[rank])
+        assert offs == (0 if symmetric else 16), (rank, got[rank])
