@@ -277,7 +277,7 @@ class BitExactChecker:
             self.inputs[key] = [O.lcg(self.dt, nbytes // O.itemsize(self.dt), r, seq) for r in range(self.n)]
         return self.inputs[key]
 
-    def expected(self, algo, nb, nt, seq, nbytes=None):
+    def expected(self, algo, nb, nt, seq, nbytes=None, rank=0):
         import mscclpp_amd as m
 
         O, n = self.O, self.n
@@ -285,13 +285,15 @@ class BitExactChecker:
         count = S // O.itemsize(self.dt)
         ins = self._ins(seq, S)
         if algo in ("packet", "allpair"):
-            key = (algo, seq, S)
+            # one-hop LL8 (allpair): every rank sums all inputs itself, own first, so the ranks' fp16
+            # results differ from each other for n > 2; two-hop LL16 (packet): the owner's sum everywhere
+            key = (algo, seq, S, rank)
             if key not in self.cache:
                 code = m.ALGO_PACKET if algo == "packet" else m.ALGO_ALLPAIR
                 half = m.scratch_required(code, n, S, self.dt) // 2
                 fn = O.allreduce_packet if algo == "packet" else O.allreduce_allpairs
                 outs, _ = fn(self.dt, O.SUM, ins, count, 1, half)
-                self.cache[key] = outs[0][: (S + 3) // 4].copy()
+                self.cache[key] = outs[rank][: (S + 3) // 4].copy()
             return self.cache[key]
         nw = (S + 15) // 16 * 4
         if algo == "rsag_pipeline":
@@ -364,9 +366,16 @@ def bench_multi(args):
         poison(o)
         comm.all_reduce(a1, o, algo=algo, nblocks=nb, nthreads=nt)
         torch.cuda.synchronize()
-        exp = checker.expected(algo, nb, nt, 1, nbytes)
+        exp = checker.expected(algo, nb, nt, 1, nbytes, rank)
         got = BitExactChecker.words(o)
-        return all_ok(bool(np.array_equal(got, exp)) and comm.device_error() == 0)
+        same = bool(np.array_equal(got, exp))
+        if not same:  # say where on stderr (the JSON line carries the verdict per candidate)
+            bad = np.nonzero(got != exp)[0]
+            sw = ((got.size * 4 + n - 1) // n + 15) // 16 * 4
+            print(f"bench: rank {rank} {algo} {nb}x{nt}: {bad.size} of {got.size} words differ, first {int(bad[0])} "
+                  f"(slice {int(bad[0]) // sw}), slices {sorted(set((bad // sw).tolist()))[:8]}, "
+                  f"{int((got[bad] == 0xFFFFFFFF).sum())} poisoned", file=sys.stderr)
+        return all_ok(same and comm.device_error() == 0)
 
     # ---- pick the algorithm and launch shape (untimed; every rank tries the same candidates in the
     # same order).  Large buckets: the scratch-based all-pairs RS+AG (fullmesh, puts), the zero-copy
@@ -378,15 +387,20 @@ def bench_multi(args):
                                            if sel in ("fullmesh", "rsag_zc", "rsag_pipeline") else [sel])
     cands = []
     shared = ndev < world  # rehearsal: ranks share a device, so every rank's grid must fit on it at once
+    # rehearsal shapes: small enough that every rank's grid is resident on the one shared device
+    bulk_shapes = ((64, 512), (128, 512), (256, 512), (128, 256), (256, 256)) if not shared else \
+        tuple((nb_, 512) for nb_ in (16, 32, 64, 128) if nb_ * world <= 256)
+    pipe_shapes = ((32, 512), (64, 512), (128, 512), (64, 256)) if not shared else \
+        tuple((nb_, 512) for nb_ in (8, 16, 32, 64) if 2 * nb_ * world <= 256)
     for a in algos:
         if a in ("fullmesh", "rsag", "rsag_zc"):
-            cands += [(a, nb_, nt_) for nb_, nt_ in ((64, 512), (128, 512), (256, 512), (128, 256), (256, 256))
-                      if not shared or nb_ * world <= 256]
+            cands += [(a, nb_, nt_) for nb_, nt_ in bulk_shapes]
         elif a == "rsag_pipeline":  # nblocks = reduce workgroups; the launch is 2x that
-            cands += [(a, nb_, nt_) for nb_, nt_ in ((32, 512), (64, 512), (128, 512), (64, 256))
-                      if not shared or 2 * nb_ * world <= 256]
+            cands += [(a, nb_, nt_) for nb_, nt_ in pipe_shapes]
         else:
             cands.append((a, 0, 0))
+    if not cands:
+        raise SystemExit(f"bench: no launch shape fits {world} ranks on {ndev} device(s)")
     tune = {}
     progress(f"tuning {len(cands)} candidates")
     for a, nb, nt in cands:
@@ -658,10 +672,12 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         for mb in (2, 4, 8, 16, 32, 64, 128, 256):
             xs, os_ = big[: (mb << 20) // 2], bout[: (mb << 20) // 2]
             row = {}
-            for a, nb_, nt_ in (("fullmesh", 64, 512), ("fullmesh", 128, 512), ("rsag_zc", 64, 512),
-                                ("rsag_zc", 128, 512), ("rsag_pipeline", 32, 512), ("rsag_pipeline", 64, 512)):
-                if ndev_shared(n) and nb_ * (2 if a == "rsag_pipeline" else 1) * n > 256:
-                    continue
+            shapes = (("fullmesh", 64, 512), ("fullmesh", 128, 512), ("rsag_zc", 64, 512),
+                      ("rsag_zc", 128, 512), ("rsag_pipeline", 32, 512), ("rsag_pipeline", 64, 512))
+            if ndev_shared(n):  # rehearsal: every rank's grid resident on the shared device
+                shapes = tuple((a, max(8, 256 // ((2 if a == "rsag_pipeline" else 1) * n) // k), 512)
+                               for a, k in (("fullmesh", 1), ("rsag_zc", 1), ("rsag_pipeline", 1)))
+            for a, nb_, nt_ in shapes:
                 try:
                     for _ in range(2):
                         comm.all_reduce(xs, os_, algo=a, nblocks=nb_, nthreads=nt_)

@@ -213,6 +213,13 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
       info("rank " + std::to_string(rank) + ": tokens mapped; allocating LL scratch");
       for (int r = 0; r < nranks; ++r) c->peerTokens[r] = (uint64_t*)c->peerTok[r];
       c->ensure(c->llScratch, c->llBytes, c->peerLL, (size_t)64 << 20);
+      // The bulk scratch at its final size now (the reference allocates its scratch once at init
+      // too, nccl.cc:180, :299): every bulk algorithm fits its need into 1 GiB (more passes or
+      // fewer pipeline stages beyond), so it is never re-allocated -- and never re-exported -- while
+      // the communicator runs.  Re-exporting a fresh allocation mid-run through hipIpcGetMemHandle
+      // misbehaved here (8 processes on one GPU): an import that mapped the previous allocation,
+      // or `invalid argument` from the export itself (tools/multi_rank_check.py).
+      c->ensure(c->bulkScratch, c->bulkBytes, c->peerBulk, bulkScratchInitBytes());
     }
     c->buildAlgorithms();
     initFallbackComm(c.get());  // vendor communicator for operations outside this path (nccl.cc:323-346)

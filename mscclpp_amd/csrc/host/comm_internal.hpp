@@ -112,6 +112,14 @@ inline uint64_t spinBudgetTicks() {
   return t;
 }
 
+// MSCCLPP_AMD_BULK_SCRATCH_MB (default 1024): the bulk scratch allocated at communicator init.
+inline size_t bulkScratchInitBytes() {
+  const char* e = std::getenv("MSCCLPP_AMD_BULK_SCRATCH_MB");
+  size_t mb = e ? std::strtoull(e, nullptr, 10) : 1024;
+  if (mb < 64) mb = 64;
+  return mb << 20;
+}
+
 inline void* allocUncached(size_t bytes) {
   void* p = nullptr;
   HIPCHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
@@ -260,6 +268,9 @@ struct ncclComm {
     void* base = nullptr;
     size_t sz = 0;
     HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)ptr));
+    if (std::getenv("MSCCLPP_AMD_DEBUG_IPC"))
+      std::fprintf(stderr, "ipc rank %d export ptr %p base %p bytes %zu id %llu\n", rank, ptr, base, sz,
+                   (unsigned long long)allocationId(base));
     HIPCHECK(hipIpcGetMemHandle(&mine.handle, base));
     info("rank " + std::to_string(rank) + ": got ipc handle, all-gather");
     mine.base = (uint64_t)base;
@@ -276,6 +287,20 @@ struct ncclComm {
       res.maps[(size_t)r] = openIpcHandle(all[r].handle);
       res[r] = (char*)res.maps[(size_t)r].get() + all[r].offset;
     }
+    if (std::getenv("MSCCLPP_AMD_DEBUG_IPC")) {  // one line per peer: what was imported and where
+      for (int r = 0; r < nranks; ++r) {
+        if (r == rank) continue;
+        std::string hex;
+        const unsigned char* h = reinterpret_cast<const unsigned char*>(&all[r].handle);
+        for (size_t i = 0; i < sizeof(all[r].handle); ++i) {
+          char b[3];
+          std::snprintf(b, sizeof b, "%02x", h[i]);
+          hex += b;
+        }
+        std::fprintf(stderr, "ipc rank %d peer %d base %llx bytes %llu handle %s mapped %p\n", rank, r,
+                     (unsigned long long)all[r].base, (unsigned long long)all[r].bytes, hex.c_str(), res.maps[(size_t)r].get());
+      }
+    }
     return res;
   }
 
@@ -290,6 +315,12 @@ struct ncclComm {
   }
 
   // Grow a scratch region collectively (every rank calls with the same size at the same call).
+  // The outgrown buffer is kept allocated until the communicator is destroyed: freeing it let the
+  // allocator hand its address range to the new buffer, and peers that imported the new buffer's
+  // IPC handle then wrote through a mapping of the OLD memory (8 processes, one GPU: after the
+  // bulk scratch grew 64 -> 128 MiB, two ranks' peers wrote the pipeline's stages into the old
+  // buffer, tools/multi_rank_check.py).  Growth is geometric, so what is kept is at most the final size.
+  std::vector<void*> outgrown;
   void ensure(void*& buf, size_t& have, PeerBufs& peers, size_t need) {
     if (need <= have) return;
     size_t want = have ? have : (size_t)64 << 20;
@@ -297,7 +328,7 @@ struct ncclComm {
     HIPCHECK(hipDeviceSynchronize());
     boot->barrier();  // every rank has drained its previous use of the old buffers
     peers = PeerBufs();  // our mappings of the peers' old buffers close here
-    if (buf) HIPCHECK(hipFree(buf));
+    if (buf) outgrown.push_back(buf);
     buf = allocUncached(want);
     have = want;
     peers = exchange(buf);
@@ -568,6 +599,8 @@ struct ncclComm {
     retired.clear();
     if (llScratch) (void)hipFree(llScratch);
     if (bulkScratch) (void)hipFree(bulkScratch);
+    for (void* p : outgrown) (void)hipFree(p);
+    outgrown.clear();
     if (tokens) (void)hipFree(tokens);
     if (expected) (void)hipFree(expected);
     if (flags) (void)hipFree(flags);

@@ -530,3 +530,67 @@ def test_symmetric_memory_registration(built, symmetric):
         assert sym == symmetric
         assert allocs == 1, (rank, got[rank])
         assert offs == (0 if symmetric else 16), (rank, got[rank])
+
+
+def _reimport_worker(rank, n, uid, q):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "10000")
+        import ctypes
+
+        import torch
+
+        import mscclpp_amd as m
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        L = m.lib()
+        bad, addrs = 0, set()
+        for it in range(40):
+            p = ctypes.c_void_p()
+            m.check(L.mscclppAmdMalloc(ctypes.byref(p), 1 << 20), "malloc")
+            addrs.add(p.value)
+            t = m.device_view(p.value, 1 << 20).view(torch.float32)
+            t.fill_(float(rank + 3 * it))
+            comm.all_reduce(t, t, algo=("fullmesh", "rsag_zc", "rsag")[it % 3])
+            torch.cuda.synchronize()
+            bad += int((t != float(sum(r + 3 * it for r in range(n)))).sum().item())
+            # every rank closes its imports of the peers' buffers BEFORE the peers free them and
+            # allocate the next one (very likely at the same address): the next import of that
+            # address must map the new memory
+            comm.deregister_all()
+            del t
+            m.check(L.mscclppAmdFree(p), "free")
+        err = comm.device_error()
+        comm.destroy()
+        q.put((rank, (bad, len(addrs), err), None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_reimport_after_close_at_the_same_address(built, n):
+    """A peer buffer imported, closed, freed and re-allocated at the same address is imported
+    afresh (the failure the scratch growth showed: an import of the new handle that mapped the old
+    memory).  40 rounds over fullmesh / zero-copy / rsag, exact."""
+    import mscclpp_amd as m
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    uid = m.Communicator.unique_id()
+    procs = [ctx.Process(target=_reimport_worker, args=(r, n, uid, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=180)
+            assert err is None, err
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        bad, naddr, err = got[rank]
+        assert bad == 0 and err == 0, (rank, got[rank])
