@@ -116,24 +116,60 @@ __device__ __forceinline__ void report_error_detail(uint32_t* err, uint32_t code
   }
 }
 
+// Release / acquire with the wait the fence needs on gfx950 (MI355X_MICROARCH.md, "Compiler hazard"
+// and the acquire row of the fence table).  A release fence writes the XCD's L2 back
+// (`buffer_wbl2`) and an acquire fence invalidates (`buffer_inv`); both complete asynchronously.
+// With a release ATOMIC alone the compiler drops the wait after the write-back whenever the wave's
+// vmcnt is provably empty (e.g. after a waited load of the peer's token address), and the signal
+// then overtakes the write-back: here 8 in-process ranks lost the plain stores of two workgroups
+// (mscclpp-test allreduce5), which the peers on the same XCD had already read.  So: fence, explicit
+// `s_waitcnt vmcnt(0)`, then a RELAXED atomic -- and after an acquire fence the same wait, so the
+// invalidate has completed before the workgroup barrier releases the other waves' loads.
+__device__ __forceinline__ void release_sys() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void release_agent() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void acquire_sys() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void acquire_agent() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Relaxed system-scope 64-bit load / store / add (global_* sc0 sc1), used for tokens and flags.
 __device__ __forceinline__ uint64_t ld_relaxed_sys(const uint64_t* p) {
   return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// A load that later loads of this wave may depend on (one acquire per call: poll with
+// ld_relaxed_sys in loops and acquire once after them where the loop is hot).
 __device__ __forceinline__ uint64_t ld_acquire_sys(const uint64_t* p) {
-  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t v = __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  acquire_sys();
+  return v;
 }
 __device__ __forceinline__ void st_relaxed_sys(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void st_release_sys(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  release_sys();
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint64_t add_release_sys(uint64_t* p, uint64_t v) {
-  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  release_sys();
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint64_t add_relaxed_sys(uint64_t* p, uint64_t v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t add_release_agent(uint64_t* p, uint64_t v) {
+  release_agent();
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace mscclpp_amd

@@ -78,12 +78,13 @@ struct FifoDeviceHandle {
     (void)maxSpinCount;
     SpinGuard g(budget ? budget : kDefaultSpinTicks);
     uint64_t v;
-    while (fifoHead >= (v = ld_acquire_sys(tail))) {
+    while (fifoHead >= (v = ld_relaxed_sys(tail))) {
       if (g.expired()) {
         report_error(err, kErrFifoTimeout);
         return;
       }
     }
+    acquire_sys();
     __hip_atomic_store(tailCache, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __device__ __forceinline__ bool poll(uint64_t fifoHead) {

@@ -22,12 +22,13 @@ namespace detail {
 // flushDonePos = pos + 1 once the connection drained (port_channel_device.hpp:21-30).
 __device__ __forceinline__ void waitFlush(uint64_t* flushDonePos, uint64_t fifoPos, uint64_t budget, uint32_t* err) {
   SpinGuard g(budget ? budget : kDefaultSpinTicks);
-  while (ld_acquire_sys(flushDonePos) <= fifoPos) {
+  while (ld_relaxed_sys(flushDonePos) <= fifoPos) {
     if (g.expired()) {
       report_error(err, kErrFifoTimeout);
       return;
     }
   }
+  acquire_sys();
 }
 #endif
 }  // namespace detail

@@ -24,10 +24,7 @@ __device__ __forceinline__ bool spinUntilAtLeast(uint64_t* token, uint64_t want,
       return false;
     }
   }
-  if (acquire) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before later loads
-  }
+  if (acquire) acquire_sys();  // the invalidate completes before later loads
   return true;
 }
 }  // namespace detail

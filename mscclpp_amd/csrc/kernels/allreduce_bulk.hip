@@ -62,8 +62,7 @@ __device__ __forceinline__ void block_handshake(const mscclppAmdRankView& v, int
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
+    acquire_sys();  // the invalidate completes before the barrier
   }
   __syncthreads();
 }
@@ -370,19 +369,20 @@ struct PipeGeom {
 __device__ __forceinline__ void sem_release(uint64_t* c) {
   drain_stores();
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) add_release_agent(c, 1);
 }
 
 __device__ __forceinline__ void sem_acquire(uint64_t* c, uint64_t target, uint64_t budget, uint32_t* err) {
   if (threadIdx.x == 0) {
     SpinGuard g(budget);
-    while (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
       if (g.expired()) {
         report_error(err, kErrSemaphoreTimeout);
         break;
       }
     }
+    acquire_agent();
   }
   __syncthreads();
 }
@@ -430,7 +430,8 @@ __global__ void __launch_bounds__(512) allreduceRsAgPipelineKernel(Views<NV> vie
         }
       }
       sem_release(&toReduce[2 * p]);
-      if (tid == 0) __hip_atomic_fetch_add(&toReduce[2 * p + 1], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      // (thread 0's release above already wrote the L2 back and waited: a relaxed add stays behind it)
+      if (tid == 0) __hip_atomic_fetch_add(&toReduce[2 * p + 1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   } else if (bid < P + g.R) {  // ---- reduce
     const uint32_t b = bid - P, p = b / 2, sub = b % 2;

@@ -171,7 +171,7 @@ __device__ void handleBarrier(const Op& op, const Ctx& c) {
   const uint32_t n = op.nThreadBlocks;
   if (n > 1 && threadIdx.x == 0) {
     uint64_t* cnt = &c.syncers[op.syncer].count;
-    const uint64_t old = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t old = add_release_agent(cnt, 1);
     const uint64_t target = (old / n + 1) * n;
     SpinGuard g(c.budget);
     while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -181,7 +181,7 @@ __device__ void handleBarrier(const Op& op, const Ctx& c) {
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    acquire_agent();
   }
   __syncthreads();
 }
@@ -447,7 +447,7 @@ __device__ void handleSemRelease(const Op& op, const Ctx& c) {
   drain();
   __syncthreads();
   if (threadIdx.x < op.nSems)
-    __hip_atomic_fetch_add(&c.sems[op.semIds[threadIdx.x]].value, (int64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    add_release_agent(reinterpret_cast<uint64_t*>(&c.sems[op.semIds[threadIdx.x]].value), 1);
 }
 __device__ void handleSemAcquire(const Op& op, const Ctx& c) {
   if (threadIdx.x < op.nSems) {

@@ -68,13 +68,13 @@ __device__ __forceinline__ void grid_sync(GridBarrier* gb, uint64_t budget, uint
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t g = __hip_atomic_load(&gb->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    if (__hip_atomic_fetch_add(&gb->count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+    release_sys();  // this workgroup's stores are written back before it arrives
+    if (__hip_atomic_fetch_add(&gb->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
       __hip_atomic_store(&gb->count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&gb->gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&gb->gen, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       SpinGuard sg(budget);
-      while (__hip_atomic_load(&gb->gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+      while (__hip_atomic_load(&gb->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
         __builtin_amdgcn_s_sleep(1);
         if (sg.expired()) {
           report_error(err, kErrSemaphoreTimeout);
@@ -82,7 +82,7 @@ __device__ __forceinline__ void grid_sync(GridBarrier* gb, uint64_t budget, uint
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    acquire_sys();
   }
   __syncthreads();
 }

@@ -59,7 +59,45 @@ def test_k5_in_place(built, n, count):
         assert ranks.errors() == [0] * n
         want = np.sum(np.stack([a.astype(np.int64) for a in ins]), axis=0).astype(np.uint32)
         for r in range(n):
-            assert np.array_equal(bufs[r].cpu().numpy().view(np.uint32), want), f"rank {r}"
+            got = bufs[r].cpu().numpy().view(np.uint32)
+            if not np.array_equal(got, want):
+                # describe the mismatch: a second copy-out with no GPU work in between, then one after
+                # a device-side compare (a kernel reading the buffer)
+                bad = np.nonzero(got != want)[0]
+                torch.cuda.synchronize()
+                again = bufs[r].cpu().numpy().view(np.uint32)
+                dev_ok = bool(torch.equal(bufs[r], torch.from_numpy(want.view(np.int32)).cuda()))
+                third = bufs[r].cpu().numpy().view(np.uint32)
+                own = ins[r].view(np.uint32)
+                # the same call again on fresh copies of the inputs at the same addresses
+                for q in range(n):
+                    bufs[q].copy_(torch.from_numpy(ins[q].copy()))
+                torch.cuda.synchronize()
+                ranks.all_reduce(bufs, bufs, m.ALGO_TEST_K5, nblocks=24, nthreads=512)
+                torch.cuda.synchronize()
+                rerun = [bool(np.array_equal(b.cpu().numpy().view(np.uint32), want)) for b in bufs]
+                # is the memory itself healthy?  torch's own fill / copy kernels on the same buffer
+                bufs[r].fill_(12345)
+                torch.cuda.synchronize()
+                fill_ok = bool((bufs[r].cpu() == 12345).all())
+                src = torch.arange(count, dtype=torch.int32, device="cuda")
+                bufs[r].copy_(src)
+                torch.cuda.synchronize()
+                copy_ok = bool(torch.equal(bufs[r].cpu(), src.cpu()))
+                # the same k5 call on freshly allocated buffers, in this process state
+                fresh = [torch.from_numpy(a.copy()).cuda() for a in ins]
+                ranks.all_reduce(fresh, fresh, m.ALGO_TEST_K5, nblocks=24, nthreads=512)
+                torch.cuda.synchronize()
+                fresh_ok = [bool(np.array_equal(b.cpu().numpy().view(np.uint32), want)) for b in fresh]
+                fresh_addrs = [hex(b.data_ptr()) for b in fresh]
+                addrs = [hex(b.data_ptr()) for b in bufs] + [hex(t.ptr) for t in ranks.tokens]
+                raise AssertionError(
+                    f"rank {r} call {call}: {bad.size} words differ ({int(bad[0])}..{int(bad[-1])}), "
+                    f"{int((got[bad] == own[bad]).sum())} equal the rank's own input; second copy-out "
+                    f"ok={np.array_equal(again, want)}, device compare ok={dev_ok}, "
+                    f"copy-out after it ok={np.array_equal(third, want)}; rerun per rank {rerun}; "
+                    f"addresses {addrs}; allocated {torch.cuda.memory_allocated() >> 20} MiB; torch fill ok={fill_ok}, "
+                    f"copy ok={copy_ok}; fresh buffers {fresh_addrs} ok {fresh_ok}")
 
 
 def test_harness_kat(built):
