@@ -46,58 +46,65 @@ def test_ll_test_kernels_bit_exact(built, kernel, n, count):
                 assert np.array_equal(img, scr[r]), f"scratch image of rank {r}"
 
 
+def _k5_cases(cases, q):
+    """Child-process body of the k5 tests: [(n, count, seed, nblocks)] -> first mismatch or None."""
+    try:
+        import mscclpp_amd as m
+
+        torch.cuda.set_device(0)
+        for n, count, seed, nb in cases:
+            ranks = m.InProcessRanks(n, 1 << 16)
+            for call in range(3):
+                if seed is None:  # the harness known answer: input = rank
+                    ins = [np.full(count, r, dtype=np.int32) for r in range(n)]
+                else:
+                    ins = _rand_i32(n, count, seed + call)
+                bufs = [torch.from_numpy(a.copy()).cuda() for a in ins]
+                ranks.all_reduce(bufs, bufs, m.ALGO_TEST_K5, nblocks=nb, nthreads=512 if nb else 0)
+                torch.cuda.synchronize()
+                errs = ranks.errors()
+                if errs != [0] * n:
+                    q.put(f"n={n} count={count} call {call}: device errors {errs}")
+                    return
+                want = np.sum(np.stack([a.astype(np.int64) for a in ins]), axis=0).astype(np.uint32)
+                for r in range(n):
+                    got = bufs[r].cpu().numpy().view(np.uint32)
+                    if not np.array_equal(got, want):
+                        bad = np.nonzero(got != want)[0]
+                        q.put(f"n={n} count={count} call {call} rank {r}: {bad.size} words differ "
+                              f"({int(bad[0])}..{int(bad[-1])}), "
+                              f"{int((got[bad] == ins[r].view(np.uint32)[bad]).sum())} equal the rank's own input")
+                        return
+        q.put(None)
+    except Exception:
+        import traceback
+
+        q.put(traceback.format_exc())
+
+
+def _run_k5(cases):
+    """The k5 (in place) checks run in a fresh process.  In the full `-m gpu` session on this pool, a
+    torch-allocated buffer of the long-lived pytest process can stop receiving some of ANY kernel's
+    stores (torch's own fill_ included, while copies land and fresh allocations are fine; DESIGN.md
+    §21): the in-place k5 result then keeps parts of the input.  A fresh process sees the kernel."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_k5_cases, args=(cases, q))
+    p.start()
+    try:
+        res = q.get(timeout=240)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert res is None, res
+
+
 @pytest.mark.parametrize("n,count", [(2, 4096), (4, 65536), (8, 8192), (8, 1 << 18), (5, 640)])
 def test_k5_in_place(built, n, count):
-    import mscclpp_amd as m
-
-    ranks = m.InProcessRanks(n, 1 << 16)
-    for call in range(3):
-        ins = _rand_i32(n, count, 100 + call)
-        bufs = [torch.from_numpy(a.copy()).cuda() for a in ins]
-        ranks.all_reduce(bufs, bufs, m.ALGO_TEST_K5, nblocks=24, nthreads=512)
-        torch.cuda.synchronize()
-        assert ranks.errors() == [0] * n
-        want = np.sum(np.stack([a.astype(np.int64) for a in ins]), axis=0).astype(np.uint32)
-        for r in range(n):
-            got = bufs[r].cpu().numpy().view(np.uint32)
-            if not np.array_equal(got, want):
-                # describe the mismatch: a second copy-out with no GPU work in between, then one after
-                # a device-side compare (a kernel reading the buffer)
-                bad = np.nonzero(got != want)[0]
-                torch.cuda.synchronize()
-                again = bufs[r].cpu().numpy().view(np.uint32)
-                dev_ok = bool(torch.equal(bufs[r], torch.from_numpy(want.view(np.int32)).cuda()))
-                third = bufs[r].cpu().numpy().view(np.uint32)
-                own = ins[r].view(np.uint32)
-                # the same call again on fresh copies of the inputs at the same addresses
-                for q in range(n):
-                    bufs[q].copy_(torch.from_numpy(ins[q].copy()))
-                torch.cuda.synchronize()
-                ranks.all_reduce(bufs, bufs, m.ALGO_TEST_K5, nblocks=24, nthreads=512)
-                torch.cuda.synchronize()
-                rerun = [bool(np.array_equal(b.cpu().numpy().view(np.uint32), want)) for b in bufs]
-                # is the memory itself healthy?  torch's own fill / copy kernels on the same buffer
-                bufs[r].fill_(12345)
-                torch.cuda.synchronize()
-                fill_ok = bool((bufs[r].cpu() == 12345).all())
-                src = torch.arange(count, dtype=torch.int32, device="cuda")
-                bufs[r].copy_(src)
-                torch.cuda.synchronize()
-                copy_ok = bool(torch.equal(bufs[r].cpu(), src.cpu()))
-                # the same k5 call on freshly allocated buffers, in this process state
-                fresh = [torch.from_numpy(a.copy()).cuda() for a in ins]
-                ranks.all_reduce(fresh, fresh, m.ALGO_TEST_K5, nblocks=24, nthreads=512)
-                torch.cuda.synchronize()
-                fresh_ok = [bool(np.array_equal(b.cpu().numpy().view(np.uint32), want)) for b in fresh]
-                fresh_addrs = [hex(b.data_ptr()) for b in fresh]
-                addrs = [hex(b.data_ptr()) for b in bufs] + [hex(t.ptr) for t in ranks.tokens]
-                raise AssertionError(
-                    f"rank {r} call {call}: {bad.size} words differ ({int(bad[0])}..{int(bad[-1])}), "
-                    f"{int((got[bad] == own[bad]).sum())} equal the rank's own input; second copy-out "
-                    f"ok={np.array_equal(again, want)}, device compare ok={dev_ok}, "
-                    f"copy-out after it ok={np.array_equal(third, want)}; rerun per rank {rerun}; "
-                    f"addresses {addrs}; allocated {torch.cuda.memory_allocated() >> 20} MiB; torch fill ok={fill_ok}, "
-                    f"copy ok={copy_ok}; fresh buffers {fresh_addrs} ok {fresh_ok}")
+    _run_k5([(n, count, 100, 24)])
 
 
 def test_harness_kat(built):
@@ -105,11 +112,12 @@ def test_harness_kat(built):
     import mscclpp_amd as m
 
     n, count = 8, 1 << 14
-    for kernel in ("k5", "k6", "k7"):
+    _run_k5([(n, count, None, 0)])  # k5 (in place), default launch shape
+    for kernel in ("k6", "k7"):
         code = m.ALGO_NAMES[kernel]
         ranks = m.InProcessRanks(n, max(m.scratch_required(code, n, count * 4, m.I32), 1 << 16))
         ins = [torch.full((count,), r, dtype=torch.int32, device="cuda") for r in range(n)]
-        outs = ins if kernel == "k5" else [torch.empty_like(t) for t in ins]
+        outs = [torch.empty_like(t) for t in ins]
         ranks.all_reduce(ins, outs, code)
         torch.cuda.synchronize()
         assert ranks.errors() == [0] * n
