@@ -354,6 +354,14 @@ def bench_multi(args):
     def poison(t):
         t.view(torch.int16).fill_(-1)  # 0xFFFF: an fp16 NaN no correct sum of the LCG inputs produces
 
+    def device_matches(o, exp):
+        """The same comparison read by a KERNEL on this rank (through its L2), not by the copy engine:
+        peers' remote stores into this rank's output must be what its next kernel reads, with no
+        stale L2 line left over from the poison fill."""
+        want = torch.from_numpy(exp.view(np.int32).copy()).to(dev)
+        flat = o.detach().contiguous().view(torch.uint8)[: want.numel() * 4].view(torch.int32)
+        return bool(torch.equal(flat, want))
+
     def check_run(algo, nb, nt, nbytes=None):
         """Untimed: run once on seq 0, poison the output, run on seq 1, compare every word with the oracle."""
         if nbytes is None:
@@ -368,7 +376,7 @@ def bench_multi(args):
         torch.cuda.synchronize()
         exp = checker.expected(algo, nb, nt, 1, nbytes, rank)
         got = BitExactChecker.words(o)
-        same = bool(np.array_equal(got, exp))
+        same = bool(np.array_equal(got, exp)) and device_matches(o, exp)
         if not same:  # say where on stderr (the JSON line carries the verdict per candidate)
             bad = np.nonzero(got != exp)[0]
             sw = ((got.size * 4 + n - 1) // n + 15) // 16 * 4
@@ -448,8 +456,9 @@ def bench_multi(args):
     bitexact = {}
     if checker is not None:
         progress("bit-exact check of the timed step and of every tuned candidate")
-        exp = checker.expected(algo, nb, nt, 1)
-        bitexact["timed_last_step"] = all_ok(bool(np.array_equal(BitExactChecker.words(out), exp)) and errc == 0)
+        exp = checker.expected(algo, nb, nt, 1, None, rank)
+        bitexact["timed_last_step"] = all_ok(bool(np.array_equal(BitExactChecker.words(out), exp))
+                                             and device_matches(out, exp) and errc == 0)
         for a, cnb, cnt in cands:
             if tune[(a, cnb, cnt)] == float("inf"):
                 continue
