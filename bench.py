@@ -205,10 +205,10 @@ def bench_single(args):
         pk.free()
         return res
     res["staged_pcie_inclusive"] = staged_rate(m, S, x, y, out, pk, flags, err)
-    # BASELINE configs[1] sweep, 64 KiB .. 48 MiB: per-launch time with 20 launches captured in one
-    # HIP graph (device time, not host launch rate)
+    # BASELINE configs[1] sweep, 64 KiB .. 48 MiB in x2 steps: per-launch time with 20 launches
+    # captured in one HIP graph (device time, not host launch rate)
     sweep = {}
-    for sz in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 48 << 20):
+    for sz in [(64 << 10) << k for k in range(10)] + [48 << 20]:
         if sz > S:
             break
         xs, ys, os_ = x[: sz // 2], y[: sz // 2], out[: sz // 2]
@@ -463,6 +463,14 @@ def bench_multi(args):
             if tune[(a, cnb, cnt)] == float("inf"):
                 continue
             bitexact[f"{a}:{cnb}x{cnt}"] = check_run(a, cnb, cnt)
+        # in place (send == recv, BASELINE configs[2] names both): the winner once more
+        a1 = xs[1].clone()
+        comm.all_reduce(a1, a1, algo=algo, nblocks=nb, nthreads=nt)
+        torch.cuda.synchronize()
+        exp1 = checker.expected(algo, nb, nt, 1, None, rank)
+        bitexact[f"{algo}:{nb}x{nt}:in_place"] = all_ok(bool(np.array_equal(BitExactChecker.words(a1), exp1))
+                                                        and device_matches(a1, exp1) and comm.device_error() == 0)
+        del a1
         for a, nbytes in (("packet", 1 << 20), ("allpair", 16 << 10)):  # the LL paths (configs[3])
             try:
                 bitexact[f"{a}:{nbytes >> 10}KiB"] = check_run(a, 0, 0, nbytes)
@@ -484,6 +492,15 @@ def bench_multi(args):
     # writes S output + 2(n-1)/n S incoming scratch
     hbm = (2 * S if algo == "rsag_zc" else 2 * S * (1 + 2 * (n - 1) / n) if algo == "rsag_pipeline"
            else S * (1 + 3 * (n - 1) / n + 1 / n))
+    progress("graph-captured headline")
+    try:
+        # common.cc:202-227: 20 calls captured in one graph, 15 graph launches, per-call time
+        g_s = tmax(graph_time_per_call(lambda: comm.all_reduce(xs[0], out, algo=algo, nblocks=nb, nthreads=nt),
+                                       calls=20, replays=15, sync=dist.barrier))
+        graph = {"us_per_call": round(g_s * 1e6, 2), "algbw_GBs": round(S / g_s / 1e9, 2),
+                 "note": "20 calls per HIP graph, 15 launches (mscclpp-test common.cc:202-227); value stays the eager loop"}
+    except Exception as e:  # recorded, never fatal for the headline line
+        graph = {"error": str(e)[-300:]}
     progress("xGMI probe")
     try:
         probe = xgmi_probe(comm, n, dev, tmax, dist.barrier)
@@ -528,6 +545,7 @@ def bench_multi(args):
         "tune_ms": {f"{k[0]}:{k[1]}x{k[2]}": round(v * 1e3, 4) for k, v in tune.items()},
         "correct": ok,
         "correct_bitexact": bitexact,
+        "graph": graph,
     }
     # the winner in the tuned-config format of python/mscclpp_benchmark/tuning_config.py, to be loaded
     # with MSCCLPP_AMD_TUNED_CONFIG (or merged into the built-in table, host/tuning.cpp)
@@ -638,6 +656,9 @@ def ndev_shared(n):
     return torch.cuda.device_count() < n
 
 
+LL_SWEEP_KIB = tuple(1 << k for k in range(11))  # BASELINE configs[3]: 1 KiB .. 1 MiB, x2 steps
+
+
 def bench_extras(args, comm, n, dev, tmax, barrier):
     """BASELINE configs[3] (LL latency sweep, fp16 1 KiB..1 MiB) and configs[4] (fp32 1 GiB
     RS+AG in ring order), timed the same way; failures are recorded, not raised."""
@@ -645,7 +666,7 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
     progress("extras: LL latency sweep")
     try:
         lat = {}
-        for kb in (1, 4, 16, 64, 256, 1024):
+        for kb in LL_SWEEP_KIB:
             cnt = kb * 512
             xs = torch.rand(cnt, device=dev).half()
             os_ = torch.empty_like(xs)
@@ -663,7 +684,7 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         # 32 us for the first size, 3.3 us for the same size measured again) -- discard one
         xw = torch.rand(512, device=dev).half()
         graph_time_per_call(lambda: comm.all_reduce(xw, torch.empty_like(xw)), sync=barrier)
-        for kb in (1, 4, 16, 64, 256, 1024):
+        for kb in LL_SWEEP_KIB:
             cnt = kb * 512
             xs = torch.rand(cnt, device=dev).half()
             os_ = torch.empty_like(xs)
