@@ -34,6 +34,10 @@ enum {
   MSCCLPP_AMD_DT_FLOAT16 = 2,
   MSCCLPP_AMD_DT_FLOAT32 = 3,
   MSCCLPP_AMD_DT_BFLOAT16 = 4,
+  MSCCLPP_AMD_DT_FLOAT8_E4M3FN = 5,   /* OCP: gfx950's hardware format */
+  MSCCLPP_AMD_DT_FLOAT8_E4M3FNUZ = 6, /* not native on gfx950: rejected, as the reference does */
+  MSCCLPP_AMD_DT_FLOAT8_E5M2 = 7,     /* OCP */
+  MSCCLPP_AMD_DT_FLOAT8_E5M2FNUZ = 8, /* not native on gfx950: rejected */
 };
 /* mscclpp::PacketType (executor.hpp:15-18) */
 enum { MSCCLPP_AMD_PACKET_LL8 = 0, MSCCLPP_AMD_PACKET_LL16 = 1 };

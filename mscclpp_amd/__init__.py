@@ -461,10 +461,13 @@ class Communicator:
 class DataType:
     """mscclpp.DataType values (gpu_data_types.hpp:169-183)."""
     int32, uint32, float16, float32, bfloat16 = 0, 1, 2, 3, 4
+    float8_e4m3fn, float8_e4m3fnuz, float8_e5m2, float8_e5m2fnuz = 5, 6, 7, 8
 
 
 EXEC_DTYPES = {torch.int32: DataType.int32, torch.float16: DataType.float16, torch.float32: DataType.float32,
-               torch.bfloat16: DataType.bfloat16}
+               torch.bfloat16: DataType.bfloat16, torch.float8_e4m3fn: DataType.float8_e4m3fn,
+               torch.float8_e5m2: DataType.float8_e5m2, torch.float8_e4m3fnuz: DataType.float8_e4m3fnuz,
+               torch.float8_e5m2fnuz: DataType.float8_e5m2fnuz}
 
 
 class PacketType:

@@ -587,6 +587,15 @@ struct mscclppAmdExecutor {
       case MSCCLPP_AMD_DT_FLOAT16: dt = MSCCLPP_AMD_F16; break;
       case MSCCLPP_AMD_DT_FLOAT32: dt = MSCCLPP_AMD_F32; break;
       case MSCCLPP_AMD_DT_BFLOAT16: dt = MSCCLPP_AMD_BF16; break;
+      // the FP8 kernels of execution_kernel.hpp:949-1000 (T == AccumT); gfx950 converts the OCP
+      // formats in hardware and, like the reference on a platform without the other variant
+      // (:952-960, :975-983), rejects FNUZ
+      case MSCCLPP_AMD_DT_FLOAT8_E4M3FN: dt = MSCCLPP_AMD_E4M3; break;
+      case MSCCLPP_AMD_DT_FLOAT8_E5M2: dt = MSCCLPP_AMD_E5M2; break;
+      case MSCCLPP_AMD_DT_FLOAT8_E4M3FNUZ:
+      case MSCCLPP_AMD_DT_FLOAT8_E5M2FNUZ:
+        warn("execution plan: FNUZ fp8 is not natively supported on gfx950; use the OCP FLOAT8_E4M3FN / FLOAT8_E5M2");
+        return ncclInvalidUsage;
       default: return ncclInvalidArgument;
     }
     if (packetType != MSCCLPP_AMD_PACKET_LL8 && packetType != MSCCLPP_AMD_PACKET_LL16) return ncclInvalidArgument;

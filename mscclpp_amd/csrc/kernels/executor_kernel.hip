@@ -582,10 +582,23 @@ int launchExecutionKernel(const exec::TbPlan* plans, int nblocks, int nthreads, 
   if (nblocks <= 0 || nthreads <= 0 || nthreads > 1024 || nthreads % 64) return 4;
   // every workgroup of a plan may wait on another: the whole grid must be resident
   if (!grid_coresident(executionKernel<kF16, true, false>, nthreads, nblocks)) return 5;
-  const int op = kSum;
-  MSCCLPP_AMD_DISPATCH(dtype, op, launchT, plans, nblocks, nthreads, ldsBytes, (uint8_t*)input, (uint8_t*)output,
-                       (uint8_t*)scratch, scratchOffset, scratchChunk, flag, syncers, sems, budget, err, s, ll16,
-                       reuseScratch);
+  // the reduce operation is per plan operation: instantiate by dtype only (FP8 with T == AccumT)
+#define MSCCLPP_AMD_EXEC_CASE(DT)                                                                                \
+  case DT:                                                                                                        \
+    launchT<DT, kSum>(plans, nblocks, nthreads, ldsBytes, (uint8_t*)input, (uint8_t*)output, (uint8_t*)scratch,   \
+                      scratchOffset, scratchChunk, flag, syncers, sems, budget, err, s, ll16, reuseScratch);     \
+    break;
+  switch (dtype) {
+    MSCCLPP_AMD_EXEC_CASE(kF16)
+    MSCCLPP_AMD_EXEC_CASE(kBF16)
+    MSCCLPP_AMD_EXEC_CASE(kF32)
+    MSCCLPP_AMD_EXEC_CASE(kI32)
+    MSCCLPP_AMD_EXEC_CASE(kU32)
+    MSCCLPP_AMD_EXEC_CASE(kE4M3)
+    MSCCLPP_AMD_EXEC_CASE(kE5M2)
+    default: return 4;
+  }
+#undef MSCCLPP_AMD_EXEC_CASE
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -31,6 +31,7 @@ CASES_4 = [
     ("allreduce_pkt_n4.json", "f16", 1 << 16, "LL16", 3),
     ("allreduce_rres_n4.json", "f32", 1 << 15, "LL16", 2),
     ("allreduce_put_n4.json", "f16", 1 << 14, "LL16", 2),
+    ("allreduce_pkt_n4.json", "e4m3", 1 << 16, "LL8", 2),
 ]
 # the reference's own 2-rank plans (test/execution-files, committed as fixtures under plans/ref/):
 # the LL packet AllReduce (ppkt / respkt / upkt, double scratch) and the memory-channel AllReduce
@@ -41,8 +42,12 @@ CASES_REF = [
     ("ref/allreduce_packet.json", "f32", 1 << 14, "LL16", 2),
     ("ref/allreduce.json", "f16", 1 << 19, "LL16", 3),
     ("ref/allreduce.json", "f32", 1 << 16, "LL16", 2),
+    # OCP fp8 (execution_kernel.hpp:949-1000: the FP8 kernels, T == AccumT)
+    ("ref/allreduce_packet.json", "e4m3", 1 << 16, "LL16", 2),
+    ("ref/allreduce.json", "e5m2", 1 << 19, "LL16", 2),
 ]
-DT = {"f16": 0, "bf16": 1, "f32": 2}
+DT = {"f16": 0, "bf16": 1, "f32": 2, "e4m3": 5, "e5m2": 6}
+NP_VIEW = {"f32": np.int32, "e4m3": np.uint8, "e5m2": np.uint8}  # others: 16-bit
 
 
 def _worker(rank, n, uid, cases, q):
@@ -56,14 +61,15 @@ def _worker(rank, n, uid, cases, q):
         torch.cuda.set_device(0)
         comm = m.Communicator(rank, n, uid)
         ex = m.Executor(comm)
-        tdt = {"f16": torch.float16, "bf16": torch.bfloat16, "f32": torch.float32}
+        tdt = {"f16": torch.float16, "bf16": torch.bfloat16, "f32": torch.float32, "e4m3": torch.float8_e4m3fn,
+               "e5m2": torch.float8_e5m2}
         results = []
         for ci, (fname, dt, count, pkt, calls) in enumerate(cases):
             plan = m.ExecutionPlan(os.path.join(PLANS, fname), rank)
             outs = []
             for call in range(calls):
                 a = O.lcg(DT[dt], count, rank, 10 * ci + call)
-                x = torch.from_numpy(a.view(np.int16 if dt != "f32" else np.int32).copy()).view(tdt[dt]).cuda()
+                x = torch.from_numpy(a.view(NP_VIEW.get(dt, np.int16)).copy()).view(tdt[dt]).cuda()
                 y = x if plan.is_in_place() else torch.zeros_like(x)
                 stream = torch.cuda.current_stream()
                 ex.execute(rank, x.data_ptr(), y.data_ptr(), x.numel() * x.element_size(), y.numel() * y.element_size(),

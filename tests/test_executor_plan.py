@@ -162,3 +162,29 @@ def test_missing_or_malformed_file(built, tmp_path):
     bad.write_text("{\"name\": \"x\", ")
     with pytest.raises(m.MscclppError):
         m.ExecutionPlan(str(bad), 0)
+
+
+@pytest.mark.parametrize("fname", ["ref/allreduce_packet.json", "ref/allreduce.json", "allreduce_pkt_n4.json"])
+@pytest.mark.parametrize("dtype,one", [("e4m3", 0x38), ("e5m2", 0x3C)])
+def test_oracle_known_answer_fp8(fname, dtype, one):
+    """OCP fp8 through a plan: inputs of small integers (exact in fp8, as are all their partial sums
+    up to 8 ranks x 3), so every rank must end with the exact integer sum whatever the order."""
+    import oracle_lib as O
+
+    with open(os.path.join(PLANS, fname)) as f:
+        doc = json.load(f)
+    n = _nranks(doc)
+    eo = E.ExecutorOracle(doc, n)
+    nbytes = _sizes(doc)[1] * 8
+    rng = np.random.default_rng(7)
+    e5 = dtype == "e5m2"
+    top = 2 if e5 else 4  # inputs in [0, top): every partial sum stays an integer fp8 holds exactly
+    enc = {v: O.fp8_encode_sat(float(v), e5) for v in range(0, (top - 1) * n + 1)}
+    assert enc[1] == one and all(O.fp8_decode(b, e5) == float(v) for v, b in enc.items())
+    vals = rng.integers(0, top, size=(n, nbytes))
+    ins = [np.array([enc[int(v)] for v in vals[r]], dtype=np.uint8) for r in range(n)]
+    exp = np.array([enc[int(v)] for v in vals.sum(axis=0)], dtype=np.uint8)
+    outs = ins if doc["inplace"] else [np.zeros_like(a) for a in ins]
+    res = eo.execute([a.copy() for a in ins], [a.copy() for a in outs], dtype)
+    for r in range(n):
+        assert np.array_equal(res[r][0 if doc["inplace"] else 1], exp), r
