@@ -589,12 +589,13 @@ def xgmi_probe(comm, n, dev, tmax, barrier, S=64 << 20):
     nxt, prv = (rank + 1) % n, (rank - 1) % n
     vp, sz = ctypes.c_void_p, ctypes.c_size_t
 
-    def jobs(pairs, bpj):
+    def jobs(pairs, bpj, lp=0, sp=0):
         k = len(pairs)
         srcs = (vp * k)(*[p[0] for p in pairs])
         dsts = (vp * k)(*[p[1] for p in pairs])
         lens = (sz * k)(*[p[2] for p in pairs])
-        return lambda: m.check(L.mscclppAmdCopyJobs(srcs, dsts, lens, k, bpj, m.stream_ptr()), "copy jobs")
+        return lambda: m.check(L.mscclppAmdCopyJobsPolicy(srcs, dsts, lens, k, bpj, lp, sp, m.stream_ptr()),
+                               "copy jobs")
 
     def timed(fn, reps=5):
         fn()
@@ -618,11 +619,17 @@ def xgmi_probe(comm, n, dev, tmax, barrier, S=64 << 20):
     get = [(psrc[q] + ((q - rank - 1) % n) * chunk, base_d + i * chunk, chunk) for i, q in enumerate(peers)]
     t_ap = timed(jobs(put, bpj))
     t_ag = timed(jobs(get, bpj))
+    # what the cache policy of the remote accesses costs over the links (the collectives use sc0 sc1
+    # everywhere): all-pairs puts by store policy, all-pairs gets by load policy
+    pol = {"sys": 0, "plain": 1, "nt": 2, "agent": 3}
+    by_store = {k: round((n - 1) * chunk / timed(jobs(put, bpj, 0, v)) / 1e9, 1) for k, v in pol.items()}
+    by_load = {k: round((n - 1) * chunk / timed(jobs(get, bpj, v, 0)) / 1e9, 1) for k, v in pol.items()}
     barrier()
     out = {"bytes": S, "launch": "mscclppAmdCopyJobs, one stream", "ring_put_GBs": round(S / t_put / 1e9, 1),
            "ring_get_GBs": round(S / t_get / 1e9, 1),
            "allpairs_put_out_GBs": round((n - 1) * chunk / t_ap / 1e9, 1),
-           "allpairs_get_in_GBs": round((n - 1) * chunk / t_ag / 1e9, 1)}
+           "allpairs_get_in_GBs": round((n - 1) * chunk / t_ag / 1e9, 1),
+           "allpairs_put_out_GBs_by_store_policy": by_store, "allpairs_get_in_GBs_by_load_policy": by_load}
     # all-pairs AllReduce moves 2(n-1)/n * S out of every rank: its algbw ceiling at the measured rate
     out["allpairs_algbw_ceiling_measured"] = round(out["allpairs_put_out_GBs"] * n / (2 * (n - 1)), 1)
     del pdst, psrc

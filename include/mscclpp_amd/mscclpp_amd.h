@@ -110,6 +110,12 @@ int mscclppAmdSelfReduceLL16Variant(const void* x, const void* y, void* pkts, vo
 int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblocks, void* stream);
 int mscclppAmdCopyJobs(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs, int blocksPerJob,
                        void* stream);
+/* The same with the cache policy of the loads / stores: 0 = sc0 sc1 (system scope, what the
+ * collectives use for remote accesses), 1 = plain, 2 = nt, 3 = sc1 (agent scope).  Combinations
+ * carried: any store policy with system loads; plain or system stores with plain loads; system stores
+ * with nt or agent loads.  4 = a combination not carried. */
+int mscclppAmdCopyJobsPolicy(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs,
+                             int blocksPerJob, int loadPolicy, int storePolicy, void* stream);
 
 /* ---- explicit-view AllReduce ------------------------------------------------------------- */
 /* Launch `algo` for `nviews` ranks of an `nranks`-rank AllReduce in ONE kernel launch (views[i]

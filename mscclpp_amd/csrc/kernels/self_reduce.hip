@@ -186,7 +186,7 @@ struct CopyJobs {
   uint64_t units[MSCCLPP_AMD_MAX_RANKS * 2];
 };
 
-template <int U>
+template <int U, int LP = kSystem, int SP = kSystem>
 __global__ void __launch_bounds__(256) copyJobsKernel(CopyJobs jobs, uint32_t blocksPerJob) {
   const uint32_t j = blockIdx.x / blocksPerJob, jb = blockIdx.x % blocksPerJob;
   const uint8_t* src = jobs.src[j];
@@ -199,10 +199,10 @@ __global__ void __launch_bounds__(256) copyJobsKernel(CopyJobs jobs, uint32_t bl
     u32x4 w[U];
 #pragma unroll
     for (int k = 0; k < U; ++k)
-      if (u0 + k * 256 + threadIdx.x < nunits) w[k] = load16<kSystem>(rs, (k * 256 + threadIdx.x) * 16);
+      if (u0 + k * 256 + threadIdx.x < nunits) w[k] = load16<LP>(rs, (k * 256 + threadIdx.x) * 16);
 #pragma unroll
     for (int k = 0; k < U; ++k)
-      if (u0 + k * 256 + threadIdx.x < nunits) store16<kSystem>(rd, (k * 256 + threadIdx.x) * 16, w[k]);
+      if (u0 + k * 256 + threadIdx.x < nunits) store16<SP>(rd, (k * 256 + threadIdx.x) * 16, w[k]);
   }
 }
 
@@ -245,8 +245,20 @@ extern "C" int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblo
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+extern "C" int mscclppAmdCopyJobsPolicy(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs,
+                                        int blocksPerJob, int loadPolicy, int storePolicy, void* streamPtr);
+
 extern "C" int mscclppAmdCopyJobs(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs,
                                   int blocksPerJob, void* streamPtr) {
+  return mscclppAmdCopyJobsPolicy(srcs, dsts, bytes, njobs, blocksPerJob, 0, 0, streamPtr);
+}
+
+// The same copy with the cache policy of its loads / stores chosen (0 = sc0 sc1 system scope, the
+// policy of every remote access in the collectives; 1 = plain; 2 = nt; 3 = sc1 agent scope): the
+// xGMI probe measures what each policy delivers over the links.
+extern "C" int mscclppAmdCopyJobsPolicy(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs,
+                                        int blocksPerJob, int loadPolicy, int storePolicy, void* streamPtr) {
+  if (loadPolicy < 0 || loadPolicy > 3 || storePolicy < 0 || storePolicy > 3) return 4;
   if (!srcs || !dsts || !bytes || njobs < 1 || njobs > 2 * MSCCLPP_AMD_MAX_RANKS) return 4;
   if (blocksPerJob <= 0) blocksPerJob = 128;
   if ((long)blocksPerJob * njobs > 65535) return 4;
@@ -257,8 +269,21 @@ extern "C" int mscclppAmdCopyJobs(const void* const* srcs, void* const* dsts, co
     jobs.dst[j] = (uint8_t*)dsts[j];
     jobs.units[j] = bytes[j] / 16;
   }
-  hipLaunchKernelGGL((copyJobsKernel<4>), dim3(blocksPerJob * njobs), dim3(256), 0, (hipStream_t)streamPtr, jobs,
-                     (uint32_t)blocksPerJob);
+  const dim3 grid(blocksPerJob * njobs), block(256);
+  hipStream_t st = (hipStream_t)streamPtr;
+  const uint32_t bpj = (uint32_t)blocksPerJob;
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, 0, st, jobs, bpj); };
+  switch (loadPolicy * 4 + storePolicy) {  // loads of remote data: system or plain; stores: any
+    case 0: go(copyJobsKernel<4, kSystem, kSystem>); break;
+    case 1: go(copyJobsKernel<4, kSystem, kPlain>); break;
+    case 2: go(copyJobsKernel<4, kSystem, kNonTemporal>); break;
+    case 3: go(copyJobsKernel<4, kSystem, kAgent>); break;
+    case 4: go(copyJobsKernel<4, kPlain, kSystem>); break;
+    case 5: go(copyJobsKernel<4, kPlain, kPlain>); break;
+    case 8: go(copyJobsKernel<4, kNonTemporal, kSystem>); break;
+    case 12: go(copyJobsKernel<4, kAgent, kSystem>); break;
+    default: return 4;
+  }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
