@@ -526,6 +526,9 @@ def bench_multi(args):
                    "bytes": S, "parallelism": f"allreduce{world}", "algo": algo, "nblocks": nb, "nthreads": nt},
         "scaling_note": SCALING_NOTE,
         "busbw": round(algbw * 2 * (n - 1) / n, 2),
+        # the bytes all ranks contributed per AllReduce (n buckets of S) over the step time, beside
+        # the metric's algbw (S / t, one bucket per collective, nccl-tests' convention)
+        "aggregate_input_GBs": round(n * S / t / 1e9, 2),
         # the dominant kernel against the xGMI roofline: wire bytes per rank 2(n-1)S/n per launch over
         # the kernel's average launch time, priced against the all-pairs put rate measured on this
         # node in this run (one launch, workgroups partitioned by peer); the task-stated link rate
