@@ -492,6 +492,13 @@ def bench_multi(args):
     # writes S output + 2(n-1)/n S incoming scratch
     hbm = (2 * S if algo == "rsag_zc" else 2 * S * (1 + 2 * (n - 1) / n) if algo == "rsag_pipeline"
            else S * (1 + 3 * (n - 1) / n + 1 / n))
+    progress("xGMI probe")
+    try:
+        probe = xgmi_probe(comm, n, dev, tmax, dist.barrier)
+    except Exception as e:  # recorded, never fatal for the headline line
+        probe = {"error": str(e)[-300:]}
+    # after the probe: on a rehearsal box the graph's extra stream queues slow every later launch of
+    # the ranks sharing the device (the probe must not measure that)
     progress("graph-captured headline")
     try:
         # common.cc:202-227: 20 calls captured in one graph, 15 graph launches, per-call time
@@ -501,11 +508,6 @@ def bench_multi(args):
                  "note": "20 calls per HIP graph, 15 launches (mscclpp-test common.cc:202-227); value stays the eager loop"}
     except Exception as e:  # recorded, never fatal for the headline line
         graph = {"error": str(e)[-300:]}
-    progress("xGMI probe")
-    try:
-        probe = xgmi_probe(comm, n, dev, tmax, dist.barrier)
-    except Exception as e:  # recorded, never fatal for the headline line
-        probe = {"error": str(e)[-300:]}
     peak = probe.get("allpairs_put_out_GBs")
     kernel = {"rsag_zc": "allreduceZeroCopyKernel", "rsag_pipeline": "allreduceRsAgPipelineKernel"}.get(
         algo, f"allreduceBulkKernel ({algo})")
@@ -688,20 +690,6 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         extras["ll_latency_us"] = lat
     except Exception as e:
         extras["ll_latency_error"] = str(e)
-    try:
-        glat = {}
-        # the first graph a process times runs slow (a one-time cost, tools/ll_small_probe.py:
-        # 32 us for the first size, 3.3 us for the same size measured again) -- discard one
-        xw = torch.rand(512, device=dev).half()
-        graph_time_per_call(lambda: comm.all_reduce(xw, torch.empty_like(xw)), sync=barrier)
-        for kb in LL_SWEEP_KIB:
-            cnt = kb * 512
-            xs = torch.rand(cnt, device=dev).half()
-            os_ = torch.empty_like(xs)
-            glat[f"{kb}KiB"] = round(tmax(graph_time_per_call(lambda: comm.all_reduce(xs, os_), sync=barrier)) * 1e6, 2)
-        extras["ll_latency_graph_us"] = glat
-    except Exception as e:
-        extras["ll_latency_error"] = str(e)
     progress("extras: bulk size sweep")
     try:
         # per message size, the best of the bulk algorithms at two shapes each (fp16): the data for
@@ -744,6 +732,21 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         del xs, os_
     except Exception as e:
         extras["fp32_1GiB_rsag_error"] = str(e)
+    progress("extras: graph-captured LL latency sweep")
+    try:
+        glat = {}
+        # the first graph a process times runs slow (a one-time cost, tools/ll_small_probe.py:
+        # 32 us for the first size, 3.3 us for the same size measured again) -- discard one
+        xw = torch.rand(512, device=dev).half()
+        graph_time_per_call(lambda: comm.all_reduce(xw, torch.empty_like(xw)), sync=barrier)
+        for kb in LL_SWEEP_KIB:
+            cnt = kb * 512
+            xs = torch.rand(cnt, device=dev).half()
+            os_ = torch.empty_like(xs)
+            glat[f"{kb}KiB"] = round(tmax(graph_time_per_call(lambda: comm.all_reduce(xs, os_), sync=barrier)) * 1e6, 2)
+        extras["ll_latency_graph_us"] = glat
+    except Exception as e:
+        extras["ll_latency_error"] = str(e)
     progress("extras: mscclpp-test kernels")
     try:
         # the mscclpp-test kernels on the sizes the reference publishes (BASELINE.md §1,
