@@ -497,17 +497,6 @@ def bench_multi(args):
         probe = xgmi_probe(comm, n, dev, tmax, dist.barrier)
     except Exception as e:  # recorded, never fatal for the headline line
         probe = {"error": str(e)[-300:]}
-    # after the probe: on a rehearsal box the graph's extra stream queues slow every later launch of
-    # the ranks sharing the device (the probe must not measure that)
-    progress("graph-captured headline")
-    try:
-        # common.cc:202-227: 20 calls captured in one graph, 15 graph launches, per-call time
-        g_s = tmax(graph_time_per_call(lambda: comm.all_reduce(xs[0], out, algo=algo, nblocks=nb, nthreads=nt),
-                                       calls=20, replays=15, sync=dist.barrier))
-        graph = {"us_per_call": round(g_s * 1e6, 2), "algbw_GBs": round(S / g_s / 1e9, 2),
-                 "note": "20 calls per HIP graph, 15 launches (mscclpp-test common.cc:202-227); value stays the eager loop"}
-    except Exception as e:  # recorded, never fatal for the headline line
-        graph = {"error": str(e)[-300:]}
     peak = probe.get("allpairs_put_out_GBs")
     kernel = {"rsag_zc": "allreduceZeroCopyKernel", "rsag_pipeline": "allreduceRsAgPipelineKernel"}.get(
         algo, f"allreduceBulkKernel ({algo})")
@@ -550,7 +539,6 @@ def bench_multi(args):
         "tune_ms": {f"{k[0]}:{k[1]}x{k[2]}": round(v * 1e3, 4) for k, v in tune.items()},
         "correct": ok,
         "correct_bitexact": bitexact,
-        "graph": graph,
     }
     # the winner in the tuned-config format of python/mscclpp_benchmark/tuning_config.py, to be loaded
     # with MSCCLPP_AMD_TUNED_CONFIG (or merged into the built-in table, host/tuning.cpp)
@@ -565,6 +553,17 @@ def bench_multi(args):
         res["xgmi"]["probe_consistent"] = algbw <= mc * 1.02  # an AllReduce cannot beat the raw puts it is made of
     if not args.no_extras:
         res["extras"] = bench_extras(args, comm, n, dev, tmax, dist.barrier)
+    # last: on a rehearsal box (ranks sharing one device) the extra stream queues of a graph capture
+    # slow every later launch of those ranks, so nothing is measured after it
+    progress("graph-captured headline")
+    try:
+        # common.cc:202-227: 20 calls captured in one graph, 15 graph launches, per-call time
+        g_s = tmax(graph_time_per_call(lambda: comm.all_reduce(xs[0], out, algo=algo, nblocks=nb, nthreads=nt),
+                                       calls=20, replays=15, sync=dist.barrier))
+        res["graph"] = {"us_per_call": round(g_s * 1e6, 2), "algbw_GBs": round(S / g_s / 1e9, 2),
+                        "note": "20 calls per HIP graph, 15 launches (mscclpp-test common.cc:202-227); value stays the eager loop"}
+    except Exception as e:  # recorded, never fatal for the headline line
+        res["graph"] = {"error": str(e)[-300:]}
     # cpu_baseline is an N=1 field (the oracle timed on rank 0 at N=1 only); at N>1 the reference's
     # host-proxy path is reported by the mscclpp-test k1 row in extras
     comm.destroy()
