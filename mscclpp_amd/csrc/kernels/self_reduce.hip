@@ -151,10 +151,21 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
 template <int DT, int OP>
 static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                              int nblocks, uint64_t budget, uint32_t* err, hipStream_t stream) {
-  // LDS-staged packets, 2 KiB of payload per wave and round, partner tiles consumed one round late
-  hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, true, false>), dim3(nblocks), dim3(256), 0, stream,
-                     (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
-                     (uint32_t*)nullptr);
+  // LDS-staged packets, 2 KiB of payload per wave and round, partner tiles consumed one round late.
+  // Exactly two rounds per workgroup (e.g. 16 MiB on 1024 workgroups): the skew's drain round is a
+  // third round, and consuming in the same round is faster there (22.1 vs 25.2 us at 16 MiB; one
+  // round or four and more: the skewed form is as fast or faster, tools/sweep_self_reduce.py).
+  constexpr uint64_t kTile = 4 * 2 * 1024;  // 4 waves x U=2 KiB
+  const uint64_t tiles = (bytes + kTile - 1) / kTile;
+  const uint64_t rounds = (tiles + (uint64_t)nblocks - 1) / (uint64_t)nblocks;
+  if (rounds == 2)
+    hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, false, false>), dim3(nblocks), dim3(256), 0, stream,
+                       (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
+                       (uint32_t*)nullptr);
+  else
+    hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, true, false>), dim3(nblocks), dim3(256), 0, stream,
+                       (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
+                       (uint32_t*)nullptr);
 }
 
 // Streaming copy (read S, write S) used by the benchmark to measure the achievable HBM ceiling on

@@ -51,7 +51,8 @@ def _assert_equal_words(got, exp, dt):
 
 @pytest.mark.parametrize("dt,op", [(O.F16, O.SUM), (O.BF16, O.SUM), (O.F32, O.SUM), (O.I32, O.SUM),
                                    (O.F16, O.MIN), (O.BF16, O.MIN), (O.F32, O.MIN)])
-@pytest.mark.parametrize("nbytes,special", [(64 << 10, True), ((1 << 20) + 48, False), (4 << 20, True)])
+@pytest.mark.parametrize("nbytes,special", [(64 << 10, True), ((1 << 20) + 48, False), (4 << 20, True),
+                                            ((12 << 20) + 16, False)])  # two rounds per workgroup: unskewed form
 def test_self_reduce_bit_exact(built, dt, op, nbytes, special):
     import mscclpp_amd as m
 
