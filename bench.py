@@ -718,6 +718,42 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         del big, bout
     except Exception as e:
         extras["bulk_size_sweep_error"] = str(e)[-300:]
+    progress("extras: ReduceScatter / AllGather")
+    try:
+        # ncclReduceScatter / ncclAllGather (row f2) at the headline bucket: 48 MiB of fp16 in per rank
+        # for the reduce-scatter, its 48/n MiB result gathered back; both checked bit-exactly (the
+        # reduce-scatter in the fullmesh order own-then-ascending, the gather byte for byte)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+
+        blk = (args.bytes // n) // 16 * 16
+        x = lcg_tensor(blk * n // 2, comm.rank, 2, torch.float16, dev)
+        rs = torch.empty(blk // 2, dtype=torch.float16, device=dev)
+        ag = torch.empty(blk * n // 2, dtype=torch.float16, device=dev)
+        for _ in range(2):
+            comm.reduce_scatter(x, rs)
+            comm.all_gather(rs, ag)
+        torch.cuda.synchronize()
+        bw = blk // 4
+        ins = [O.lcg(O.F16, blk * n // 2, r, 2) for r in range(n)]
+        full = O.allreduce_owned(O.F16, O.SUM, [a.view(np.uint32) for a in ins], bw * n, bw * n, bw, 0)[: bw * n]
+        mine = full[comm.rank * bw:(comm.rank + 1) * bw]
+        ok_rs = bool(np.array_equal(rs.view(torch.uint8).cpu().numpy().view(np.uint32), mine))
+        ok_ag = bool(np.array_equal(ag.view(torch.uint8).cpu().numpy().view(np.uint32), full))
+        t_rs = tmax(_time_calls(lambda: comm.reduce_scatter(x, rs), 5))
+        t_ag = tmax(_time_calls(lambda: comm.all_gather(rs, ag), 5))
+        extras["reduce_scatter_allgather"] = {
+            "bytes_in_per_rank_rs": blk * n, "bytes_out_per_rank_ag": blk * n,
+            "reduce_scatter_us": round(t_rs * 1e6, 1), "all_gather_us": round(t_ag * 1e6, 1),
+            # nccl-tests convention: algbw = total buffer bytes / t (recvcount * n for both)
+            "reduce_scatter_algbw_GBs": round(blk * n / t_rs / 1e9, 1),
+            "all_gather_algbw_GBs": round(blk * n / t_ag / 1e9, 1),
+            # every rank's check (a max over ranks of "differs")
+            "correct_bitexact": {"reduce_scatter": tmax(0.0 if ok_rs else 1.0) == 0.0,
+                                 "all_gather": tmax(0.0 if ok_ag else 1.0) == 0.0}}
+        del x, rs, ag
+    except Exception as e:
+        extras["reduce_scatter_allgather_error"] = str(e)[-300:]
     progress("extras: fp32 1 GiB rsag")
     try:
         S = 1 << 30
