@@ -80,3 +80,41 @@ def test_owned_allreduce_matches_sliced():
     for o in range(n):
         seq = O.reduce_seq(O.F16, O.SUM, [padded[(o + k) % n] for k in range(n)])
         assert np.array_equal(owned[owner == o], seq[owner == o])
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_checker_expectations_per_algorithm(built, n):
+    """bench.py's BitExactChecker against direct oracle calls (host logic only): the one-hop LL8
+    result is per rank (own first), the two-hop LL16 result is the owners' everywhere, the bulk
+    orders are own-then-ascending (fullmesh) and ring (rsag / zero-copy), and the pipeline's
+    ownership interleaves slots of 4*C words (C = nblocks * nthreads * 4 units of 16 B)."""
+    import bench
+    import mscclpp_amd as m
+    import oracle_lib as O
+
+    S = 64 << 10
+    chk = bench.BitExactChecker(n, S, m.F16)
+    ins = [O.lcg(m.F16, S // 2, r, 1) for r in range(n)]
+    half = m.scratch_required(m.ALGO_ALLPAIR, n, 16 << 10, m.F16) // 2
+    ins16 = [O.lcg(m.F16, (16 << 10) // 2, r, 1) for r in range(n)]
+    outs, _ = O.allreduce_allpairs(m.F16, O.SUM, ins16, (16 << 10) // 2, 1, half)
+    for r in range(n):
+        assert np.array_equal(chk.expected("allpair", 0, 0, 1, 16 << 10, r), outs[r][: (16 << 10) // 4])
+    half = m.scratch_required(m.ALGO_PACKET, n, S, m.F16) // 2
+    outs, _ = O.allreduce_packet(m.F16, O.SUM, ins, S // 2, 1, half)
+    for r in range(n):
+        assert np.array_equal(chk.expected("packet", 0, 0, 1, S, r), outs[r][: S // 4])
+    nw = S // 4
+    sw = ((S + n - 1) // n + 15) // 16 * 4
+    words = [a.view(np.uint32) for a in ins]
+    for algo, order in (("fullmesh", 0), ("rsag", 1), ("rsag_zc", 1)):
+        exp = O.allreduce_sliced(m.F16, O.SUM, words, nw, sw, order)[0]
+        assert np.array_equal(chk.expected(algo, 64, 512, 1, S, 0), exp[:nw]), algo
+    nb, nt = 2, 64
+    C = nb * nt * 4
+    owner = ((np.arange(nw) // 4) % (n * C)) // C
+    exp = np.zeros(nw, np.uint32)
+    for o in range(n):
+        seq = O.reduce_seq(m.F16, O.SUM, [words[(o + k) % n] for k in range(n)])
+        exp[owner == o] = seq[owner == o]
+    assert np.array_equal(chk.expected("rsag_pipeline", nb, nt, 1, S, 0), exp)
