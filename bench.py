@@ -362,9 +362,8 @@ def bench_multi(args):
         flat = o.detach().contiguous().view(torch.uint8)[: want.numel() * 4].view(torch.int32)
         return bool(torch.equal(flat, want))
 
-    def check_run(algo, nb, nt, nbytes=None, pol="sys"):
+    def check_run(algo, nb, nt, nbytes=None):
         """Untimed: run once on seq 0, poison the output, run on seq 1, compare every word with the oracle."""
-        comm.set_remote_store(pol)
         if nbytes is None:
             a0, a1, o = xs[0], xs[1], out
         else:
@@ -381,7 +380,7 @@ def bench_multi(args):
         if not same:  # say where on stderr (the JSON line carries the verdict per candidate)
             bad = np.nonzero(got != exp)[0]
             sw = ((got.size * 4 + n - 1) // n + 15) // 16 * 4
-            print(f"bench: rank {rank} {algo} {nb}x{nt} {pol}: {bad.size} of {got.size} words differ, first {int(bad[0])} "
+            print(f"bench: rank {rank} {algo} {nb}x{nt}: {bad.size} of {got.size} words differ, first {int(bad[0])} "
                   f"(slice {int(bad[0]) // sw}), slices {sorted(set((bad // sw).tolist()))[:8]}, "
                   f"{int((got[bad] == 0xFFFFFFFF).sum())} poisoned", file=sys.stderr)
         return all_ok(same and comm.device_error() == 0)
@@ -401,43 +400,36 @@ def bench_multi(args):
         tuple((nb_, 512) for nb_ in (16, 32, 64, 128) if nb_ * world <= 256)
     pipe_shapes = ((32, 512), (64, 512), (128, 512), (64, 256)) if not shared else \
         tuple((nb_, 512) for nb_ in (8, 16, 32, 64) if 2 * nb_ * world <= 256)
-    # the bulk kernels' stores into peers' memory: sc0 sc1 (sys) or nt (mscclppAmdCommSetRemoteStore)
     for a in algos:
         if a in ("fullmesh", "rsag", "rsag_zc"):
-            cands += [(a, nb_, nt_, pol) for pol in ("sys", "nt") for nb_, nt_ in bulk_shapes]
+            cands += [(a, nb_, nt_) for nb_, nt_ in bulk_shapes]
         elif a == "rsag_pipeline":  # nblocks = reduce workgroups; the launch is 2x that
-            cands += [(a, nb_, nt_, "sys") for nb_, nt_ in pipe_shapes]
+            cands += [(a, nb_, nt_) for nb_, nt_ in pipe_shapes]
         else:
-            cands.append((a, 0, 0, "sys"))
-
-    def key(a, nb_, nt_, pol):
-        return f"{a}:{nb_}x{nt_}" + ("" if pol == "sys" else f":{pol}")
+            cands.append((a, 0, 0))
     if not cands:
         raise SystemExit(f"bench: no launch shape fits {world} ranks on {ndev} device(s)")
     tune = {}
     progress(f"tuning {len(cands)} candidates")
-    for a, nb, nt, pol in cands:
+    for a, nb, nt in cands:
         try:
-            comm.set_remote_store(pol)
             for j in range(2):
                 comm.all_reduce(xs[j], out, algo=a, nblocks=nb, nthreads=nt)
-            tune[(a, nb, nt, pol)] = tmax(_time_calls(lambda: comm.all_reduce(xs[0], out, algo=a, nblocks=nb, nthreads=nt),
-                                                      5))
+            tune[(a, nb, nt)] = tmax(_time_calls(lambda: comm.all_reduce(xs[0], out, algo=a, nblocks=nb, nthreads=nt), 5))
         except Exception as e:  # a rejected shape is simply skipped
-            tune[(a, nb, nt, pol)] = float("inf")
+            tune[(a, nb, nt)] = float("inf")
             if rank == 0:
-                print(f"tune {key(a, nb, nt, pol)}: {e}", file=sys.stderr)
+                print(f"tune {a} {nb}x{nt}: {e}", file=sys.stderr)
     if tmax(float(comm.device_error())) != 0:  # a spin timed out somewhere: say so instead of hanging on
         print("bench: device error after tuning; results below are suspect", file=sys.stderr)
-    algo, nb, nt, pol = min(tune, key=tune.get)
-    comm.set_remote_store(pol)
+    algo, nb, nt = min(tune, key=tune.get)
 
     total = args.warmup + args.steps
 
     def step(j):  # step j of warmup + timed; the last timed step runs on seq 1
         comm.all_reduce(xs[1 if args.same_input else 1 - (total - 1 - j) % 2], out, algo=algo, nblocks=nb, nthreads=nt)
 
-    progress(f"selected {key(algo, nb, nt, pol)}; warmup + timed region")
+    progress(f"selected {algo} {nb}x{nt}; warmup + timed region")
     poison(out)  # the fill kernel's first launch loads its code object (~4 ms): never inside the timed region
     for j in range(args.warmup):
         step(j)
@@ -467,17 +459,16 @@ def bench_multi(args):
         exp = checker.expected(algo, nb, nt, 1, None, rank)
         bitexact["timed_last_step"] = all_ok(bool(np.array_equal(BitExactChecker.words(out), exp))
                                              and device_matches(out, exp) and errc == 0)
-        for a, cnb, cnt, cpol in cands:
-            if tune[(a, cnb, cnt, cpol)] == float("inf"):
+        for a, cnb, cnt in cands:
+            if tune[(a, cnb, cnt)] == float("inf"):
                 continue
-            bitexact[key(a, cnb, cnt, cpol)] = check_run(a, cnb, cnt, None, cpol)
+            bitexact[f"{a}:{cnb}x{cnt}"] = check_run(a, cnb, cnt)
         # in place (send == recv, BASELINE configs[2] names both): the winner once more
-        comm.set_remote_store(pol)
         a1 = xs[1].clone()
         comm.all_reduce(a1, a1, algo=algo, nblocks=nb, nthreads=nt)
         torch.cuda.synchronize()
         exp1 = checker.expected(algo, nb, nt, 1, None, rank)
-        bitexact[key(algo, nb, nt, pol) + ":in_place"] = all_ok(bool(np.array_equal(BitExactChecker.words(a1), exp1))
+        bitexact[f"{algo}:{nb}x{nt}:in_place"] = all_ok(bool(np.array_equal(BitExactChecker.words(a1), exp1))
                                                         and device_matches(a1, exp1) and comm.device_error() == 0)
         del a1
         for a, nbytes in (("packet", 1 << 20), ("allpair", 16 << 10)):  # the LL paths (configs[3])
@@ -523,8 +514,7 @@ def bench_multi(args):
         "dtype": "f16",
         "data": "synthetic (LCG of test/torch/correctness_test.py, seq alternating per step)",
         "config": {"workload": f"allreduce_fp16_{S >> 20}MiB (BASELINE configs[2]: 2048x12288 fp16 bucket per rank)",
-                   "bytes": S, "parallelism": f"allreduce{world}", "algo": algo, "nblocks": nb, "nthreads": nt,
-                   "remote_store": pol},
+                   "bytes": S, "parallelism": f"allreduce{world}", "algo": algo, "nblocks": nb, "nthreads": nt},
         "scaling_note": SCALING_NOTE,
         "busbw": round(algbw * 2 * (n - 1) / n, 2),
         # the bytes all ranks contributed per AllReduce (n buckets of S) over the step time, beside
@@ -546,7 +536,7 @@ def bench_multi(args):
                              "bytes_per_launch": int(hbm)}},
         "xgmi": {"allpairs_algbw_ceiling_assumed": round(ceiling, 1), "frac_of_assumed_ceiling": round(algbw / ceiling, 4),
                  "link_GBs_assumed": XGMI_LINK_GBS, "wire_bytes_per_rank": int(wire), "measured": probe},
-        "tune_ms": {key(*k): round(v * 1e3, 4) for k, v in tune.items()},
+        "tune_ms": {f"{k[0]}:{k[1]}x{k[2]}": round(v * 1e3, 4) for k, v in tune.items()},
         "correct": ok,
         "correct_bitexact": bitexact,
     }
@@ -555,7 +545,7 @@ def bench_multi(args):
     res["tuned_config"] = {"version": 1, "profiles": [{"sku": torch.cuda.get_device_name(dev), "scale": n,
                                                        "collectives": {"allreduce": [
                                                            {"message_size": S, "algorithm": FULL_NAMES[algo],
-                                                            "nblocks": nb, "nthreads": nt, "remote_store": pol,
+                                                            "nblocks": nb, "nthreads": nt,
                                                             "time_us": round(t * 1e6, 2)}]}}]}
     mc = probe.get("allpairs_algbw_ceiling_measured")
     if mc:

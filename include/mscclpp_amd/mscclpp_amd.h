@@ -80,9 +80,7 @@ typedef struct {
   uint32_t* err;                                   /* device error word (0 = ok) */
   uint64_t scratchBytes;
   int32_t rank;
-  int32_t remoteStore;                             /* cache policy of the bulk kernels' stores into peers'
-                                                      memory: 0 = sc0 sc1 (default), 2 = nt;
-                                                      every hand-off still ends with a system-scope release */
+  int32_t pad;
   const void* peerInput[MSCCLPP_AMD_MAX_RANKS];    /* rank q's input as mapped here (zero-copy reads) */
   uint64_t* pipeSems;                              /* rsag_pipeline: 3 x 256 intra-launch counters, zeroed
                                                       before each launch (stream-ordered) */
@@ -175,12 +173,6 @@ int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear);
  * synchronize before they close.  Any pointer may be NULL. */
 int mscclppAmdCommRegistrationStats(ncclComm_t comm, size_t* userRegistrations, size_t* liveMappings,
                                     size_t* retiredMappings);
-/* Cache policy of the bulk AllReduce / ReduceScatter / AllGather kernels' stores into peers' memory
- * (fullmesh, rsag, zero-copy): 0 = sc0 sc1 system scope (default), 2 = nt.  Every
- * hand-off still ends with a system-scope release, so results do not depend on it; its speed over
- * xGMI does (the benchmark's probe and tuning measure it).  Default from MSCCLPP_AMD_REMOTE_STORE. */
-int mscclppAmdCommSetRemoteStore(ncclComm_t comm, int policy);
-int mscclppAmdCommGetRemoteStore(ncclComm_t comm, int* policy);
 /* Host all-gathers made by user-buffer registration so far: one per newly registered allocation,
  * one per new buffer offset inside a registered allocation (none when the communicator runs with
  * MSCCLPP_NCCL_SYMMETRIC_MEMORY, env.hpp:101-107, which *symmetricMemory reports). */

@@ -69,7 +69,7 @@ class RankView(ctypes.Structure):
         ("err", ctypes.c_void_p),
         ("scratchBytes", ctypes.c_uint64),
         ("rank", ctypes.c_int32),
-        ("remoteStore", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
         ("peerInput", ctypes.c_void_p * MAX_RANKS),
         ("pipeSems", ctypes.c_void_p),
     ]
@@ -130,8 +130,6 @@ def lib():
         "mscclppAmdCommGetDeviceError": [vp, ctypes.POINTER(ctypes.c_uint32), i32],
         "mscclppAmdCommScratch": [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)],
         "mscclppAmdCommRegistrationStats": [vp, ctypes.POINTER(sz), ctypes.POINTER(sz), ctypes.POINTER(sz)],
-        "mscclppAmdCommSetRemoteStore": [vp, i32],
-        "mscclppAmdCommGetRemoteStore": [vp, ctypes.POINTER(ctypes.c_int)],
         "mscclppAmdCommRegistrationExchanges": [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                                 ctypes.POINTER(ctypes.c_int)],
         "mscclppAmdCommFlags": [vp, ctypes.POINTER(vp)],
@@ -239,9 +237,8 @@ class InProcessRanks:
     blockIdx.y = rank) without IPC.
     """
 
-    def __init__(self, nranks, scratch_bytes, bulk_scratch_bytes=0, remote_store=0):
+    def __init__(self, nranks, scratch_bytes, bulk_scratch_bytes=0):
         self.n = nranks
-        self.remote_store = remote_store  # mscclppAmdRankView::remoteStore: 0 sc0 sc1, 2 nt
         self.scratch = [DeviceBuffer(scratch_bytes) for _ in range(nranks)]
         self.scratch_bytes = scratch_bytes
         self.bulk = [DeviceBuffer(bulk_scratch_bytes) for _ in range(nranks)] if bulk_scratch_bytes else None
@@ -277,7 +274,6 @@ class InProcessRanks:
             v.pipeSems = self.pipe_sems[r].data_ptr()
             v.scratchBytes = sbytes
             v.rank = r
-            v.remoteStore = self.remote_store
         return arr
 
     def all_reduce(self, inputs, outputs, algo, op=SUM, nblocks=0, nthreads=0, budget_ticks=500_000_000, stream=None,
@@ -447,12 +443,6 @@ class Communicator:
         check(lib().mscclppAmdCommRegistrationStats(self.comm, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
               "registration stats")
         return a.value, b.value, c.value
-
-    REMOTE_STORE = {"sys": 0, "nt": 2}
-
-    def set_remote_store(self, policy):
-        """Cache policy of the bulk kernels' stores into peers' memory: "sys" (sc0 sc1) or "nt"."""
-        check(lib().mscclppAmdCommSetRemoteStore(self.comm, self.REMOTE_STORE[policy]), "set remote store")
 
     def registration_exchanges(self):
         """(allocation exchanges, offset exchanges, symmetric memory on) of user-buffer registration."""

@@ -225,11 +225,9 @@ std::shared_ptr<Algorithm> builtin(ncclComm* comm, const std::string& name, cons
       std::string tuned;
       int nb = 0, nt = 0;
       const size_t msg = inSize;  // the request's messageSize for all three (nccl.cc:586, :697, :748)
-      int rs = -1;
-      if (tunedConfig(collective, c->nranks, msg, tuned, nb, nt, &rs) && tuned == name) {
+      if (tunedConfig(collective, c->nranks, msg, tuned, nb, nt) && tuned == name) {
         nBlocks = nb;
         nThreads = nt;
-        c->callRemoteStore = rs;  // consumed by the launch below (baseView)
       }
     }
     if (coll == 2) {  // AllGather moves bytes: the element type only sets the unit

@@ -494,19 +494,6 @@ int mscclppAmdCommRegistrationStats(ncclComm_t comm, size_t* userRegistrations, 
   return ncclSuccess;
 }
 
-int mscclppAmdCommSetRemoteStore(ncclComm_t comm, int policy) {
-  if (!comm || (policy != 0 && policy != 2)) return ncclInvalidArgument;
-  std::lock_guard<std::mutex> lk(comm->mu);
-  comm->remoteStore = policy;
-  return ncclSuccess;
-}
-
-int mscclppAmdCommGetRemoteStore(ncclComm_t comm, int* policy) {
-  if (!comm || !policy) return ncclInvalidArgument;
-  *policy = comm->remoteStore;
-  return ncclSuccess;
-}
-
 int mscclppAmdCommRegistrationExchanges(ncclComm_t comm, uint64_t* allocationExchanges, uint64_t* offsetExchanges,
                                         int* symmetricMemory) {
   if (!comm) return ncclInvalidArgument;

@@ -177,14 +177,6 @@ inline bool envSymmetricMemory() {
   return e && std::string(e) != "0";
 }
 
-// MSCCLPP_AMD_REMOTE_STORE = sys (default) | nt: the cache policy of the bulk kernels' stores into
-// peers' memory (mscclppAmdRankView::remoteStore); mscclppAmdCommSetRemoteStore sets it per
-// communicator (the benchmark tunes it).
-inline int envRemoteStore() {
-  const char* e = std::getenv("MSCCLPP_AMD_REMOTE_STORE");
-  return (e && std::string(e) == "nt") ? 2 : 0;
-}
-
 inline int envAlgo() {
   const char* e = std::getenv("MSCCLPP_AMD_ALGO");
   if (!e) return MSCCLPP_AMD_ALGO_AUTO;
@@ -215,7 +207,7 @@ uint64_t allocationId(const void* ptr);  // HIP_POINTER_ATTRIBUTE_BUFFER_ID (0 i
 // Tuned configuration (tuning.cpp) for a collective of `bytes` on `nranks` ranks of this device's
 // SKU: the algorithm name and launch shape (0 = the algorithm's default); false if none.
 bool tunedConfig(const std::string& collective, int nranks, uint64_t bytes, std::string& algorithm, int& nblocks,
-                 int& nthreads, int* remoteStore = nullptr);
+                 int& nthreads);
 int algoCodeOf(const std::string& name);  // MSCCLPP_AMD_ALGO_* of a default_allreduce_* name, or -1
 }  // namespace host
 }  // namespace mscclpp_amd
@@ -364,8 +356,6 @@ struct ncclComm {
   std::map<std::pair<uint64_t, uint64_t>, UserReg> userRegs;
   uint64_t useClock = 0;
   bool symmetricMemory = envSymmetricMemory();
-  int remoteStore = envRemoteStore();  // mscclppAmdRankView::remoteStore of this communicator's launches
-  int callRemoteStore = -1;            // a tuned entry's policy for the next launch only (-1: none)
   // host all-gathers the registration path made: allocations exchanged, offsets exchanged
   uint64_t allocExchanges = 0, offsetExchanges = 0;
 
@@ -471,11 +461,9 @@ struct ncclComm {
     if (nblocks > 0 || nthreads > 0) return;
     std::string name;
     int nb = 0, nt = 0;
-    int rs = -1;
-    if (tunedConfig(coll, nranks, bytes, name, nb, nt, &rs) && algoCodeOf(name) == algo) {
+    if (tunedConfig(coll, nranks, bytes, name, nb, nt) && algoCodeOf(name) == algo) {
       nblocks = nb;
       nthreads = nt;
-      callRemoteStore = rs;
     }
   }
 
@@ -488,8 +476,6 @@ struct ncclComm {
     v.flags = flags;
     v.err = err;
     v.rank = rank;
-    v.remoteStore = callRemoteStore >= 0 ? callRemoteStore : remoteStore;
-    callRemoteStore = -1;
     for (int r = 0; r < nranks; ++r) v.peerTokens[r] = peerTokens[r];
     return v;
   }

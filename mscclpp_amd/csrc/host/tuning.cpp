@@ -28,7 +28,6 @@ struct Entry {
   uint64_t size;
   std::string algorithm;
   int nblocks = 0, nthreads = 0;
-  int remoteStore = -1;  // this library's extension: "remote_store": "sys" | "nt" (-1: the communicator's)
 };
 struct Profile {
   std::string sku;  // empty: any
@@ -77,11 +76,6 @@ std::vector<Profile> parseStore(const std::string& text) {
           en.algorithm = e["algorithm"].str();
           if (e.contains("nblocks") && e["nblocks"].kind != json::Value::Null) en.nblocks = (int)e["nblocks"].asI64();
           if (e.contains("nthreads") && e["nthreads"].kind != json::Value::Null) en.nthreads = (int)e["nthreads"].asI64();
-          if (e.contains("remote_store") && e["remote_store"].kind != json::Value::Null) {
-            const std::string rs = e["remote_store"].str();
-            if (rs != "sys" && rs != "nt") throw std::invalid_argument("tuned config: remote_store must be sys or nt");
-            en.remoteStore = rs == "nt" ? 2 : 0;
-          }
           es.push_back(en);
         }
         std::sort(es.begin(), es.end(), [](const Entry& a, const Entry& b) { return a.size < b.size; });
@@ -164,7 +158,7 @@ const Entry* selectProfiles(const std::vector<Profile>& ps, const std::string& s
 }  // namespace
 
 bool tunedConfig(const std::string& collective, int nranks, uint64_t bytes, std::string& algorithm, int& nblocks,
-                 int& nthreads, int* remoteStore) {
+                 int& nthreads) {
   Store& s = store();
   std::lock_guard<std::mutex> lk(s.mu);
   const Entry* e = selectProfiles(s.user, s.sku, nranks, collective, bytes);
@@ -173,7 +167,6 @@ bool tunedConfig(const std::string& collective, int nranks, uint64_t bytes, std:
   algorithm = e->algorithm;
   nblocks = e->nblocks;
   nthreads = e->nthreads;
-  if (remoteStore) *remoteStore = e->remoteStore;
   return true;
 }
 

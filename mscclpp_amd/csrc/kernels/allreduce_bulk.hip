@@ -36,17 +36,6 @@ struct BulkGeom {
 
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// A 16-byte store into a peer's memory with the view's policy (mscclppAmdRankView::remoteStore:
-// 0 sc0 sc1, 2 nt).
-// Whatever the policy, the storing workgroup drains and issues a SYSTEM-scope release (write-back of
-// its XCD's L2) before it signals the peer (block_handshake), so the peer's reads see the data.
-__device__ __forceinline__ void store_remote(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v, int32_t policy) {
-  if (policy == 2)
-    store16<kNonTemporal>(r, off, v);
-  else
-    store16<kSystem>(r, off, v);
-}
-
 // All lanes of the block: publish every prior store, then lane p < nranks signals peer p on
 // channel `ch`; then lanes wait for the peers' matching signals.
 __device__ __forceinline__ void block_handshake(const mscclppAmdRankView& v, int nranks, int rank, uint32_t ch,
@@ -84,7 +73,6 @@ template <int DT, int OP, int NV, int ORDER, int MODE>
 __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, BulkGeom g, int nranks, uint64_t budget) {
   const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
   const int rank = v.rank;
-  const int32_t pol = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)v.remoteStore);
   const uint32_t T = blockDim.x, tid = threadIdx.x, b = blockIdx.x;
   const uint8_t* in = (const uint8_t*)v.input;
   uint8_t* out = (uint8_t*)v.output;
@@ -131,7 +119,7 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
 #pragma unroll
             for (int k2 = 0; k2 < U; ++k2) {
               const uint32_t u = u0 + k2 * T;
-              if (u < nUnits) store_remote(rq, u * 16u, w[k2], pol);
+              if (u < nUnits) store16<kSystem>(rq, u * 16u, w[k2]);
             }
           }
         }
@@ -181,7 +169,7 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
             const int q = k < rank ? k : k + 1;
             uint8_t* po = (uint8_t*)v.peerOutput[q] + myOff;
             if (vb >= 16)
-              store_remote(make_rsrc(po), u * 16u, acc, pol);
+              store16<kSystem>(make_rsrc(po), u * 16u, acc);
             else
               store_tail(po + (uint64_t)u * 16, acc, vb);
           }
@@ -204,7 +192,6 @@ template <int DT, int OP, int NV>
 __global__ void __launch_bounds__(512) allreduceZeroCopyKernel(Views<NV> views, BulkGeom g, int nranks, uint64_t budget) {
   const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
   const int rank = v.rank;
-  const int32_t pol = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)v.remoteStore);
   const uint32_t T = blockDim.x, tid = threadIdx.x, b = blockIdx.x;
   const uint64_t bOff = (uint64_t)b * g.blk;
   uint64_t bLen = 0;
@@ -248,7 +235,7 @@ __global__ void __launch_bounds__(512) allreduceZeroCopyKernel(Views<NV> views, 
       for (int k = 1; k < nranks; ++k) {
         uint8_t* po = (uint8_t*)v.peerOutput[(rank + k) % nranks] + myOff;
         if (vb >= 16)
-          store_remote(make_rsrc(po), u * 16u, acc, pol);
+          store16<kSystem>(make_rsrc(po), u * 16u, acc);
         else
           store_tail(po + (uint64_t)u * 16, acc, vb);
       }

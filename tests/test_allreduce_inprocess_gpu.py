@@ -117,36 +117,6 @@ def test_bulk_allreduce_bit_exact(built, algo, order, n, dt, count):
             _cmp(_bytes(douts[r]), exp[r].view(np.uint8)[:nbytes], dt)
 
 
-@pytest.mark.parametrize("policy", [2])
-@pytest.mark.parametrize("algo,order", [("fullmesh", 0), ("rsag", 1), ("rsag_zc", 1)])
-def test_bulk_remote_store_policies(built, algo, order, policy):
-    """The bulk kernels with nt stores into the peers' memory (mscclppAmdRankView::remoteStore = 2):
-    the same bit-exact results as the default sc0 sc1 stores, the release before every signal carries
-    the visibility."""
-    import mscclpp_amd as m
-
-    n, dt, count = 8, O.F16, (1 << 18) + 40
-    nbytes = count * ITEM[dt]
-    slice_bytes = ((nbytes + n - 1) // n + 15) // 16 * 16
-    ranks = m.InProcessRanks(n, 1 << 16, bulk_scratch_bytes=n * slice_bytes, remote_store=policy)
-    for call in range(3):
-        ins = _inputs(dt, n, count, seq=call, special=(call == 1))
-        dins = [_dev(a, dt) for a in ins]
-        douts = [torch.full_like(d, 0) for d in dins]
-        ranks.all_reduce(dins, douts, m.ALGO_NAMES[algo], nblocks=16, nthreads=256)
-        torch.cuda.synchronize()
-        assert ranks.errors() == [0] * n
-        nwords = (nbytes + 3) // 4
-        padded = []
-        for a in ins:
-            w = np.zeros(nwords, np.uint32)
-            w.view(np.uint8)[:nbytes] = a.view(np.uint8)
-            padded.append(w)
-        exp = O.allreduce_sliced(dt, O.SUM, padded, nwords, slice_bytes // 4, order)
-        for r in range(n):
-            _cmp(_bytes(douts[r]), exp[r].view(np.uint8)[:nbytes], dt)
-
-
 @pytest.mark.parametrize("algo", ["packet", "allpair", "fullmesh", "rsag_zc"])
 def test_in_place(built, algo):
     import mscclpp_amd as m

@@ -19,11 +19,9 @@ CASES = [  # (algo, dtype code, count)
 ]
 
 
-def _worker(rank, n, uid, q, cases=None, rsag=True, remote_store=None):
+def _worker(rank, n, uid, q, cases=None, rsag=True):
     try:
         os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "5000")
-        if remote_store:
-            os.environ["MSCCLPP_AMD_REMOTE_STORE"] = remote_store
         if n > 2:  # many ranks on one device: one hardware queue each keeps every rank's queue mapped
             os.environ["GPU_MAX_HW_QUEUES"] = "1"
         import torch
@@ -86,13 +84,13 @@ def _worker(rank, n, uid, q, cases=None, rsag=True, remote_store=None):
         q.put((rank, None, traceback.format_exc()))
 
 
-def _run(n, cases=None, rsag=True, timeout=240, remote_store=None):
+def _run(n, cases=None, rsag=True, timeout=240):
     import mscclpp_amd as m
 
     uid = m.Communicator.unique_id()  # root thread lives in this (parent) process
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, n, uid, q, cases, rsag, remote_store)) for r in range(n)]
+    procs = [ctx.Process(target=_worker, args=(r, n, uid, q, cases, rsag)) for r in range(n)]
     for p in procs:
         p.start()
     got = {}
@@ -128,14 +126,6 @@ MANY_CASES = [("allpair", 0, 4096), ("packet", 0, 1 << 17), ("packet", 1, 30001)
 @pytest.mark.parametrize("n", [4, 8])
 def test_many_process_ncclallreduce(built, n):
     _run(n, MANY_CASES, rsag=True, timeout=300)
-
-
-@pytest.mark.parametrize("policy", ["nt"])
-def test_remote_store_policies_four_processes(built, policy):
-    """MSCCLPP_AMD_REMOTE_STORE: the bulk AllReduces and ReduceScatter / AllGather with nt
-    stores into the peers' IPC-mapped memory, bit-exact like the default."""
-    cases = [("fullmesh", 0, 1 << 19), ("rsag", 2, 100000), ("rsag_zc", 0, 1 << 19), ("rsag_zc", 1, 77777)]
-    _run(4, cases, rsag=True, timeout=300, remote_store=policy)
 
 
 def test_host_proxy_paths(built):

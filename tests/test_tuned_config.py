@@ -80,24 +80,3 @@ def test_malformed_file_is_rejected(built, tmp_path):
     bad.write_text('{"profiles": [{"collectives": {"allreduce": [{"message_size": 0, "algorithm": "x"}]}}]}')
     assert m.lib().mscclppAmdTunedConfigLoad(os.fsencode(str(bad))) == 4
     assert m.lib().mscclppAmdTunedConfigLoad(os.fsencode(str(tmp_path / "missing.json"))) == 4
-
-
-def test_remote_store_field(built, tmp_path):
-    """The bench's tuned_config carries this library's "remote_store" ("sys" | "nt", the bulk kernels'
-    store policy into peers' memory); other values are rejected, the reference's fields unaffected."""
-    import mscclpp_amd as m
-
-    good = tmp_path / "good.json"
-    good.write_text(json.dumps({"version": 1, "profiles": [{"scale": 8, "collectives": {"allreduce": [
-        {"message_size": 1048577, "algorithm": "default_allreduce_rsag_zero_copy", "nblocks": 128, "nthreads": 512,
-         "remote_store": "nt"}]}}]}))
-    assert m.lib().mscclppAmdTunedConfigLoad(os.fsencode(str(good))) == 0
-    assert m.tuned_config("allreduce", 8, 48 << 20) == ("default_allreduce_rsag_zero_copy", 128, 512) or \
-        m.tuned_config("allreduce", 8, 48 << 20) == ["default_allreduce_rsag_zero_copy", 128, 512]
-    bad = tmp_path / "bad.json"
-    bad.write_text(json.dumps({"profiles": [{"collectives": {"allreduce": [
-        {"message_size": 1, "algorithm": "default_allreduce_fullmesh", "remote_store": "plain"}]}}]}))
-    assert m.lib().mscclppAmdTunedConfigLoad(os.fsencode(str(bad))) == 4
-    empty = tmp_path / "empty.json"  # leave this process with the built-in table only
-    empty.write_text('{"version": 1, "profiles": []}')
-    assert m.lib().mscclppAmdTunedConfigLoad(os.fsencode(str(empty))) == 0
