@@ -219,7 +219,11 @@ def bench_single(args):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": committed_traffic(S),
                      "kernel": "selfReduceLL16LdsKernel", "kernel_us": round(kern_ms * 1e3, 2),
-                     "algorithmic_bytes_per_launch": 7 * S},
+                     "algorithmic_bytes_per_launch": 7 * S,
+                     # BASELINE.md §3 row 2's secondary figure: the HBM reads alone (Y, P, X = 4*S)
+                     "read_only": {"bytes_per_launch": 4 * S,
+                                   "achieved": round(4 * S / (kern_ms * 1e-3) / 1e9, 1),
+                                   "frac": round(4 * S / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
     }
     if args.no_extras:  # profiling runs: only the headline launches, so per-kernel stats are of one size
         pk.free()
