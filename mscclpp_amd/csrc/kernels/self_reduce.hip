@@ -29,10 +29,7 @@ namespace mscclpp_amd {
 //
 // COUNT: diagnostic build that adds the number of packets whose first poll missed to pollMiss[0]
 // (one atomic per wave and round), to measure the re-poll traffic the skew removes.
-// SKEW: rounds between packing a tile and its partner consuming it (0, 1 or 2).  EARLY: the packet
-// loads of the consumed tile are issued at the top of the round, beside its X loads and before the
-// pack's stores, so each wave keeps more bytes in flight while it packs.
-template <int DT, int OP, int U, int SKEW, bool COUNT, bool EARLY = false>
+template <int DT, int OP, int U, bool SKEW, bool COUNT>
 __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
                                                                uint8_t* pkts, uint8_t* __restrict__ out, uint64_t bytes,
                                                                uint32_t* flags, uint64_t budget, uint32_t* err,
@@ -58,21 +55,11 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
     }
   };
   if (b < ntiles) load_y(b);
-  u32x4 v[2 * U];
-  auto load_packets = [&](uint64_t tc) {
-#pragma unroll
-    for (int k = 0; k < U; ++k) {
-      const uint64_t c = chunk(tc, k);
-      const auto rp = make_rsrc(pkts + 2 * c);
-      if (c + lane * 8 < bytes) v[2 * k] = load16<kSystem>(rp, lane * 16);
-      if (c + 512 + lane * 8 < bytes) v[2 * k + 1] = load16<kSystem>(rp, 1024 + lane * 16);
-    }
-  };
-  for (uint64_t i = 0; i < rounds + SKEW; ++i) {
-    const uint64_t t = i * G + b;                 // packed this round (i < rounds)
-    const uint64_t tp = (i - SKEW) * G + partner;  // consumed this round (i >= SKEW)
+  for (uint64_t i = 0; i < rounds + (SKEW ? 1 : 0); ++i) {
+    const uint64_t t = i * G + b;                          // packed this round (i < rounds)
+    const uint64_t tp = (SKEW ? i - 1 : i) * G + partner;  // consumed this round
     const bool pack = i < rounds && t < ntiles;
-    const bool consume = i >= (uint64_t)SKEW && partner < G && tp < ntiles;
+    const bool consume = (!SKEW || i > 0) && partner < G && tp < ntiles;
     u32x4 a[U];
     if (consume) {
 #pragma unroll
@@ -80,7 +67,6 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
         const uint64_t c = chunk(tp, k);
         if (c + lane * 16 < bytes) a[k] = load16<kNonTemporal>(make_rsrc(x + c), lane * 16);
       }
-      if constexpr (EARLY) load_packets(tp);
     }
     // ---- pack: payload -> LDS -> packet-major stores (packets j and 64 + j of each 1 KiB chunk)
     if (pack) {
@@ -100,13 +86,20 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
     }
     // ---- consume a partner tile: packet-major polls -> LDS -> payload-major sum and store
     if (consume) {
-      if constexpr (!EARLY) load_packets(tp);
+      u32x4 v[2 * U];
       bool ok = true;
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const uint64_t c = chunk(tp, k);
-        if (c + lane * 8 < bytes) ok &= LL16Packet::ready(v[2 * k], flag);
-        if (c + 512 + lane * 8 < bytes) ok &= LL16Packet::ready(v[2 * k + 1], flag);
+        const auto rp = make_rsrc(pkts + 2 * c);
+        if (c + lane * 8 < bytes) {
+          v[2 * k] = load16<kSystem>(rp, lane * 16);
+          ok &= LL16Packet::ready(v[2 * k], flag);
+        }
+        if (c + 512 + lane * 8 < bytes) {
+          v[2 * k + 1] = load16<kSystem>(rp, 1024 + lane * 16);
+          ok &= LL16Packet::ready(v[2 * k + 1], flag);
+        }
       }
       if constexpr (COUNT) {
         uint32_t miss = 0;
@@ -166,11 +159,11 @@ static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out
   const uint64_t tiles = (bytes + kTile - 1) / kTile;
   const uint64_t rounds = (tiles + (uint64_t)nblocks - 1) / (uint64_t)nblocks;
   if (rounds == 2)
-    hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, 0, false>), dim3(nblocks), dim3(256), 0, stream,
+    hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, false, false>), dim3(nblocks), dim3(256), 0, stream,
                        (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
                        (uint32_t*)nullptr);
   else
-    hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, 1, false>), dim3(nblocks), dim3(256), 0, stream,
+    hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, true, false>), dim3(nblocks), dim3(256), 0, stream,
                        (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
                        (uint32_t*)nullptr);
 }
@@ -230,32 +223,25 @@ using namespace mscclpp_amd;
 
 // Tuning / diagnostic entry (fp16 SUM): variant 0 = the product form (skewed, 2 KiB per wave and
 // round), 1 = unskewed (round-1 form), 2 = skewed with 4 KiB per wave and round, 3 = skewed with
-// 1 KiB; 4 / 5 = variants 0 / 1 counting first-poll misses into pollMiss[0] (must not be null);
-// 6 = EARLY packet loads (skew 1), 7 = EARLY with skew 2, 8 = skew 2 (all within 1 % of variant 0
-// at 48 MiB).
+// 1 KiB; 4 / 5 = variants 0 / 1 counting first-poll misses into pollMiss[0] (must not be null).
 extern "C" int mscclppAmdSelfReduceLL16Variant(const void* x, const void* y, void* pkts, void* out, size_t bytes,
                                                uint32_t* flags, int nblocks, int variant, uint64_t budgetTicks,
                                                uint32_t* err, uint32_t* pollMiss, void* streamPtr) {
   hipStream_t s = (hipStream_t)streamPtr;
-  if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0) return 4;
-  // every pair must be co-resident: 2048 workgroups fit at <= 64 VGPRs (8 per CU), the U=4 form at 1024
-  if (nblocks > (variant == 2 ? 1024 : 2048)) return 4;
+  if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > 1024) return 4;
   if ((variant == 4 || variant == 5) && !pollMiss) return 4;
   if (nblocks % 2) nblocks += 1;
-#define SRV(U, SKEW, COUNT, ...)                                                                                  \
-  hipLaunchKernelGGL((selfReduceLL16LdsKernel<kF16, kSum, U, SKEW, COUNT, ##__VA_ARGS__>), dim3(nblocks), dim3(256), 0, s, \
+#define SRV(U, SKEW, COUNT)                                                                                       \
+  hipLaunchKernelGGL((selfReduceLL16LdsKernel<kF16, kSum, U, SKEW, COUNT>), dim3(nblocks), dim3(256), 0, s,       \
                      (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, (uint64_t)bytes, flags, \
                      budgetTicks, err, pollMiss)
   switch (variant) {
-    case 0: SRV(2, 1, false); break;
-    case 1: SRV(2, 0, false); break;
-    case 2: SRV(4, 1, false); break;
-    case 3: SRV(1, 1, false); break;
-    case 4: SRV(2, 1, true); break;
-    case 5: SRV(2, 0, true); break;
-    case 6: SRV(2, 1, false, true); break;
-    case 7: SRV(2, 2, false, true); break;
-    case 8: SRV(2, 2, false); break;
+    case 0: SRV(2, true, false); break;
+    case 1: SRV(2, false, false); break;
+    case 2: SRV(4, true, false); break;
+    case 3: SRV(1, true, false); break;
+    case 4: SRV(2, true, true); break;
+    case 5: SRV(2, false, true); break;
     default: return 4;
   }
 #undef SRV
