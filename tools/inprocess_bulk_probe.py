@@ -35,8 +35,10 @@ NAMES = {m.ALGO_FULLMESH: "fullmesh", m.ALGO_RSAG: "rsag", m.ALGO_RSAG_ZC: "rsag
 # every rank's grid must be resident at once (cross-rank handshakes): at most 2048 workgroup slots of
 # 256 threads would fit at <= 64 VGPRs; kept to 1024 threads per CU: nblocks * N * nthreads <= 256 * 1024
 shapes = [(nb, nt) for nb in (8, 16, 32, 64, 128) for nt in (256, 512) if nb * N * nt <= 256 * 1024]
-cands = [(a, nb, nt) for a in (m.ALGO_FULLMESH, m.ALGO_RSAG, m.ALGO_RSAG_ZC) for nb, nt in shapes]
-cands += [(m.ALGO_RSAG_PIPELINE, nb, nt) for nb, nt in shapes if 2 * nb * N * nt <= 256 * 1024 and nb >= 2]
+want = [m.ALGO_NAMES[a] for a in os.environ.get("ALGOS", "fullmesh,rsag,rsag_zc,rsag_pipeline").split(",")]
+cands = [(a, nb, nt) for a in (m.ALGO_FULLMESH, m.ALGO_RSAG, m.ALGO_RSAG_ZC) if a in want for nb, nt in shapes]
+if m.ALGO_RSAG_PIPELINE in want:
+    cands += [(m.ALGO_RSAG_PIPELINE, nb, nt) for nb, nt in shapes if 2 * nb * N * nt <= 256 * 1024 and nb >= 2]
 
 
 def run(a, nb, nt):
@@ -86,7 +88,7 @@ for a, nb, nt, good in ok_c:
 rows.sort(key=lambda r: r.get("us", 1e18))
 res = {"nranks": N, "bytes": S, "copy_TBs_2S": round(2 * S / float(np.median(copy_t)) / 1e6, 3), "rows": rows}
 os.makedirs(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out"), exist_ok=True)
-json.dump(res, open(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "inprocess_bulk_probe.json"), "w"),
+json.dump(res, open(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", os.environ.get("OUT", "inprocess_bulk_probe.json")), "w"),
           indent=1)
 for r in rows:
     print(r)
