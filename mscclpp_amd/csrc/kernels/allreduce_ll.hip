@@ -383,17 +383,22 @@ static void launchLL8(const mscclppAmdRankView* views, int nviews, const LL8Geom
   }
 }
 
-// Default grids.  LL16: a multiple of the peer count (allreduce_packet.cu:164, :180-212 restated
-// for 64-wide waves: the slice is split into 16-byte units, one per lane).
+// Default grids.  LL16: a multiple of the peer count (allreduce_packet.cu:164; its defaults, :180-212,
+// are (n-1)*4 blocks below 32 KiB and (n-1)*8 above).  Restated for this kernel from the fabric-free
+// sweep (tools/inprocess_ll_probe.py, profiles/r2g_inprocess_ll_probe.json, 8 ranks): steps 1 and 3
+// move a peer's slice with G/(n-1) blocks, and every extra pass over it adds a poll round trip, so
+// the blocks per peer cover the slice in one pass, from 4 up to 16 per peer and at most 56 in all;
+// 512 lanes below 32 KiB and from 256 KiB, 256 between.
 static void ll16Defaults(int nranks, size_t bytes, int& nblocks, int& nthreads) {
   const int nPeers = nranks - 1;
   const LL16Geom g = ll16Geometry(nranks, bytes, kF16);
-  if (nthreads <= 0) nthreads = g.units >= 4096 ? 512 : (g.units >= 1024 ? 256 : 128);
+  if (nthreads <= 0) nthreads = (bytes < (32u << 10) || bytes >= (256u << 10)) ? 512 : 256;
   if (nblocks <= 0) {
-    uint64_t want = (g.units + nthreads - 1) / nthreads;  // blocks to cover the slice once
-    if (want < (uint64_t)nPeers) want = nPeers;
-    if (want > 16ull * nPeers) want = 16ull * nPeers;
-    nblocks = (int)want;
+    uint64_t bpp = (g.units + nthreads - 1) / nthreads;  // blocks per peer for one pass
+    if (bpp < 4) bpp = 4;
+    if (bpp > 16) bpp = 16;
+    while (bpp > 1 && bpp * nPeers > 56) --bpp;
+    nblocks = (int)(bpp * nPeers);
   }
   nblocks = nblocks / nPeers * nPeers;
   if (nblocks < nPeers) nblocks = nPeers;
