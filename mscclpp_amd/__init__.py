@@ -437,6 +437,12 @@ class Communicator:
         check(lib().mscclppAmdCommGetDeviceError(self.comm, ctypes.byref(c), 1 if clear else 0), "device error")
         return c.value
 
+    def async_error(self):
+        """ncclCommGetAsyncError: 0 (ncclSuccess), or 6 (ncclRemoteError) once a wait timed out."""
+        c = ctypes.c_int32()
+        check(lib().ncclCommGetAsyncError(self.comm, ctypes.byref(c)), "ncclCommGetAsyncError")
+        return c.value
+
     def registration_stats(self):
         """(user buffers registered, IPC mappings open in this process, mappings awaiting close)."""
         a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
