@@ -263,6 +263,7 @@ def progress(msg):
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+SELECT_NAMES = {1: "packet", 2: "allpair", 3: "fullmesh", 4: "rsag", 5: "rsag_zc", 6: "rsag_pipeline"}
 FULL_NAMES = {"packet": "default_allreduce_packet", "allpair": "default_allreduce_allpair_packet",
               "fullmesh": "default_allreduce_fullmesh", "rsag": "default_allreduce_rsag",
               "rsag_zc": "default_allreduce_rsag_zero_copy", "rsag_pipeline": "default_allreduce_rsag_pipeline"}
@@ -413,8 +414,7 @@ def bench_multi(args):
     # same order).  Large buckets: the scratch-based all-pairs RS+AG (fullmesh, puts), the zero-copy
     # RS+AG (reads peers' inputs, writes peers' outputs) and the pipelined RS+AG -- which one drives
     # xGMI best is measured here, on the node, not assumed.
-    sel = {1: "packet", 2: "allpair", 3: "fullmesh", 4: "rsag", 5: "rsag_zc", 6: "rsag_pipeline"}[
-        m.lib().mscclppAmdSelectAlgo(n, S, 0)]
+    sel = SELECT_NAMES[m.lib().mscclppAmdSelectAlgo(n, S, 0)]
     algos = [args.algo] if args.algo else ([sel] + [a for a in ("fullmesh", "rsag_zc", "rsag_pipeline") if a != sel]
                                            if sel in ("fullmesh", "rsag_zc", "rsag_pipeline") else [sel])
     cands = []
@@ -577,6 +577,9 @@ def bench_multi(args):
         res["xgmi"]["probe_consistent"] = algbw <= mc * 1.02  # an AllReduce cannot beat the raw puts it is made of
     if not args.no_extras:
         res["extras"] = bench_extras(args, comm, n, dev, tmax, dist.barrier)
+        # every measured winner as a ready-to-commit tuned-config profile for this node and scale
+        res["tuned_config_table"] = node_tuned_table(n, torch.cuda.get_device_name(dev), res["extras"],
+                                                     (S, algo, nb, nt))
     # last: on a rehearsal box (ranks sharing one device) the extra stream queues of a graph capture
     # slow every later launch of those ranks, so nothing is measured after it
     progress("graph-captured headline")
@@ -692,11 +695,44 @@ def ndev_shared(n):
 
 
 LL_SWEEP_KIB = tuple(1 << k for k in range(11))  # BASELINE configs[3]: 1 KiB .. 1 MiB, x2 steps
+CROSSOVER_KIB = (4, 8, 16, 32, 64, 256, 512, 1024, 2048, 4096)  # both sides of the 16 KiB and 1 MiB thresholds
+
+
+def node_tuned_table(n, sku, extras, headline):
+    """The node's measured winners as one tuned-config profile (python/mscclpp_benchmark/
+    tuning_config.py format, loaded by MSCCLPP_AMD_TUNED_CONFIG): per measured message size the
+    fastest candidate of the selector-crossover and bulk-size sweeps and the headline's tuning;
+    an entry applies from its message_size up to the next one, so runs of one winner collapse."""
+    pts = []
+    for kb, row in (extras.get("selector_crossover") or {}).items():
+        pts.append((int(kb[:-3]) << 10, row["best"]))
+    for mb, row in (extras.get("bulk_size_sweep") or {}).items():
+        pts.append((int(mb[:-3]) << 20, row["best"]))
+    if headline:
+        pts.append((headline[0], f"{headline[1]}:{headline[2]}x{headline[3]}"))
+    pts.sort(key=lambda p: p[0])  # stable: at a size both sweeps measured, the bulk sweep's row comes last and wins
+    if pts:
+        pts.insert(0, (1, pts[0][1]))
+    entries = []
+    for size, key in pts:
+        algo, shape = key.split(":")
+        nb, nt = (int(v) for v in shape.split("x"))
+        e = {"message_size": size, "algorithm": FULL_NAMES[algo], "nblocks": nb, "nthreads": nt}
+        if entries and {k: v for k, v in entries[-1].items() if k != "message_size"} == \
+                {k: v for k, v in e.items() if k != "message_size"}:
+            continue
+        if entries and entries[-1]["message_size"] == size:
+            entries[-1] = e
+            continue
+        entries.append(e)
+    return {"version": 1, "profiles": [{"sku": sku, "scale": n, "collectives": {"allreduce": entries}}]}
 
 
 def bench_extras(args, comm, n, dev, tmax, barrier):
     """BASELINE configs[3] (LL latency sweep, fp16 1 KiB..1 MiB) and configs[4] (fp32 1 GiB
     RS+AG in ring order), timed the same way; failures are recorded, not raised."""
+    import mscclpp_amd as m
+
     extras = {}
     progress("extras: LL latency sweep")
     try:
@@ -742,6 +778,39 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         del big, bout
     except Exception as e:
         extras["bulk_size_sweep_error"] = str(e)[-300:]
+    progress("extras: selector crossover")
+    try:
+        # both sides of each selector threshold (algorithm_selector.cc:107-131: LL8 / LL16 at 16 KiB,
+        # LL16 / bulk at 1 MiB) timed on this node, default launch shapes for the LL paths
+        cross = {}
+        bulk_c = (("fullmesh", 64, 512), ("rsag_zc", 64, 512))
+        if ndev_shared(n):
+            bulk_c = tuple((a, max(8, 256 // n), 512) for a, _, _ in bulk_c)
+        for kb in CROSSOVER_KIB:
+            cnt = kb * 512
+            xs = torch.rand(cnt, device=dev).half()
+            os_ = torch.empty_like(xs)
+            cands = (("allpair", 0, 0), ("packet", 0, 0)) if kb <= 64 else (("packet", 0, 0),) + bulk_c
+            row = {}
+            for a, nb_, nt_ in cands:
+                try:
+                    for _ in range(3):
+                        comm.all_reduce(xs, os_, algo=a, nblocks=nb_, nthreads=nt_)
+                    torch.cuda.synchronize()
+                    barrier()
+                    row[f"{a}:{nb_}x{nt_}"] = round(tmax(_time_calls(
+                        lambda: comm.all_reduce(xs, os_, algo=a, nblocks=nb_, nthreads=nt_), 20)) * 1e6, 2)
+                except Exception as e:  # noqa: BLE001
+                    row[f"{a}:{nb_}x{nt_}"] = str(e)[:80]
+            best = min((v, k) for k, v in row.items() if isinstance(v, float))
+            # within 3 % the built-in selector's choice stands (timing noise must not flip a threshold)
+            sel = SELECT_NAMES[m.lib().mscclppAmdSelectAlgo(n, kb << 10, 0)]
+            keep = [k for k, v in row.items() if k.startswith(sel + ":") and isinstance(v, float) and v <= 1.03 * best[0]]
+            cross[f"{kb}KiB"] = {"us": row, "best": keep[0] if keep else best[1]}
+            del xs, os_
+        extras["selector_crossover"] = cross
+    except Exception as e:
+        extras["selector_crossover_error"] = str(e)[-300:]
     progress("extras: ReduceScatter / AllGather")
     try:
         # ncclReduceScatter / ncclAllGather (row f2) at the headline bucket: 48 MiB of fp16 in per rank

@@ -80,3 +80,31 @@ def test_malformed_file_is_rejected(built, tmp_path):
     bad.write_text('{"profiles": [{"collectives": {"allreduce": [{"message_size": 0, "algorithm": "x"}]}}]}')
     assert m.lib().mscclppAmdTunedConfigLoad(os.fsencode(str(bad))) == 4
     assert m.lib().mscclppAmdTunedConfigLoad(os.fsencode(str(tmp_path / "missing.json"))) == 4
+
+
+def test_bench_node_table_loads_and_selects(built, tmp_path):
+    """bench.py --gpus N turns its crossover / bulk sweeps into one profile (tuned_config_table); the
+    library must accept it and pick each measured winner from its size up to the next one."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    extras = {"selector_crossover": {"4KiB": {"best": "allpair:0x0"}, "16KiB": {"best": "allpair:0x0"},
+                                     "32KiB": {"best": "packet:0x0"}, "1024KiB": {"best": "packet:0x0"},
+                                     "2048KiB": {"best": "rsag_zc:64x512"}},
+              "bulk_size_sweep": {"2MiB": {"best": "fullmesh:64x512"}, "64MiB": {"best": "rsag_zc:128x512"}}}
+    table = b.node_tuned_table(8, None, extras, (48 << 20, "rsag_zc", 128, 512))
+    entries = table["profiles"][0]["collectives"]["allreduce"]
+    assert [e["message_size"] for e in entries] == [1, 32 << 10, 2 << 20, 48 << 20]  # runs collapsed
+    assert entries[2]["algorithm"] == "default_allreduce_fullmesh"  # the bulk sweep's row wins a tie of sizes
+    del table["profiles"][0]["sku"]  # no GPU here: only a profile without a sku can match
+    path = tmp_path / "node.json"
+    path.write_text(json.dumps(table))
+    q = _query({"MSCCLPP_AMD_TUNED_CONFIG": str(path)})
+    assert q["ar/8/1024"] == ["default_allreduce_allpair_packet", 0, 0]
+    assert q["ar/8/16385"] == ["default_allreduce_allpair_packet", 0, 0]
+    assert q["ar/8/1048576"] == ["default_allreduce_packet", 0, 0]
+    assert q["ar/8/1048577"] == ["default_allreduce_packet", 0, 0]
+    assert q["ar/8/50331648"] == ["default_allreduce_rsag_zero_copy", 128, 512]
+    assert q["ar/4/50331648"][0] == "default_allreduce_fullmesh"  # other scales keep the built-in table
