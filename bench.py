@@ -500,6 +500,7 @@ def bench_multi(args):
                 bitexact[f"{a}:{nbytes >> 10}KiB"] = check_run(a, 0, 0, nbytes)
             except Exception as e:  # recorded, never fatal for the headline line
                 bitexact[f"{a}:{nbytes >> 10}KiB"] = f"error: {e}"[:200]
+    phases = phase_breakdown(m, comm, n, dev, tmax, algo, nb, nt, xs[0], out)
     ok = errc == 0 and all(v is True for v in bitexact.values()) if bitexact else errc == 0
     if not bitexact:  # --no-check: fp32 gloo reference with the tolerance of correctness.py:257-258
         ref = xs[1].float().cpu()
@@ -563,6 +564,7 @@ def bench_multi(args):
         "tune_ms": {f"{k[0]}:{k[1]}x{k[2]}": round(v * 1e3, 4) for k, v in tune.items()},
         "correct": ok,
         "correct_bitexact": bitexact,
+        "phases_us": phases,
     }
     # the winner in the tuned-config format of python/mscclpp_benchmark/tuning_config.py, to be loaded
     # with MSCCLPP_AMD_TUNED_CONFIG (or merged into the built-in table, host/tuning.cpp)
@@ -597,6 +599,37 @@ def bench_multi(args):
     dist.barrier()
     dist.destroy_process_group()
     return res if rank == 0 else None
+
+
+def phase_breakdown(m, comm, n, dev, tmax, algo, nb, nt, x, out):
+    """Where the time of one call goes, per kernel phase (the NPKit role; m.PhaseTrace): the
+    headline winner at its shape and the two LL paths of configs[3] (1 MiB LL16, 16 KiB LL8).  Four
+    calls run back to back with the trace on, so the stamped (last) call starts when its
+    predecessor's handshakes released every rank; each phase's mean and max over workgroups, then
+    the max over ranks.  Untimed, after the headline; failures are recorded, not raised."""
+    res = {}
+    for a, nb_, nt_, nbytes in ((algo, nb, nt, None), ("packet", 0, 0, 1 << 20), ("allpair", 0, 0, 16 << 10)):
+        if a not in m.TRACE_PHASES:
+            continue
+        key = f"{a}:{nb_}x{nt_}" if nbytes is None else f"{a}:{nbytes >> 10}KiB"
+        try:
+            xi, oi = (x, out) if nbytes is None else (x[: nbytes // 2], out[: nbytes // 2])
+            comm.all_reduce(xi, oi, algo=a, nblocks=nb_, nthreads=nt_)
+            torch.cuda.synchronize()
+            with m.PhaseTrace(dev) as tr:
+                for _ in range(4):
+                    comm.all_reduce(xi, oi, algo=a, nblocks=nb_, nthreads=nt_)
+            ph = tr.phases(a)
+            row = {}
+            for name in m.TRACE_PHASES[a]:
+                v = ph.get(name, {"mean_us": 0.0, "max_us": 0.0})
+                row[name] = {"mean_us": round(tmax(v["mean_us"]), 2), "max_us": round(tmax(v["max_us"]), 2)}
+            row["kernel_span_us"] = round(tmax(ph.get("kernel_span_us", 0.0)), 2)
+            row["workgroups"] = ph.get("workgroups", 0)
+            res[key] = row
+        except Exception as e:  # noqa: BLE001
+            res[key] = {"error": str(e)[-200:]}
+    return res
 
 
 def xgmi_probe(comm, n, dev, tmax, barrier, S=64 << 20):

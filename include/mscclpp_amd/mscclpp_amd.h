@@ -148,6 +148,18 @@ int mscclppAmdTunedConfig(const char* collective, int nranks, size_t bytes, char
                           int* nblocks, int* nthreads);
 
 /* ---- communicator extensions -------------------------------------------------------------- */
+// Phase trace of the collective kernels (the reference's NPKit events, npkit.hpp): while a buffer of
+// at least MSCCLPP_AMD_TRACE_BYTES device bytes is set, every AllReduce / ReduceScatter / AllGather
+// launch of this process has lane 0 of each workgroup write the wall clock (s_memrealtime ticks,
+// 100 MHz) at its phase boundaries to buf[(rankView * 256 + workgroup) * 8 + event] (u64).  Events:
+// bulk (fullmesh / rsag): 0 start, 1 reduce-scatter puts issued, 2 reduce-scatter handshake done,
+// 3 reduce + all-gather stores issued, 4 end; zero-copy: 0 start, 1 entry handshake done, 2 reduce +
+// all-gather stores issued, 3 end; LL16: 0 start, 1 step 1 (puts), 2 step 2 (reduce + broadcast),
+// 3 step 3 (unpack) done; LL8: 0 start, 1 puts issued, 2 end.  buf = NULL turns it off.  Returns 0,
+// or 4 when the buffer is too small.
+#define MSCCLPP_AMD_TRACE_BYTES ((size_t)MSCCLPP_AMD_MAX_RANKS * 256 * 8 * 8)
+int mscclppAmdTraceSet(void* buf, size_t bytes);
+
 int mscclppAmdCommAllReduce(ncclComm_t comm, const void* sendbuff, void* recvbuff, size_t count, int ncclDtype,
                             int ncclOp, int algo, int nblocks, int nthreads, void* stream);
 /* As above with the accumulation type of Algorithm::execute (accumNcclDtype: -1 = AUTO, i.e. the

@@ -95,6 +95,7 @@ def lib():
         "mscclppAmdMallocUncached": [ctypes.POINTER(vp), sz],
         "mscclppAmdMalloc": [ctypes.POINTER(vp), sz],
         "mscclppAmdFree": [vp],
+        "mscclppAmdTraceSet": [vp, sz],
         "mscclppAmdFlagsInit": [vp, vp],
         "mscclppAmdSelfReduceLL16": [vp, vp, vp, vp, sz, i32, i32, vp, i32, u64, vp, vp],
         "mscclppAmdAllReduceLaunch": [i32, ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, i32, u64, vp],
@@ -223,6 +224,64 @@ def tuned_config(collective, nranks, nbytes):
 
 def load_tuned_config(path):
     check(lib().mscclppAmdTunedConfigLoad(os.fsencode(path)), f"tuned config {path}")
+
+
+TRACE_BLOCKS, TRACE_EVENTS = 256, 8
+TRACE_BYTES = MAX_RANKS * TRACE_BLOCKS * TRACE_EVENTS * 8
+# phase names per kernel family, in event order (mscclpp_amd.h, mscclppAmdTraceSet)
+TRACE_PHASES = {
+    "fullmesh": ("rs_put", "rs_handshake", "reduce_ag", "exit_handshake"),
+    "rsag": ("rs_put", "rs_handshake", "reduce_ag", "exit_handshake"),
+    "rsag_zc": ("entry_handshake", "reduce_ag", "exit_handshake"),
+    "packet": ("step1_put", "step2_reduce_bcast", "step3_unpack"),
+    "allpair": ("put", "reduce"),
+}
+
+
+class PhaseTrace:
+    """Phase stamps of the collective kernels (the reference's NPKit events): while active, every
+    launch of this process stamps s_memrealtime at its phase boundaries, lane 0 of each workgroup.
+
+        with PhaseTrace() as tr:
+            comm.all_reduce(x, y, algo="fullmesh"); torch.cuda.synchronize()
+        tr.phases("fullmesh")   # {"rs_put": {"mean_us": ..., "max_us": ...}, ...}
+    """
+
+    def __init__(self, device=None):
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.buf = torch.zeros(TRACE_BYTES // 8, dtype=torch.int64, device=dev)
+
+    def __enter__(self):
+        torch.cuda.synchronize()
+        self.buf.zero_()
+        check(lib().mscclppAmdTraceSet(ctypes.c_void_p(self.buf.data_ptr()), TRACE_BYTES), "mscclppAmdTraceSet")
+        return self
+
+    def __exit__(self, *exc):
+        torch.cuda.synchronize()
+        lib().mscclppAmdTraceSet(None, 0)
+        return False
+
+    def stamps(self, view=0):
+        """[workgroup][event] ticks (10 ns) of one rank view; rows of workgroups that never stamped are 0."""
+        import numpy  # noqa: F401  (.numpy() below)
+
+        return self.buf.view(MAX_RANKS, TRACE_BLOCKS, TRACE_EVENTS)[view].cpu().numpy()
+
+    def phases(self, algo, view=0):
+        import numpy as np
+
+        names = TRACE_PHASES[algo]
+        st = self.stamps(view)
+        rows = st[st[:, 0] != 0][:, : len(names) + 1].astype(np.float64)
+        if rows.size == 0:
+            return {}
+        d = np.diff(rows, axis=1) / 100.0  # ticks -> us
+        out = {nm: {"mean_us": round(float(d[:, i].mean()), 2), "max_us": round(float(d[:, i].max()), 2)}
+               for i, nm in enumerate(names)}
+        out["kernel_span_us"] = round(float((rows[:, -1].max() - rows[:, 0].min()) / 100.0), 2)
+        out["workgroups"] = int(rows.shape[0])
+        return out
 
 
 def scratch_required(algo, nranks, nbytes, dtype_code):

@@ -32,6 +32,7 @@ struct BulkGeom {
   uint32_t debug;       // MSCCLPP_AMD_DEBUG_SKIP_HANDSHAKE (bit 0): skip the reduce-scatter handshake.
                         // Diagnostic only -- it makes the result wrong on purpose, so that the
                         // benchmark's bit-exact check can be shown to catch a missing handshake.
+  uint64_t* trace;      // phase stamps (mscclppAmdTraceSet) or null
 };
 
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -78,6 +79,7 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
   uint8_t* out = (uint8_t*)v.output;
   uint8_t* scr = (uint8_t*)v.scratch;
   constexpr int U = 8;  // units per lane per step (128 B in flight per lane in the put phase)
+  trace_stamp(g.trace, 0);
 
   // AllGather writes straight into the peers' outputs: first make sure every peer's kernel is
   // running, i.e. all earlier work on the peer's stream (which may still write that memory, e.g. a
@@ -124,7 +126,9 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
           }
         }
       }
+      trace_stamp(g.trace, 1);
       if (!(g.debug & 1u)) block_handshake(v, nranks, rank, b, budget);
+      trace_stamp(g.trace, 2);
     }
 
     // ---- my slice sub-range: reduce (AR, RS), write locally, and (AR, AG) into every peer's output
@@ -176,8 +180,10 @@ __global__ void __launch_bounds__(512) allreduceBulkKernel(Views<NV> views, Bulk
         }
       }
     }
+    trace_stamp(g.trace, 3);
     block_handshake(v, nranks, rank, b, budget);
   }
+  trace_stamp(g.trace, 4);
 }
 
 // Zero-copy RS+AG (allreduceRsAgZeroCopy, allreduce_rsag_zero_copy.cu:41-112): no scratch.  Each
@@ -197,7 +203,9 @@ __global__ void __launch_bounds__(512) allreduceZeroCopyKernel(Views<NV> views, 
   uint64_t bLen = 0;
   if (bOff < g.slice) bLen = (bOff + g.blk > g.slice) ? g.slice - bOff : g.blk;
   const uint32_t nUnits = (uint32_t)((bLen + 15) / 16);
+  trace_stamp(g.trace, 0);
   block_handshake(v, nranks, rank, b, budget);
+  trace_stamp(g.trace, 1);
   const uint64_t myOff = (uint64_t)rank * g.slice + bOff;
   if (nUnits && myOff < g.bytes) {
     const uint64_t valid = g.bytes - myOff;
@@ -241,7 +249,9 @@ __global__ void __launch_bounds__(512) allreduceZeroCopyKernel(Views<NV> views, 
       }
     }
   }
+  trace_stamp(g.trace, 2);
   block_handshake(v, nranks, rank, b, budget);
+  trace_stamp(g.trace, 3);
 }
 
 // mscclpp-test allreduce5, AMD branch (test/mscclpp-test/allreduce_test.cu:959-970 ->
@@ -505,6 +515,7 @@ static thread_local int g_launch_status = 0;
 
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks) {
   BulkGeom g{};
+  g.trace = g_mscclppAmdTrace;
   g.bytes = bytes;
   const uint64_t per = (bytes + nranks - 1) / nranks;
   g.slice = (per + 15) & ~15ull;
@@ -597,6 +608,7 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
     for (int i = 0; i < nviews; ++i)
       if (views[i].input != views[i].output) return 5;  // allreduce5 runs in place (isInPlace, :1262-1264)
     BulkGeom g{};
+    g.trace = g_mscclppAmdTrace;
     g.bytes = bytes;
     g.slice = bytes / nranks;
     g.pass = g.slice;
@@ -637,6 +649,7 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
   if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC) {
     if (mode != 0) return 4;
     BulkGeom g{};
+    g.trace = g_mscclppAmdTrace;
     g.bytes = bytes;
     g.slice = ((bytes + nranks - 1) / nranks + 15) & ~15ull;
     g.pass = g.slice;
@@ -649,6 +662,7 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
   }
   if (mode != 0 && (bytes % ((size_t)16 * nranks))) return 5;
   BulkGeom g{};
+  g.trace = g_mscclppAmdTrace;
   if (!bulkScratchRequired(nranks, bytes, views[0].scratchBytes, &g, nblocks)) return 5;
   const int order = (algo == MSCCLPP_AMD_ALGO_RSAG && mode != 2) ? 1 : 0;
   static const uint32_t debug = [] {
@@ -768,3 +782,11 @@ int launchAllReduceBulk(int algo, const mscclppAmdRankView* views, int nviews, i
 }
 
 }  // namespace mscclpp_amd
+
+uint64_t* g_mscclppAmdTrace = nullptr;
+
+extern "C" int mscclppAmdTraceSet(void* buf, size_t bytes) {
+  if (buf && bytes < MSCCLPP_AMD_TRACE_BYTES) return 4;
+  g_mscclppAmdTrace = (uint64_t*)buf;
+  return 0;
+}

@@ -34,6 +34,7 @@ struct LL16Geom {
   uint64_t hbEven;  // ... when the flag is even (:60: 0)
   uint32_t units;   // packets per slice (= ppr)
   uint32_t pad;
+  uint64_t* trace;  // phase stamps (mscclppAmdTraceSet) or null
 };
 
 struct LL8Geom {
@@ -41,6 +42,7 @@ struct LL8Geom {
   uint64_t W;       // words (= LL8 packets) per rank buffer (allreduce_allpair_packet.cu:20)
   uint32_t units;   // 2-word units = ceil(W / 2)
   uint32_t pad;
+  uint64_t* trace;  // phase stamps (mscclppAmdTraceSet) or null
 };
 
 // ---- packet-major units ------------------------------------------------------------------------
@@ -131,6 +133,7 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
   const int peerIdx = inPeerGroup ? (int)(b / bpp) : 0;
   const int remote = peerIdx < rank ? peerIdx : peerIdx + 1;
   const uint32_t lb = inPeerGroup ? b % bpp : 0;
+  trace_stamp(g.trace, 0);
 
   // step 1: put my copy of slice `remote` into rank `remote`'s scratch at rank*ppr packets (:89-90)
   if (inPeerGroup) {
@@ -142,6 +145,8 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
       unit_put<kSystem>(rdst, j * 16u, payload_ld(rin, in, off, clamp_valid(send, off, 8)), flag, false);
     }
   }
+
+  trace_stamp(g.trace, 1);
 
   // step 2: reduce my slice from the n-1 incoming streams (own first, then peers ascending,
   // :93-106), store locally, broadcast the reduced packets (:111-122)
@@ -180,6 +185,8 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
     }
   }
 
+  trace_stamp(g.trace, 2);
+
   // step 3: unpack the reduced slice of peer `remote` (:125-132)
   if (inPeerGroup) {
     const auto rres = make_rsrc(scr + g.roff + (uint64_t)remote * g.ppr * 16);
@@ -191,6 +198,7 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
       payload_st(rout, out, off, w, clamp_valid(send, off, 8));
     }
   }
+  trace_stamp(g.trace, 3);
   bump_flags(v.flags, flag);
 }
 
@@ -207,6 +215,7 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
   const auto rin = make_rsrc(in);
   const auto rout = make_rsrc(out);
   const uint64_t region = g.W * 8;  // LL8 bytes one source rank occupies in a peer's scratch half
+  trace_stamp(g.trace, 0);
 
   // put my whole buffer into every peer's scratch at rank*W packets (allreduce_allpair_packet.cu:39-42)
   for (uint32_t j = gtid; j < g.units; j += G * T) {
@@ -220,6 +229,7 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
       unit_put<kSystem>(rq, j * 16u, w, flag, single);
     }
   }
+  trace_stamp(g.trace, 1);
   // reduce: own first, then peers ascending (:49-61).  The same lane handled unit j above, so an
   // in-place call reads its input before overwriting it.
   const auto rscr = make_rsrc((uint8_t*)v.scratch + base);
@@ -245,6 +255,7 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
     }
     payload_st(rout, out, off, sum.template get<u32x2>(), valid);  // downcastVector (:61)
   }
+  trace_stamp(g.trace, 2);
   bump_flags(v.flags, flag);
 }
 
@@ -263,6 +274,7 @@ static inline uint64_t llWords(size_t bytes, int dtype) {
 
 static LL16Geom ll16Geometry(int nranks, size_t bytes, int dtype) {
   LL16Geom g{};
+  g.trace = g_mscclppAmdTrace;
   g.bytes = bytes;
   g.W = llWords(bytes, dtype);
   g.wpr = g.W / (uint64_t)nranks;
@@ -283,6 +295,7 @@ static LL16Geom ll16Geometry(int nranks, size_t bytes, int dtype) {
 
 static LL8Geom ll8Geometry(size_t bytes, int dtype) {
   LL8Geom g{};
+  g.trace = g_mscclppAmdTrace;
   g.bytes = bytes;
   g.W = llWords(bytes, dtype);
   g.units = (uint32_t)((g.W + 1) / 2);
@@ -300,6 +313,7 @@ static LL8Geom ll8Geometry(size_t bytes, int dtype) {
 static bool testLLGeometry(int nranks, size_t bytes, LL16Geom* out) {
   if (bytes == 0 || bytes % (8 * (size_t)nranks)) return false;
   LL16Geom g{};
+  g.trace = g_mscclppAmdTrace;
   g.bytes = bytes;
   g.W = bytes / 4;
   g.wpr = g.W / nranks;

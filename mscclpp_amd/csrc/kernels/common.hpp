@@ -59,6 +59,23 @@ __device__ __forceinline__ void bump_flags(uint32_t* flags, uint32_t flag) {
 
 __device__ __forceinline__ uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Phase trace (the role of the reference's NPKit events, allreduce_packet.cu:20-49, npkit.hpp):
+// with a trace buffer set through mscclppAmdTraceSet, lane 0 of every workgroup stamps the wall
+// clock (s_memrealtime, 10 ns) at the kernel's phase boundaries into
+// trace[(view * kTraceBlocks + block) * kTraceEvents + event], view = the in-process rank index
+// (0 with one rank per process).  Without one the stamps cost one scalar branch each.  The stamp
+// is lane 0's own view of the phase (the other lanes of the workgroup may still be in it).  Only
+// workgroups below kTraceBlocks (and views below kMaxRanks) stamp, so the buffer bound holds.
+constexpr int kTraceEvents = 8;
+constexpr int kTraceBlocks = kMaxChannels;
+__device__ __forceinline__ void trace_stamp(uint64_t* trace, int event) {
+  if (trace && threadIdx.x == 0 && blockIdx.x < (uint32_t)kTraceBlocks && blockIdx.y < (uint32_t)kMaxRanks) {
+    const uint64_t t = wall_ticks();
+    const uint32_t slot = ((uint32_t)blockIdx.y * kTraceBlocks + blockIdx.x) * kTraceEvents + (uint32_t)event;
+    store8<kPlain>(make_rsrc(trace), slot * 8u, u32x2{(uint32_t)t, (uint32_t)(t >> 32)});
+  }
+}
+
 // Kernel argument carrying NV rank views (NV = 1: one rank per process; NV = n: in-process ranks).
 template <int NV>
 struct Views {
@@ -104,3 +121,6 @@ __device__ __forceinline__ uint32_t clamp_valid(uint64_t total, uint64_t off, ui
 }
 
 }  // namespace mscclpp_amd
+
+// The trace buffer the next launches stamp into (null: off); set by mscclppAmdTraceSet.
+extern uint64_t* g_mscclppAmdTrace;
