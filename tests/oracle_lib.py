@@ -5,7 +5,8 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+# MSCCLPP_AMD_ORACLE_SO: another build of the same source (the host-sanitizer test loads an ASan/UBSan one)
+ORACLE_SO = os.environ.get("MSCCLPP_AMD_ORACLE_SO") or os.path.join(ROOT, "oracle", "liboracle.so")
 
 F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
 # OCP fp8 reduce types: element type (e4m3 / e5m2) x accumulation type (element, half, float)
