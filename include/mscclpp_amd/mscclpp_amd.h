@@ -82,8 +82,9 @@ typedef struct {
   int32_t rank;
   int32_t pad;
   const void* peerInput[MSCCLPP_AMD_MAX_RANKS];    /* rank q's input as mapped here (zero-copy reads) */
-  uint64_t* pipeSems;                              /* rsag_pipeline: 3 x 256 intra-launch counters, zeroed
-                                                      before each launch (stream-ordered) */
+  uint64_t* pipeSems;                              /* rsag_pipeline: 3 x 256 + 64 intra-launch counters,
+                                                      zero before the first launch; every launch leaves
+                                                      them zero (graph replays need no memset) */
 } mscclppAmdRankView;
 
 /* ---- memory ------------------------------------------------------------------------------- */

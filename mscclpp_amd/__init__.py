@@ -308,7 +308,7 @@ class InProcessRanks:
         self.expected = [torch.zeros(tok_elems, dtype=torch.int64, device=dev) for _ in range(nranks)]
         self.flags = [torch.ones(FLAG_SLOTS, dtype=torch.int32, device=dev) for _ in range(nranks)]
         self.err = [torch.zeros(64, dtype=torch.int32, device=dev) for _ in range(nranks)]
-        self.pipe_sems = [torch.zeros(3 * 256, dtype=torch.int64, device=dev) for _ in range(nranks)]
+        self.pipe_sems = [torch.zeros(3 * 256 + 64, dtype=torch.int64, device=dev) for _ in range(nranks)]
 
     def views(self, inputs, outputs, bulk=False):
         arr = (RankView * self.n)()

@@ -239,7 +239,8 @@ struct ncclComm {
   // present when MSCCLPP_AMD_NCCL_LIB_PATH names librccl (nccl_compat.cpp)
   void* fallback = nullptr;
   hipStream_t errStream = nullptr;  // ncclCommGetAsyncError's reads
-  uint64_t* pipeSems = nullptr;      // rsag_pipeline's intra-launch counters (3 x 256)
+  static constexpr size_t kPipeSemsWords = 3 * 256 + 64;
+  uint64_t* pipeSems = nullptr;      // rsag_pipeline's intra-launch counters (3 x 256 + done count)
   std::shared_ptr<mscclpp_amd::Executor> executor;
   void buildAlgorithms();
   int rank = 0, nranks = 1, device = 0;
@@ -536,7 +537,10 @@ struct ncclComm {
       v.scratch = bulkScratch;
       v.scratchBytes = bulkBytes;
       for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
-      if (!pipeSems) HIPCHECK(hipMalloc((void**)&pipeSems, 3 * 256 * sizeof(uint64_t)));
+      if (!pipeSems) {  // counters must start at zero; each launch leaves them at zero (allreduce_bulk.hip)
+        HIPCHECK(hipMalloc((void**)&pipeSems, kPipeSemsWords * sizeof(uint64_t)));
+        HIPCHECK(hipMemset(pipeSems, 0, kPipeSemsWords * sizeof(uint64_t)));
+      }
       v.pipeSems = pipeSems;
       return launchAllReducePipeline(&v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
     }

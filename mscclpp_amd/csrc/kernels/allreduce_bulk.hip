@@ -364,9 +364,12 @@ __global__ void __launch_bounds__(512) broadcastKernel(Views<NV> views, uint64_t
 //   recv v   : waits for reduce 2v and 2v+1, handshakes with the peers' recv v (their reduced
 //              slots are in my AG region), copies them into the output, releases the credit.
 // Every remote store lands in communicator-owned scratch (nothing written into peers' user
-// buffers), and the iterations overlap.  Intra-launch counters live in v.pipeSems (zeroed,
-// stream-ordered, before each launch): [0, 256) recv->put credits, [256, 512) put->reduce,
-// [512, 768) reduce->recv.
+// buffers), and the iterations overlap.  Intra-launch counters live in v.pipeSems: [0, 256)
+// recv->put credits, [256, 512) put->reduce, [512, 768) reduce->recv, [768] workgroups done.  They
+// are zero when a launch starts: zeroed once at allocation, and the last workgroup of every launch
+// to finish puts them back to zero (a stream-ordered memset before each launch did the same in
+// eager mode, but in a replayed HIP graph the kernel read the previous replay's counters -- every
+// replay after the first came back with stale data, tests/test_graph_capture_gpu.py).
 struct PipeGeom {
   uint64_t bytes;   // buffer bytes
   uint64_t C;       // units per slot and iteration
@@ -380,6 +383,24 @@ __device__ __forceinline__ void sem_release(uint64_t* c) {
   drain_stores();
   __syncthreads();
   if (threadIdx.x == 0) add_release_agent(c, 1);
+}
+
+// End of a pipeline workgroup: count it done; the last of the launch's `total` workgroups (every
+// other one has made its last counter access before counting itself) zeroes the counters for the
+// next launch.
+__device__ __forceinline__ void pipe_done(uint64_t* sems, uint32_t R, uint32_t total) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (add_release_agent(sems + 768, 1) == total - 1) {
+      acquire_agent();
+      for (uint32_t i = 0; i < R / 2; ++i) __hip_atomic_store(sems + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t i = 0; i < R; ++i) {
+        __hip_atomic_store(sems + 256 + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sems + 512 + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(sems + 768, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 __device__ __forceinline__ void sem_acquire(uint64_t* c, uint64_t target, uint64_t budget, uint32_t* err) {
@@ -443,6 +464,7 @@ __global__ void __launch_bounds__(512) allreduceRsAgPipelineKernel(Views<NV> vie
       // (thread 0's release above already wrote the L2 back and waited: a relaxed add stays behind it)
       if (tid == 0) __hip_atomic_fetch_add(&toReduce[2 * p + 1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    pipe_done(v.pipeSems, g.R, 2 * g.R);
   } else if (bid < P + g.R) {  // ---- reduce
     const uint32_t b = bid - P, p = b / 2, sub = b % 2;
     for (uint32_t it = 0; it < g.nIters; ++it) {
@@ -475,6 +497,7 @@ __global__ void __launch_bounds__(512) allreduceRsAgPipelineKernel(Views<NV> vie
       }
       sem_release(&toRecv[b]);
     }
+    pipe_done(v.pipeSems, g.R, 2 * g.R);
   } else {  // ---- recv
     const uint32_t r = bid - P - g.R;
     for (uint32_t it = 0; it < g.nIters; ++it) {
@@ -508,6 +531,7 @@ __global__ void __launch_bounds__(512) allreduceRsAgPipelineKernel(Views<NV> vie
     // that peer is still copying it.  The peers' reduce workgroups are done too: their recv waited
     // for them.  Same channel as the entry handshakes, so every rank's counters stay in step.
     block_handshake(v, nranks, rank, g.R + r, budget);
+    pipe_done(v.pipeSems, g.R, 2 * g.R);
   }
 }
 
@@ -754,8 +778,6 @@ int launchAllReducePipeline(const mscclppAmdRankView* views, int nviews, int nra
   for (int i = 1; i < nviews; ++i) minScratch = views[i].scratchBytes < minScratch ? views[i].scratchBytes : minScratch;
   uint64_t D = minScratch / stage;
   g.D = (uint32_t)(D > g.nIters ? (g.nIters ? g.nIters : 1) : D);
-  for (int i = 0; i < nviews; ++i)
-    if (hipMemsetAsync(views[i].pipeSems, 0, 3 * 256 * sizeof(uint64_t), s) != hipSuccess) return 1;
   g_launch_status = 0;
   if (dtype == kF16)
     op == kMin ? launchPipeline<kF16, kMin>(views, nviews, g, nranks, nthreads, budget, s)

@@ -1,0 +1,119 @@
+"""AllReduce captured in a HIP graph (torch.cuda.CUDAGraph) and replayed with new data, two processes
+through the NCCL ABI: the way frameworks run collectives inside captured steps, and the way the
+reference's harness times them (test/mscclpp-test/common.cc:202-227).  Every replay must read the
+inputs as they are at replay time and produce the oracle's bits: the LL flags and the bulk
+semaphore counters live in device memory and advance inside the kernels, so nothing captured goes
+stale between replays.  Buffers are registered by one eager call before the capture (a new buffer
+costs a host exchange, which has no place inside a capture)."""
+import multiprocessing as mp
+import queue
+import traceback
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("allpair", 0, 4096), ("packet", 0, 1 << 17), ("fullmesh", 0, 1 << 20), ("rsag", 2, 100000),
+         ("rsag_zc", 0, 1 << 20), ("rsag_pipeline", 2, 1 << 18)]
+REPLAYS = 3
+
+
+def _expected(O, algo, dt, count, ins, rank, n):
+    nbytes = count * (2 if dt < 2 else 4)
+    if algo == "packet":
+        exp, _ = O.allreduce_packet(dt, O.SUM, ins, count, 1, 1 << 22)
+        return exp[rank].view(np.uint8)[:nbytes]
+    if algo == "allpair":
+        exp, _ = O.allreduce_allpairs(dt, O.SUM, ins, count, 1, 1 << 22)
+        return exp[rank].view(np.uint8)[:nbytes]
+    nw = (nbytes + 3) // 4
+    pad = []
+    for a in ins:
+        w = np.zeros(nw, np.uint32)
+        w.view(np.uint8)[:nbytes] = a.view(np.uint8)
+        pad.append(w)
+    if algo == "rsag_pipeline":
+        return None  # interleaved ownership: checked against fp32 sums with the tolerance below
+    sl = ((nbytes + n - 1) // n + 15) // 16 * 16
+    order = 1 if algo in ("rsag", "rsag_zc") else 0
+    return O.allreduce_sliced(dt, O.SUM, pad, nw, sl // 4, order)[rank].view(np.uint8)[:nbytes]
+
+
+def _worker(rank, n, uid, q):
+    try:
+        import os
+
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "5000")
+        import torch
+
+        import mscclpp_amd as m
+        import oracle_lib as O
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        tdt = {0: torch.float16, 2: torch.float32}
+        out = []
+        for algo, dt, count in CASES:
+            x = torch.zeros(count, dtype=tdt[dt], device="cuda")
+            y = torch.zeros_like(x)
+            comm.all_reduce(x, y, algo=algo)  # registers x and y (host exchange) outside the capture
+            torch.cuda.synchronize()
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                comm.all_reduce(x, y, algo=algo)
+            torch.cuda.synchronize()
+            bad = []
+            for k in range(REPLAYS):
+                ins = [O.lcg(dt, count, r, 20 + k) for r in range(n)]
+                x.copy_(torch.from_numpy(ins[rank].view(np.int16 if dt < 2 else np.int32).copy()).view(tdt[dt]))
+                y.fill_(-1)
+                torch.cuda.synchronize()
+                g.replay()
+                torch.cuda.synchronize()
+                got = y.cpu().contiguous().view(torch.uint8).numpy()
+                e = _expected(O, algo, dt, count, ins, rank, n)
+                if e is None:
+                    ref = sum(a.view(np.float32).astype(np.float64) for a in ins)
+                    ok = np.allclose(got.view(np.float32), ref, rtol=1e-5, atol=1e-5)
+                    bad.append(0 if ok else 1)
+                else:
+                    bad.append(int(np.count_nonzero(got != e)))
+            out.append((algo, bad, comm.device_error()))
+            del g
+        comm.barrier()
+        comm.destroy()
+        q.put((rank, out, None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_captured_allreduce_replays_with_new_data(built):
+    import mscclpp_amd as m
+
+    n = 2
+    uid = m.Communicator.unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, n, uid, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=240)
+            assert err is None, err
+            got[rank] = res
+    except queue.Empty:
+        pytest.fail("graph-captured AllReduce timed out")
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        for algo, bad, errc in got[rank]:
+            assert errc == 0, (rank, algo, errc)
+            assert bad == [0] * REPLAYS, (rank, algo, bad)
