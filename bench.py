@@ -587,10 +587,23 @@ def bench_multi(args):
     progress("graph-captured headline")
     try:
         # common.cc:202-227: 20 calls captured in one graph, 15 graph launches, per-call time
-        g_s = tmax(graph_time_per_call(lambda: comm.all_reduce(xs[0], out, algo=algo, nblocks=nb, nthreads=nt),
-                                       calls=20, replays=15, sync=dist.barrier))
+        g_s, graph = graph_time_per_call(lambda: comm.all_reduce(xs[0], out, algo=algo, nblocks=nb, nthreads=nt),
+                                         calls=20, replays=15, sync=dist.barrier, keep=True)
+        g_s = tmax(g_s)
         res["graph"] = {"us_per_call": round(g_s * 1e6, 2), "algbw_GBs": round(S / g_s / 1e9, 2),
                         "note": "20 calls per HIP graph, 15 launches (mscclpp-test common.cc:202-227); value stays the eager loop"}
+        if checker is not None:  # a replay reads the input as it is at replay time: new data, poisoned output
+            xs[0].copy_(xs[1])
+            poison(out)
+            torch.cuda.synchronize()
+            dist.barrier()
+            graph.replay()
+            torch.cuda.synchronize()
+            exp = checker.expected(algo, nb, nt, 1, None, rank)
+            res["graph"]["replay_bitexact"] = all_ok(bool(np.array_equal(BitExactChecker.words(out), exp))
+                                                     and device_matches(out, exp) and comm.device_error() == 0)
+            res["correct"] = bool(res["correct"] and res["graph"]["replay_bitexact"])
+        del graph
     except Exception as e:  # recorded, never fatal for the headline line
         res["graph"] = {"error": str(e)[-300:]}
     # cpu_baseline is an N=1 field (the oracle timed on rank 0 at N=1 only); at N>1 the reference's
@@ -700,10 +713,10 @@ def xgmi_probe(comm, n, dev, tmax, barrier, S=64 << 20):
     return out
 
 
-def graph_time_per_call(fn, calls=20, replays=10, sync=None):
+def graph_time_per_call(fn, calls=20, replays=10, sync=None, keep=False):
     """Per-call time with `calls` calls captured in one HIP graph (mscclpp-test common.cc:202-227).
     `sync` (a host barrier across ranks) lines the ranks up before the timed replays, so the first
-    replay does not absorb another rank's late start."""
+    replay does not absorb another rank's late start.  keep=True: (time, graph)."""
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -719,7 +732,8 @@ def graph_time_per_call(fn, calls=20, replays=10, sync=None):
     torch.cuda.synchronize()
     if sync is not None:
         sync()
-    return _time_calls(g.replay, replays) / calls
+    t = _time_calls(g.replay, replays) / calls
+    return (t, g) if keep else t
 
 
 def ndev_shared(n):
