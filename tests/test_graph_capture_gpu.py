@@ -1,6 +1,7 @@
 """AllReduce captured in a HIP graph (torch.cuda.CUDAGraph) and replayed with new data, two processes
 through the NCCL ABI: the way frameworks run collectives inside captured steps, and the way the
-reference's harness times them (test/mscclpp-test/common.cc:202-227).  Every replay must read the
+reference's harness times them (test/mscclpp-test/common.cc:202-227); ncclReduceScatter and
+ncclAllGather are captured together as well.  Every replay must read the
 inputs as they are at replay time and produce the oracle's bits: the LL flags and the bulk
 semaphore counters live in device memory and advance inside the kernels, so nothing captured goes
 stale between replays.  Buffers are registered by one eager call before the capture (a new buffer
@@ -83,6 +84,36 @@ def _worker(rank, n, uid, q):
                     bad.append(int(np.count_nonzero(got != e)))
             out.append((algo, bad, comm.device_error()))
             del g
+        # ncclReduceScatter then ncclAllGather (fp32, block 8192) captured together
+        block = 8192
+        x = torch.zeros(block * n, dtype=torch.float32, device="cuda")
+        rs = torch.zeros(block, dtype=torch.float32, device="cuda")
+        ag = torch.zeros(block * n, dtype=torch.float32, device="cuda")
+        comm.reduce_scatter(x, rs)
+        comm.all_gather(rs, ag)
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            comm.reduce_scatter(x, rs)
+            comm.all_gather(rs, ag)
+        torch.cuda.synchronize()
+        bad = []
+        for k in range(REPLAYS):
+            ins = [O.lcg(2, block * n, r, 60 + k) for r in range(n)]
+            x.copy_(torch.from_numpy(ins[rank].view(np.int32).copy()).view(torch.float32))
+            rs.fill_(-1)
+            ag.fill_(-1)
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            e = O.allreduce_sliced(2, O.SUM, [a.view(np.uint32) for a in ins], block * n, block, 0)[0]
+            got_ag = ag.cpu().numpy().view(np.uint32)
+            got_rs = rs.cpu().numpy().view(np.uint32)
+            bad.append(int(np.count_nonzero(got_ag != e)) + int(np.count_nonzero(got_rs != e[rank * block:(rank + 1) * block])))
+        out.append(("reducescatter+allgather", bad, comm.device_error()))
+        del g
         comm.barrier()
         comm.destroy()
         q.put((rank, out, None))
