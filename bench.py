@@ -420,7 +420,7 @@ def bench_multi(args):
     cands = []
     shared = ndev < world  # rehearsal: ranks share a device, so every rank's grid must fit on it at once
     # rehearsal shapes: small enough that every rank's grid is resident on the one shared device
-    bulk_shapes = ((64, 512), (128, 512), (256, 512), (128, 256), (256, 256)) if not shared else \
+    bulk_shapes = ((32, 512), (64, 512), (128, 512), (256, 512), (128, 256), (256, 256)) if not shared else \
         tuple((nb_, 512) for nb_ in (16, 32, 64, 128) if nb_ * world <= 256)
     pipe_shapes = ((32, 512), (64, 512), (128, 512), (64, 256)) if not shared else \
         tuple((nb_, 512) for nb_ in (8, 16, 32, 64) if 2 * nb_ * world <= 256)
