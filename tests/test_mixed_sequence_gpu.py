@@ -53,6 +53,8 @@ def _worker(rank, n, uid, q):
         import time
 
         os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "8000")
+        if n > 2:  # many ranks on one device: one hardware queue each keeps every rank's queue mapped
+            os.environ["GPU_MAX_HW_QUEUES"] = "1"
         import torch
 
         import mscclpp_amd as m
@@ -71,7 +73,7 @@ def _worker(rank, n, uid, q):
         comm.barrier()
         for i, (algo, count) in enumerate(seq):
             if rank == 1 and i % 3 == 1:
-                time.sleep(0.02)  # rank 1 launches late: its peer runs ahead by a call
+                time.sleep(0.02)  # rank 1 launches late: its peers run ahead by a call
             _, x, y = data[i]
             comm.all_reduce(x, y, algo=algo)
         torch.cuda.synchronize()
@@ -95,10 +97,10 @@ def _worker(rank, n, uid, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-def test_mixed_algorithm_sequence_back_to_back(built):
+@pytest.mark.parametrize("n", [2, 4])
+def test_mixed_algorithm_sequence_back_to_back(built, n):
     import mscclpp_amd as m
 
-    n = 2
     uid = m.Communicator.unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
