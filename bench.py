@@ -104,6 +104,21 @@ def committed_traffic(S):
     return d.get("hbm_bytes_per_launch_corrected")
 
 
+def committed_multirank_pmc(kernel):
+    """read / write byte ratios of `kernel` from profiles/*_multirank_pmc.json (tools/pmc_multirank.sh), or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_multirank_pmc.json")))
+    if not files:
+        return None
+    ks = json.load(open(files[-1])).get("kernels", {})
+    name = {"allreduceZeroCopyKernel": "allreduceZeroCopyKernel<0, 0, 8>"}.get(
+        kernel, "allreduceBulkKernel<0, 0, 8, 0, 0>" if kernel.startswith("allreduceBulkKernel") else None)
+    k = ks.get(name) if name else None
+    return None if k is None else {"read_ratio": k["read_ratio"], "write_ratio": k["write_ratio"],
+                                   "source": os.path.basename(files[-1])}
+
+
 def host_proxy_baseline():
     """BASELINE config 1 (host-proxy path, 2 ranks, 4 KiB) -- spawned before this process touches the GPU."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -558,7 +573,10 @@ def bench_multi(args):
                      "algorithmic_bytes_per_launch": int(wire),
                      "hbm": {"achieved": round(hbm / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                              "frac": round(hbm / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                             "bytes_per_launch": int(hbm)}},
+                             "bytes_per_launch": int(hbm)},
+                     # traffic stays null: no counters run on the node.  The committed fabric-free PMC
+                     # run of the same kernel (8 in-process ranks) gives its bytes over its algorithmic ones
+                     "pmc_fabric_free": committed_multirank_pmc(kernel)},
         "xgmi": {"allpairs_algbw_ceiling_assumed": round(ceiling, 1), "frac_of_assumed_ceiling": round(algbw / ceiling, 4),
                  "link_GBs_assumed": XGMI_LINK_GBS, "wire_bytes_per_rank": int(wire), "measured": probe},
         "tune_ms": {f"{k[0]}:{k[1]}x{k[2]}": round(v * 1e3, 4) for k, v in tune.items()},
