@@ -347,10 +347,16 @@ struct ncclComm {
   //  * At most kMaxUserRegs allocations stay registered; the least recently used one is retired
   //    beyond that (every rank sees the same sequence of buffers, so every rank evicts the same).
   //  * Retired mappings close after a device synchronize (flushRetired), never under a running kernel.
+  //  * A registration used while its stream is capturing a HIP graph is pinned: the graph keeps
+  //    the peer pointers in its kernel arguments, so evicting it (and closing the mappings) would
+  //    leave every later replay writing through closed mappings.  Pinned entries are never evicted
+  //    (the cap then only bounds the unpinned ones); capture happens in the same calls on every
+  //    rank, so every rank pins the same.
   static constexpr size_t kMaxUserRegs = 64;
   struct UserReg {
     uint64_t bufferId = 0;
     uint64_t lastUse = 0;
+    bool pinned = false;  // used under stream capture
     PeerBufs bases;
     std::map<uint64_t, std::array<void*, MSCCLPP_AMD_MAX_RANKS>> byOffset;
   };
@@ -378,10 +384,12 @@ struct ncclComm {
       it = userRegs.end();
     }
     if (it == userRegs.end()) {
-      if (userRegs.size() >= kMaxUserRegs) {
-        auto lru = userRegs.begin();
+      size_t unpinned = 0;
+      for (const auto& e : userRegs) unpinned += e.second.pinned ? 0 : 1;
+      if (unpinned >= kMaxUserRegs) {
+        auto lru = userRegs.end();
         for (auto j = userRegs.begin(); j != userRegs.end(); ++j)
-          if (j->second.lastUse < lru->second.lastUse) lru = j;
+          if (!j->second.pinned && (lru == userRegs.end() || j->second.lastUse < lru->second.lastUse)) lru = j;
         retireReg(lru);
       }
       UserReg reg;
@@ -392,6 +400,10 @@ struct ncclComm {
     }
     UserReg& reg = it->second;
     reg.lastUse = ++useClock;
+    if (stream) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) reg.pinned = true;
+    }
     const uint64_t off = (uint64_t)((char*)out - (char*)base);
     auto pit = reg.byOffset.find(off);
     if (pit == reg.byOffset.end()) {

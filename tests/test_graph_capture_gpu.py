@@ -148,3 +148,87 @@ def test_captured_allreduce_replays_with_new_data(built):
         for algo, bad, errc in got[rank]:
             assert errc == 0, (rank, algo, errc)
             assert bad == [0] * REPLAYS, (rank, algo, bad)
+
+
+def _churn_worker(rank, n, uid, q):
+    try:
+        import os
+
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "5000")
+        import torch
+
+        import mscclpp_amd as m
+        import oracle_lib as O
+
+        torch.cuda.set_device(0)
+        comm = m.Communicator(rank, n, uid)
+        count = 6 << 20  # 12 MiB: above the caching allocator's 10 MiB packing, so its own segment
+        x = torch.zeros(count, dtype=torch.float16, device="cuda")
+        y = torch.zeros_like(x)
+        comm.all_reduce(x, y, algo="rsag_zc")
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            comm.all_reduce(x, y, algo="rsag_zc")  # pins x's and y's registrations
+        torch.cuda.synchronize()
+        pinned = comm.registration_stats()[0]
+        # more fresh allocations than the registration cache holds (64), each its own segment
+        keep = []
+        for i in range(70):
+            a = torch.full((6 << 20,), float(i % 7), dtype=torch.float16, device="cuda")
+            b = torch.empty_like(a)
+            comm.all_reduce(a, b, algo="rsag_zc")
+            keep.append((a, b))
+        torch.cuda.synchronize()
+        regs, live, retired = comm.registration_stats()
+        res = {"regs": regs, "pinned": pinned}
+        if pinned >= 1 and regs == 64 + pinned:  # every pinned registration survived: replaying is safe
+            ins = [O.lcg(O.F16, count, r, 77) for r in range(n)]
+            x.copy_(torch.from_numpy(ins[rank].view(np.int16).copy()).view(torch.float16))
+            y.fill_(-1)
+            torch.cuda.synchronize()
+            comm.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            e = _expected(O, "rsag_zc", 0, count, ins, rank, n)
+            res["bad"] = int(np.count_nonzero(y.cpu().contiguous().view(torch.uint8).numpy() != e))
+            res["err"] = comm.device_error()
+        del g, keep
+        comm.barrier()
+        comm.destroy()
+        q.put((rank, res, None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_captured_buffers_survive_registration_churn(built):
+    """A graph keeps the peer pointers of its buffers: their registrations must not be evicted by
+    later eager calls on 140 other buffers (the cache holds 64), or the replay would write through
+    closed mappings.  The pin is checked through the registration count before anything replays."""
+    import mscclpp_amd as m
+
+    n = 2
+    uid = m.Communicator.unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_churn_worker, args=(r, n, uid, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=240)
+            assert err is None, err
+            got[rank] = res
+    except queue.Empty:
+        pytest.fail("registration churn case timed out")
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in range(n):
+        assert got[rank]["pinned"] >= 1 and got[rank]["regs"] == 64 + got[rank]["pinned"], got
+        assert got[rank]["bad"] == 0 and got[rank]["err"] == 0, got
