@@ -53,43 +53,100 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline_self_reduce(nbytes, budget_s):
-    """Oracle (scalar C port, 1 thread) pack+sum+unpack on the same workload, bounded in time."""
+def cpu_threads():
+    """Threads for the all-core CPU figures: the CPUs this process may use, capped by OMP_NUM_THREADS
+    where the pool sets it (16 per GPU on the GPU boxes, whose nproc shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else n
+
+
+def _parallel_rate(work, threads, budget_s, max_iters):
+    """Run work(t) for t in range(threads) on a thread pool (the oracle's ctypes calls release the
+    GIL), repeatedly until budget_s; returns (iterations, seconds).  One untimed warm pass first."""
+    import concurrent.futures as cf
+
+    with cf.ThreadPoolExecutor(threads) as ex:
+        list(ex.map(work, range(threads)))
+        iters, t0 = 0, time.perf_counter()
+        while True:
+            list(ex.map(work, range(threads)))
+            iters += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s or iters >= max_iters:
+                return iters, el
+
+
+def _sum_parts(n_src, nbytes, threads):
+    """The inputs, output and per-thread slices of cpu_baseline_sum."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
 
-    count = nbytes // 2
-    x = O.lcg(O.F16, count, 0, 0)
-    y = O.lcg(O.F16, count, 1, 0)
-    iters, t0 = 0, time.perf_counter()
-    while True:
-        O.self_reduce(O.F16, O.SUM, x, y, iters + 1)
-        iters += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or iters >= 200:
-            break
-    return {"value": round(nbytes * iters / el / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{iters} x oracle_self_reduce fp16 {nbytes >> 20} MiB (scalar C, 1 thread) in {el:.1f} s"}
+    nw = nbytes // 4
+    ins = [O.lcg(O.F16, nbytes // 2, r, 0).view(np.uint32) for r in range(n_src)]
+    out = np.empty(nw, np.uint32)
+    parts = []
+    for t in range(threads):
+        a, b = nw * t // threads, nw * (t + 1) // threads
+        parts.append(((ctypes.c_void_p * n_src)(*[x.ctypes.data + 4 * a for x in ins]), b - a,
+                      ctypes.c_void_p(out.ctypes.data + 4 * a)))
+
+    def work(t):
+        srcs, words, dst = parts[t]
+        if words:
+            O.L().oracle_reduce_seq(O.F16, O.SUM, n_src, srcs, words, dst)
+
+    return ins, out, work
 
 
-def cpu_baseline_allreduce(nbytes, n, budget_s):
-    """Oracle fullmesh-order AllReduce arithmetic for n ranks on a bounded slice of the bucket."""
+def _threaded_sum_for_test(n_src, nbytes, threads):
+    ins, out, work = _sum_parts(n_src, nbytes, threads)
+    for t in range(threads):
+        work(t)
+    return out
+
+
+def cpu_baseline_sum(n_src, nbytes, budget_s, threads=None):
+    """SURVEY §8(d)'s CPU context figure: the oracle's fp16 n-way sum (own, then ascending -- the
+    fullmesh order of rank 0, oracle_reduce_seq) of n LCG buckets of `nbytes`, the bucket split over
+    `threads` threads; GB/s = result bytes (one bucket per AllReduce) per second, as `value`."""
+    threads = threads or cpu_threads()
+    ins, out, work = _sum_parts(n_src, nbytes, threads)
+    iters, el = _parallel_rate(work, threads, budget_s, 1000)
+    return {"value": round(nbytes * iters / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(),
+            "sample": f"{iters} x oracle fp16 {n_src}-way sum (own then ascending) of {n_src} x {nbytes >> 20} MiB "
+                      f"LCG buckets, split over {threads} threads, in {el:.1f} s"}
+
+
+def cpu_baseline_self_reduce(nbytes, budget_s, threads=1):
+    """The N=1 workload itself on the CPU: the oracle's pack + sum + unpack (oracle_self_reduce) of
+    the same 48 MiB fp16 bucket, split over `threads` threads (LL16 packets pair words: even slices)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
 
-    sample = min(nbytes, 8 << 20)
-    count = sample // 2
-    ins = [O.lcg(O.F16, count, r, 0).view(np.uint32) for r in range(n)]
-    nw = sample // 4
-    iters, t0 = 0, time.perf_counter()
-    while True:
-        O.allreduce_sliced(O.F16, O.SUM, ins, nw, nw // n, 0)
-        iters += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or iters >= 1000:
-            break
-    return {"value": round(sample * iters / el / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{iters} x oracle {n}-rank fullmesh-order fp16 sum of {sample >> 20} MiB (scalar C, 1 thread)"}
+    nw = nbytes // 4
+    x = O.lcg(O.F16, nbytes // 2, 0, 0).view(np.uint32)
+    y = O.lcg(O.F16, nbytes // 2, 1, 0).view(np.uint32)
+    pk = np.empty(2 * nw, np.uint32)
+    out = np.empty(nw, np.uint32)
+    L = O.L()
+    cut = [nw * t // threads // 2 * 2 for t in range(threads)] + [nw]
+
+    def work(t):
+        a, b = cut[t], cut[t + 1]
+        if b > a:
+            L.oracle_self_reduce(O.F16, O.SUM, ctypes.c_void_p(x.ctypes.data + 4 * a),
+                                 ctypes.c_void_p(y.ctypes.data + 4 * a), b - a, 1,
+                                 ctypes.c_void_p(pk.ctypes.data + 8 * a), ctypes.c_void_p(out.ctypes.data + 4 * a))
+
+    iters, el = _parallel_rate(work, threads, budget_s, 200)
+    return {"value": round(nbytes * iters / el / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{iters} x oracle_self_reduce fp16 {nbytes >> 20} MiB (pack + sum + unpack, scalar C) "
+                      f"over {threads} thread(s) in {el:.1f} s"}
 
 
 def committed_traffic(S):
@@ -243,6 +300,10 @@ def bench_single(args):
     if args.no_extras:  # profiling runs: only the headline launches, so per-kernel stats are of one size
         pk.free()
         return res
+    # the same run's ceilings beside the headline: a streaming copy of the
+    # bucket (read S + write S), and the kernel from a cold Infinity Cache (a 512 MiB write between
+    # launches evicts the 240 MiB working set that back-to-back launches find in the 256 MiB MALL)
+    res["roofline"].update(same_run_ceilings(m, S, x, y, pk, out, flags, err, kern_ms))
     res["staged_pcie_inclusive"] = staged_rate(m, S, x, y, out, pk, flags, err)
     # BASELINE configs[1] sweep, 64 KiB .. 48 MiB in x2 steps: per-launch time with 20 launches
     # captured in one HIP graph (device time, not host launch rate)
@@ -256,10 +317,64 @@ def bench_single(args):
                                    "hbm_7S_TBs": round(7 * sz / us / 1e6, 3)}
     res["sweep"] = sweep
     if not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline_self_reduce(S, args.cpu_seconds)
+        # the oracle's fp16 8-way sum on the box's cores; beside it the N=1 workload
+        # itself (pack + sum + unpack) on one core and on all of them, and the host-proxy path
+        res["cpu_baseline"] = cpu_baseline_sum(8, S, args.cpu_seconds)
+        res["cpu_baseline_self_reduce"] = {"1_thread": cpu_baseline_self_reduce(S, args.cpu_seconds / 2, 1),
+                                           "all_threads": cpu_baseline_self_reduce(S, args.cpu_seconds / 2,
+                                                                                   cpu_threads())}
         res["host_proxy_baseline"] = hp
     pk.free()
     return res
+
+
+def same_run_ceilings(m, S, x, y, pk, out, flags, err, kern_ms, reps=20):
+    """Copy ceiling and cold-cache time of the headline kernel, measured in this run."""
+    L = m.lib()
+    vp = ctypes.c_void_p
+    dst = torch.empty_like(x)
+
+    def copy():
+        m.check(L.mscclppAmdCopy(vp(x.data_ptr()), vp(dst.data_ptr()), S, 0, m.stream_ptr()), "copy")
+
+    copy()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        copy()
+    b.record()
+    torch.cuda.synchronize()
+    copy_us = a.elapsed_time(b) * 1e3 / reps
+    copy_gbs = 2 * S / (copy_us * 1e-6) / 1e9
+    scrub = torch.empty(512 << 20, dtype=torch.uint8, device=x.device)
+
+    def one_pair(cold):
+        if cold:
+            scrub.fill_(1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        m.self_reduce_ll16(x, y, pk.ptr, out, flags, err)
+        e1.record()
+        return e0, e1
+
+    res = {}
+    for name, cold in (("warm_pair", False), ("cold", True)):
+        evs = [one_pair(cold) for _ in range(reps)]
+        torch.cuda.synchronize()
+        res[name] = float(np.median([e0.elapsed_time(e1) * 1e3 for e0, e1 in evs]))
+    del scrub, dst
+    seven = 7 * S
+    return {"copy_ceiling_GBs": round(copy_gbs, 1), "copy_ceiling_frac": round(copy_gbs / HBM_PEAK_GBS, 4),
+            "copy_us": round(copy_us, 2),
+            "frac_of_copy_ceiling": round(seven / (kern_ms * 1e-3) / 1e9 / copy_gbs, 4),
+            "cold": {"kernel_us": round(res["cold"], 2),
+                     "achieved": round(seven / (res["cold"] * 1e-6) / 1e9, 1),
+                     "frac": round(seven / (res["cold"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                     "warm_same_method_us": round(res["warm_pair"], 2),
+                     "method": "median of 20 launches, one event pair each; cold: a 512 MiB fill before each launch"},
+            "note": "frac is the warm back-to-back replay (the 240 MiB working set fits the 256 MiB Infinity Cache); "
+                    "cold and the same run's streaming-copy ceiling beside it"}
 
 
 def _time_calls(fn, reps):
@@ -360,6 +475,12 @@ def bench_multi(args):
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    # CPU baselines first, on rank 0 before this process touches a GPU (the other ranks wait in the
+    # rendezvous below): the reference's host-proxy path (config 1, its own two processes) and the
+    # oracle's n-way sum of the bucket on this box's cores
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = {"host_proxy": host_proxy_baseline(), "sum": cpu_baseline_sum(world, args.bytes, args.cpu_seconds)}
     ndev = torch.cuda.device_count()
     if ndev < world:  # rehearsal on a smaller box: ranks share devices (never the case on the 8-GPU node)
         local = local % ndev
@@ -522,24 +643,12 @@ def bench_multi(args):
         dist.all_reduce(ref)
         ok = bool(torch.allclose(out.float().cpu(), ref, rtol=1e-2, atol=5e-4 * n)) and errc == 0
     algbw = S / t / 1e9
-    ceiling = n * XGMI_LINK_GBS / 2  # all-pairs algbw ceiling at the assumed link rate
-    wire = 2 * (n - 1) * S / n  # bytes each rank moves out over xGMI per AllReduce (all-pairs RS + AG)
-    wire_ach = wire / (kern_ms * 1e-3) / 1e9
-    # HBM bytes one rank's AllReduce moves.  fullmesh/rsag: reads S input + (n-1)/n S scratch;
-    # writes S/n own output + (n-1)/n S incoming scratch + (n-1)/n S incoming output.  rsag_zc: reads
-    # S of input (own slice locally, the rest by the peers), writes S of output (own slice locally,
-    # the rest by the peers).  rsag_pipeline: reads S input + 2(n-1)/n S scratch (RS and AG regions),
-    # writes S output + 2(n-1)/n S incoming scratch
-    hbm = (2 * S if algo == "rsag_zc" else 2 * S * (1 + 2 * (n - 1) / n) if algo == "rsag_pipeline"
-           else S * (1 + 3 * (n - 1) / n + 1 / n))
     progress("xGMI probe")
     try:
         probe = xgmi_probe(comm, n, dev, tmax, dist.barrier)
     except Exception as e:  # recorded, never fatal for the headline line
         probe = {"error": str(e)[-300:]}
-    peak = probe.get("allpairs_put_out_GBs")
-    kernel = {"rsag_zc": "allreduceZeroCopyKernel", "rsag_pipeline": "allreduceRsAgPipelineKernel"}.get(
-        algo, f"allreduceBulkKernel ({algo})")
+    roofline, xgmi = multi_roofline(n, S, algo, t, kern_ms, probe, ndev < world)
     res = {
         "metric": "device-resident AllReduce algbw GB/s fp16 at 1/2/4/8 MI355X; % xGMI roofline",
         "value": round(algbw, 2),
@@ -560,25 +669,8 @@ def bench_multi(args):
         # the bytes all ranks contributed per AllReduce (n buckets of S) over the step time, beside
         # the metric's algbw (S / t, one bucket per collective, nccl-tests' convention)
         "aggregate_input_GBs": round(n * S / t / 1e9, 2),
-        # the dominant kernel against the xGMI roofline: wire bytes per rank 2(n-1)S/n per launch over
-        # the kernel's average launch time, priced against the all-pairs put rate measured on this
-        # node in this run (one launch, workgroups partitioned by peer); the task-stated link rate
-        # (n-1) x 153.6 GB/s is kept beside it
-        "roofline": {"bound": "xgmi", "achieved": round(wire_ach, 1), "peak": peak, "unit": "GB/s",
-                     "frac": round(wire_ach / peak, 4) if peak else None, "traffic": None,
-                     "peak_source": "measured all-pairs put rate per rank (xgmi_probe)",
-                     "peak_assumed": round((n - 1) * XGMI_LINK_GBS, 1),
-                     "frac_of_assumed": round(wire_ach / ((n - 1) * XGMI_LINK_GBS), 4),
-                     "kernel": kernel, "kernel_us": round(kern_ms * 1e3, 2),
-                     "algorithmic_bytes_per_launch": int(wire),
-                     "hbm": {"achieved": round(hbm / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                             "frac": round(hbm / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                             "bytes_per_launch": int(hbm)},
-                     # traffic stays null: no counters run on the node.  The committed fabric-free PMC
-                     # run of the same kernel (8 in-process ranks) gives its bytes over its algorithmic ones
-                     "pmc_fabric_free": committed_multirank_pmc(kernel)},
-        "xgmi": {"allpairs_algbw_ceiling_assumed": round(ceiling, 1), "frac_of_assumed_ceiling": round(algbw / ceiling, 4),
-                 "link_GBs_assumed": XGMI_LINK_GBS, "wire_bytes_per_rank": int(wire), "measured": probe},
+        "roofline": roofline,
+        "xgmi": xgmi,
         "tune_ms": {f"{k[0]}:{k[1]}x{k[2]}": round(v * 1e3, 4) for k, v in tune.items()},
         "correct": ok,
         "correct_bitexact": bitexact,
@@ -591,15 +683,19 @@ def bench_multi(args):
                                                            {"message_size": S, "algorithm": FULL_NAMES[algo],
                                                             "nblocks": nb, "nthreads": nt,
                                                             "time_us": round(t * 1e6, 2)}]}}]}
-    mc = probe.get("allpairs_algbw_ceiling_measured")
-    if mc:
-        res["xgmi"]["frac_of_measured_ceiling"] = round(algbw / mc, 4)
-        res["xgmi"]["probe_consistent"] = algbw <= mc * 1.02  # an AllReduce cannot beat the raw puts it is made of
+    if cpu is not None:
+        hp = cpu["host_proxy"]
+        res["cpu_baseline"] = dict(cpu["sum"])
+        res["host_proxy_baseline"] = hp
     if not args.no_extras:
         res["extras"] = bench_extras(args, comm, n, dev, tmax, dist.barrier)
-        # every measured winner as a ready-to-commit tuned-config profile for this node and scale
-        res["tuned_config_table"] = node_tuned_table(n, torch.cuda.get_device_name(dev), res["extras"],
-                                                     (S, algo, nb, nt))
+        # every measured winner as a ready-to-commit tuned-config profile for this node and scale --
+        # only from a node where every rank has its own GPU; a rehearsal's table is tagged as such
+        table = node_tuned_table(n, torch.cuda.get_device_name(dev), res["extras"], (S, algo, nb, nt))
+        if ndev < world:
+            res["tuned_config_table_rehearsal"] = dict(table, rehearsal=True)
+        else:
+            res["tuned_config_table"] = table
     # last: on a rehearsal box (ranks sharing one device) the extra stream queues of a graph capture
     # slow every later launch of those ranks, so nothing is measured after it
     progress("graph-captured headline")
@@ -624,12 +720,60 @@ def bench_multi(args):
         del graph
     except Exception as e:  # recorded, never fatal for the headline line
         res["graph"] = {"error": str(e)[-300:]}
-    # cpu_baseline is an N=1 field (the oracle timed on rank 0 at N=1 only); at N>1 the reference's
-    # host-proxy path is reported by the mscclpp-test k1 row in extras
     comm.destroy()
     dist.barrier()
     dist.destroy_process_group()
     return res if rank == 0 else None
+
+
+def multi_roofline(n, S, algo, t, kern_ms, probe, rehearsal):
+    """The N>1 line's `roofline` and `xgmi` objects.  The dominant kernel's wire bytes per rank
+    (2(n-1)/n * S per AllReduce, in + out) over its average launch time, priced against the rate the
+    node's probe measured for the SAME remote-access pattern: zero-copy reduce-scatters by remote
+    reads of every peer's input and all-gathers by remote writes (allreduce_rsag_zero_copy.cu:88-92),
+    so its peak is all-pairs gets + puts in one launch; the scratch-based kernels only put.  An
+    AllReduce cannot move its bytes faster than the raw accesses it is made of, so frac > 1 (a probe
+    that under-drove the links) sets probe_consistent false, with no slack."""
+    algbw = S / t / 1e9
+    ceiling = n * XGMI_LINK_GBS / 2  # all-pairs algbw ceiling at the assumed link rate (BASELINE.md §2)
+    wire = 2 * (n - 1) * S / n
+    wire_ach = wire / (kern_ms * 1e-3) / 1e9
+    # HBM bytes one rank's AllReduce moves.  fullmesh/rsag: reads S input + (n-1)/n S scratch;
+    # writes S/n own output + (n-1)/n S incoming scratch + (n-1)/n S incoming output.  rsag_zc: reads
+    # S of input (own slice locally, the rest by the peers), writes S of output (own slice locally,
+    # the rest by the peers).  rsag_pipeline: reads S input + 2(n-1)/n S scratch (RS and AG regions),
+    # writes S output + 2(n-1)/n S incoming scratch
+    hbm = (2 * S if algo == "rsag_zc" else 2 * S * (1 + 2 * (n - 1) / n) if algo == "rsag_pipeline"
+           else S * (1 + 3 * (n - 1) / n + 1 / n))
+    pattern = "allpairs_getput_GBs" if algo == "rsag_zc" else "allpairs_put_out_GBs"
+    peak = probe.get(pattern)
+    kernel = {"rsag_zc": "allreduceZeroCopyKernel", "rsag_pipeline": "allreduceRsAgPipelineKernel"}.get(
+        algo, f"allreduceBulkKernel ({algo})")
+    roofline = {"bound": "xgmi", "achieved": round(wire_ach, 1), "peak": peak, "unit": "GB/s",
+                "frac": round(wire_ach / peak, 4) if peak else None, "traffic": None,
+                "peak_source": f"xgmi_probe.{pattern}: the measured rate of the winning kernel's remote-access "
+                               "pattern per rank (bytes in + out over time), one launch on this node",
+                "rehearsal": bool(rehearsal),
+                "peak_assumed": round((n - 1) * XGMI_LINK_GBS, 1),
+                "frac_of_assumed": round(wire_ach / ((n - 1) * XGMI_LINK_GBS), 4),
+                "kernel": kernel, "kernel_us": round(kern_ms * 1e3, 2),
+                "algorithmic_bytes_per_launch": int(wire),
+                "hbm": {"achieved": round(hbm / (kern_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "frac": round(hbm / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "bytes_per_launch": int(hbm)},
+                # traffic stays null: no counters run on the node.  The committed fabric-free PMC
+                # run of the same kernel (8 in-process ranks) gives its bytes over its algorithmic ones
+                "pmc_fabric_free": committed_multirank_pmc(kernel)}
+    xgmi = {"allpairs_algbw_ceiling_assumed": round(ceiling, 1), "frac_of_assumed_ceiling": round(algbw / ceiling, 4),
+            "link_GBs_assumed": XGMI_LINK_GBS, "wire_bytes_per_rank": int(wire), "measured": probe}
+    if peak:
+        mc = peak * n / (2 * (n - 1))  # algbw ceiling: 2(n-1)/n * S wire bytes per AllReduce at that rate
+        xgmi["allpairs_algbw_ceiling_measured"] = round(mc, 1)
+        xgmi["frac_of_measured_ceiling"] = round(algbw / mc, 4)
+        xgmi["probe_consistent"] = bool(wire_ach <= peak and algbw <= mc)
+    else:
+        xgmi["probe_consistent"] = False
+    return roofline, xgmi
 
 
 def phase_breakdown(m, comm, n, dev, tmax, algo, nb, nt, x, out):
@@ -714,6 +858,12 @@ def xgmi_probe(comm, n, dev, tmax, barrier, S=64 << 20):
     get = [(psrc[q] + ((q - rank - 1) % n) * chunk, base_d + i * chunk, chunk) for i, q in enumerate(peers)]
     t_ap = timed(jobs(put, bpj))
     t_ag = timed(jobs(get, bpj))
+    # the zero-copy pattern: gets from every peer and puts into every peer in ONE launch, the gets
+    # landing in a buffer of their own (bytes in + bytes out per rank over the time)
+    gdst = torch.empty(S, dtype=torch.uint8, device=dev)
+    getput = [(psrc[q] + ((q - rank - 1) % n) * chunk, gdst.data_ptr() + i * chunk, chunk) for i, q in enumerate(peers)]
+    t_gp = timed(jobs(put + getput, max(16, bpj // 2)))
+    del gdst
     # what the cache policy of the remote accesses costs over the links (the collectives use sc0 sc1
     # everywhere): all-pairs puts by store policy, all-pairs gets by load policy
     pol = {"sys": 0, "plain": 1, "nt": 2, "agent": 3}
@@ -724,9 +874,11 @@ def xgmi_probe(comm, n, dev, tmax, barrier, S=64 << 20):
            "ring_get_GBs": round(S / t_get / 1e9, 1),
            "allpairs_put_out_GBs": round((n - 1) * chunk / t_ap / 1e9, 1),
            "allpairs_get_in_GBs": round((n - 1) * chunk / t_ag / 1e9, 1),
+           "allpairs_getput_GBs": round(2 * (n - 1) * chunk / t_gp / 1e9, 1),
            "allpairs_put_out_GBs_by_store_policy": by_store, "allpairs_get_in_GBs_by_load_policy": by_load}
-    # all-pairs AllReduce moves 2(n-1)/n * S out of every rank: its algbw ceiling at the measured rate
-    out["allpairs_algbw_ceiling_measured"] = round(out["allpairs_put_out_GBs"] * n / (2 * (n - 1)), 1)
+    # all-pairs AllReduce moves 2(n-1)/n * S per rank: its algbw ceilings at the measured rates
+    out["allpairs_algbw_ceiling_put"] = round(out["allpairs_put_out_GBs"] * n / (2 * (n - 1)), 1)
+    out["allpairs_algbw_ceiling_getput"] = round(out["allpairs_getput_GBs"] * n / (2 * (n - 1)), 1)
     del pdst, psrc
     return out
 

@@ -7,6 +7,7 @@ the reference's operator surface for this path (``ncclAllReduce`` / ``Algorithm:
 the same argument meaning and error behaviour).  PyTorch is used only for device memory and
 streams.  There is no fallback: if the library is missing, importing a GPU entry point raises.
 """
+import collections
 import ctypes
 import os
 
@@ -174,19 +175,27 @@ def stream_ptr(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+# (op, ptr, nbytes, uncached) of the last DeviceBuffer allocations and frees of this process: what a
+# test diagnostic compares a misbehaving buffer's address range with
+ALLOC_HISTORY = collections.deque(maxlen=4096)
+
+
 class DeviceBuffer:
     """Raw device allocation owned by the library (uncached = hipDeviceMallocUncached)."""
 
     def __init__(self, nbytes, uncached=True):
         self.nbytes = nbytes
+        self.uncached = uncached
         p = ctypes.c_void_p()
         fn = lib().mscclppAmdMallocUncached if uncached else lib().mscclppAmdMalloc
         check(fn(ctypes.byref(p), nbytes), "device alloc")
         self.ptr = p.value
+        ALLOC_HISTORY.append(("alloc", self.ptr, nbytes, uncached))
 
     def free(self):
         if self.ptr:
             lib().mscclppAmdFree(ctypes.c_void_p(self.ptr))
+            ALLOC_HISTORY.append(("free", self.ptr, self.nbytes, self.uncached))
             self.ptr = None
 
     def __del__(self):

@@ -119,11 +119,24 @@ def build_tests():
     return outs
 
 
+DIAG_LIB = os.path.join(TESTBIN, "libxcdprobe.so")
+
+
+def build_diag():
+    """Test diagnostics with device code (tests/diag/xcd_probe.hip: per-XCD readback) -> tests/bin/."""
+    os.makedirs(TESTBIN, exist_ok=True)
+    src = os.path.join(ROOT, "tests", "diag", "xcd_probe.hip")
+    if _newer(DIAG_LIB, [src]):
+        _run([HIPCC, "--offload-arch=" + ARCH, "-O2", "-std=c++17", "-shared", "-fPIC", src, "-o", DIAG_LIB])
+    return DIAG_LIB
+
+
 def build_all(verbose=False):
     build_oracle()
     build_library(verbose=verbose)
     build_audit()
     build_tests()
+    build_diag()
     ref = os.path.join(ROOT, "oracle", "build_ref.sh")
     if os.path.isdir("/root/reference") and os.path.exists(ref):
         # the reference-header harness (oracle/_ref) can only be built where /root/reference exists

@@ -1,6 +1,7 @@
 #include "bootstrap.hpp"
 
 #include <arpa/inet.h>
+#include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <poll.h>
@@ -73,11 +74,29 @@ constexpr uint32_t kMsgAllGather = 1, kMsgP2P = 2;
 
 // Root: accept nranks ranks, then serve messages until a rank disconnects: all-gather rounds
 // complete when every rank has contributed (in order), point-to-point messages are forwarded at once.
+// The relay never blocks on one rank: sockets are non-blocking, every rank has an inbound buffer
+// (messages are parsed once complete) and an outbound queue written as poll reports POLLOUT, so a
+// rank that is itself busy sending a large message to the root cannot stall the others.
+struct RelayConn {
+  int fd = -1;
+  std::vector<char> in;  // bytes received, not yet parsed
+  std::deque<std::vector<char>> out;
+  size_t outOff = 0;  // bytes of out.front() already sent
+};
+
+void enqueue(RelayConn& c, const MsgHeader& h, const char* body) {
+  std::vector<char> m(sizeof(h) + h.len);
+  std::memcpy(m.data(), &h, sizeof(h));
+  if (h.len) std::memcpy(m.data() + sizeof(h), body, h.len);
+  c.out.push_back(std::move(m));
+}
+
 void rootLoop(int lfd, uint64_t nonce) {
-  std::vector<int> fds;
+  std::vector<RelayConn> cs;
   int nranks = -1;
   try {
     int have = 0;
+    std::vector<int> fds;
     while (nranks < 0 || have < nranks) {
       pollfd pf{lfd, POLLIN, 0};
       int r = ::poll(&pf, 1, 600 * 1000);
@@ -109,51 +128,81 @@ void rootLoop(int lfd, uint64_t nonce) {
     }
     ::close(lfd);
     lfd = -1;
-    for (int fd : fds) setTimeouts(fd, 0);  // relay phase: ranks may stay idle indefinitely
+    cs.resize(nranks);
+    for (int r = 0; r < nranks; ++r) {
+      cs[r].fd = fds[r];
+      setTimeouts(fds[r], 0);  // relay phase: ranks may stay idle indefinitely
+      ::fcntl(fds[r], F_SETFL, ::fcntl(fds[r], F_GETFL, 0) | O_NONBLOCK);
+    }
     std::vector<std::deque<std::vector<char>>> pending(nranks);  // all-gather contributions per rank
     std::vector<pollfd> pfs(nranks);
+    std::vector<char> chunk(1 << 16);
     for (;;) {
-      for (int r = 0; r < nranks; ++r) pfs[r] = pollfd{fds[r], POLLIN, 0};
+      for (int r = 0; r < nranks; ++r)
+        pfs[r] = pollfd{cs[r].fd, (short)(POLLIN | (cs[r].out.empty() ? 0 : POLLOUT)), 0};
       if (::poll(pfs.data(), pfs.size(), -1) < 0) {
         if (errno == EINTR) continue;
         throw std::runtime_error("bootstrap root: poll failed");
       }
       for (int r = 0; r < nranks; ++r) {
-        if (!(pfs[r].revents & (POLLIN | POLLHUP | POLLERR))) continue;
-        MsgHeader h{};
-        recvAll(fds[r], &h, sizeof(h));  // throws when the rank has gone: the root ends
-        std::vector<char> body(h.len);
-        if (h.len) recvAll(fds[r], body.data(), h.len);
-        if (h.kind == kMsgP2P) {
-          if (h.peer < 0 || h.peer >= nranks) throw std::runtime_error("bootstrap root: bad destination");
-          MsgHeader out{kMsgP2P, r, h.tag, h.len};
-          sendAll(fds[h.peer], &out, sizeof(out));
-          if (h.len) sendAll(fds[h.peer], body.data(), h.len);
-        } else {
-          pending[r].push_back(std::move(body));
+        RelayConn& c = cs[r];
+        if (pfs[r].revents & POLLOUT) {
+          while (!c.out.empty()) {
+            const std::vector<char>& m = c.out.front();
+            ssize_t k = ::send(c.fd, m.data() + c.outOff, m.size() - c.outOff, MSG_NOSIGNAL);
+            if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR)) break;
+            if (k <= 0) throw std::runtime_error("bootstrap root: send failed");
+            c.outOff += (size_t)k;
+            if (c.outOff == m.size()) {
+              c.out.pop_front();
+              c.outOff = 0;
+            }
+          }
         }
+        if (!(pfs[r].revents & (POLLIN | POLLHUP | POLLERR))) continue;
+        for (;;) {
+          ssize_t k = ::recv(c.fd, chunk.data(), chunk.size(), 0);
+          if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+          if (k < 0 && errno == EINTR) continue;
+          if (k <= 0) throw std::runtime_error("bootstrap root: a rank has gone");  // the root ends
+          c.in.insert(c.in.end(), chunk.data(), chunk.data() + k);
+        }
+        size_t off = 0;
+        while (c.in.size() - off >= sizeof(MsgHeader)) {
+          MsgHeader h{};
+          std::memcpy(&h, c.in.data() + off, sizeof(h));
+          if (c.in.size() - off - sizeof(h) < h.len) break;  // body not complete yet
+          const char* body = c.in.data() + off + sizeof(h);
+          if (h.kind == kMsgP2P) {
+            if (h.peer < 0 || h.peer >= nranks) throw std::runtime_error("bootstrap root: bad destination");
+            enqueue(cs[h.peer], MsgHeader{kMsgP2P, r, h.tag, h.len}, body);
+          } else {
+            pending[r].emplace_back(body, body + h.len);
+          }
+          off += sizeof(h) + h.len;
+        }
+        c.in.erase(c.in.begin(), c.in.begin() + (std::ptrdiff_t)off);
       }
-      bool ready = true;
-      for (int r = 0; r < nranks; ++r) ready = ready && !pending[r].empty();
-      if (!ready) continue;
-      const uint64_t len = pending[0].front().size();
-      std::vector<char> all(len * nranks);
-      for (int r = 0; r < nranks; ++r) {
-        if (pending[r].front().size() != len) throw std::runtime_error("bootstrap root: mismatched round sizes");
-        if (len) std::memcpy(all.data() + r * len, pending[r].front().data(), len);
-        pending[r].pop_front();
-      }
-      MsgHeader out{kMsgAllGather, -1, 0, (uint64_t)all.size()};
-      for (int r = 0; r < nranks; ++r) {
-        sendAll(fds[r], &out, sizeof(out));
-        if (!all.empty()) sendAll(fds[r], all.data(), all.size());
+      for (;;) {  // every complete all-gather round, in order
+        bool ready = true;
+        for (int r = 0; r < nranks; ++r) ready = ready && !pending[r].empty();
+        if (!ready) break;
+        const uint64_t len = pending[0].front().size();
+        std::vector<char> all(len * nranks);
+        for (int r = 0; r < nranks; ++r) {
+          if (pending[r].front().size() != len) throw std::runtime_error("bootstrap root: mismatched round sizes");
+          if (len) std::memcpy(all.data() + r * len, pending[r].front().data(), len);
+          pending[r].pop_front();
+        }
+        const MsgHeader out{kMsgAllGather, -1, 0, (uint64_t)all.size()};
+        for (int r = 0; r < nranks; ++r) enqueue(cs[r], out, all.data());
       }
     }
   } catch (...) {
   }
   if (lfd >= 0) ::close(lfd);
-  for (int fd : fds)
-    if (fd >= 0) ::close(fd);
+  for (auto& c : cs)
+    if (c.fd >= 0) ::close(c.fd);
 }
 
 }  // namespace
@@ -212,32 +261,65 @@ TcpBootstrap::~TcpBootstrap() {
   if (fd_ >= 0) ::close(fd_);
 }
 
-bool TcpBootstrap::readOne(void* agOut, size_t agBytes) {
+void TcpBootstrap::readOne() {
   MsgHeader h{};
   recvAll(fd_, &h, sizeof(h));
-  if (h.kind == kMsgAllGather) {
-    if (h.len != agBytes) throw std::runtime_error("bootstrap: unexpected all-gather result");
-    if (agBytes) recvAll(fd_, agOut, agBytes);
-    return true;
-  }
   std::vector<char> body(h.len);
   if (h.len) recvAll(fd_, body.data(), h.len);
-  mailbox_[{h.peer, (int)h.tag}].push_back(std::move(body));
-  return false;
+  std::lock_guard<std::mutex> lk(mu_);
+  if (h.kind == kMsgAllGather)
+    agResults_.push_back(std::move(body));
+  else
+    mailbox_[{h.peer, (int)h.tag}].push_back(std::move(body));
+}
+
+template <typename Ready>
+void TcpBootstrap::waitFor(Ready ready) {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    if (ready()) return;
+    if (!reading_) {
+      reading_ = true;
+      lk.unlock();
+      try {
+        readOne();
+      } catch (...) {
+        lk.lock();
+        reading_ = false;
+        cv_.notify_all();
+        throw;
+      }
+      lk.lock();
+      reading_ = false;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk);
+    }
+  }
 }
 
 void TcpBootstrap::allGather(const void* send, void* recv, size_t bytes) {
-  std::lock_guard<std::mutex> lk(mu_);
-  MsgHeader h{kMsgAllGather, -1, 0, (uint64_t)bytes};
-  sendAll(fd_, &h, sizeof(h));
-  if (bytes) sendAll(fd_, send, bytes);
-  while (!readOne(recv, bytes * nranks_)) {
+  std::lock_guard<std::mutex> round(agMu_);
+  {
+    std::lock_guard<std::mutex> lk(sendMu_);
+    MsgHeader h{kMsgAllGather, -1, 0, (uint64_t)bytes};
+    sendAll(fd_, &h, sizeof(h));
+    if (bytes) sendAll(fd_, send, bytes);
   }
+  std::vector<char> all;
+  waitFor([&] {
+    if (agResults_.empty()) return false;
+    all = std::move(agResults_.front());
+    agResults_.pop_front();
+    return true;
+  });
+  if (all.size() != bytes * (size_t)nranks_) throw std::runtime_error("bootstrap: unexpected all-gather result");
+  if (!all.empty()) std::memcpy(recv, all.data(), all.size());
 }
 
 void TcpBootstrap::send(const void* data, size_t bytes, int peer, int tag) {
   if (peer < 0 || peer >= nranks_) throw std::invalid_argument("bootstrap send: bad peer");
-  std::lock_guard<std::mutex> lk(mu_);
+  std::lock_guard<std::mutex> lk(sendMu_);
   MsgHeader h{kMsgP2P, peer, tag, (uint64_t)bytes};
   sendAll(fd_, &h, sizeof(h));
   if (bytes) sendAll(fd_, data, bytes);
@@ -245,22 +327,20 @@ void TcpBootstrap::send(const void* data, size_t bytes, int peer, int tag) {
 
 void TcpBootstrap::recv(void* data, size_t bytes, int peer, int tag) {
   if (peer < 0 || peer >= nranks_) throw std::invalid_argument("bootstrap recv: bad peer");
-  std::lock_guard<std::mutex> lk(mu_);
   const auto key = std::make_pair(peer, tag);
-  for (;;) {
+  std::vector<char> m;
+  waitFor([&] {  // under mu_: take the message in the same critical section that found it
     auto it = mailbox_.find(key);
-    if (it != mailbox_.end() && !it->second.empty()) {
-      std::vector<char> m = std::move(it->second.front());
-      it->second.pop_front();
-      if (m.size() != bytes)
-        throw std::runtime_error("bootstrap recv: message from rank " + std::to_string(peer) + " tag " +
-                                 std::to_string(tag) + " has " + std::to_string(m.size()) + " bytes, expected " +
-                                 std::to_string(bytes));
-      if (bytes) std::memcpy(data, m.data(), bytes);
-      return;
-    }
-    if (readOne(nullptr, 0)) throw std::runtime_error("bootstrap recv: all-gather result while receiving");
-  }
+    if (it == mailbox_.end() || it->second.empty()) return false;
+    m = std::move(it->second.front());
+    it->second.pop_front();
+    return true;
+  });
+  if (m.size() != bytes)
+    throw std::runtime_error("bootstrap recv: message from rank " + std::to_string(peer) + " tag " +
+                             std::to_string(tag) + " has " + std::to_string(m.size()) + " bytes, expected " +
+                             std::to_string(bytes));
+  if (bytes) std::memcpy(data, m.data(), bytes);
 }
 
 void TcpBootstrap::barrier() {

@@ -9,6 +9,7 @@
 // received.
 #pragma once
 
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
 #include <deque>
@@ -52,14 +53,23 @@ class TcpBootstrap {
   void recv(void* data, size_t bytes, int peer, int tag);
 
  private:
-  // Read one message from the root; point-to-point deliveries go to the mailbox.  Returns true
-  // for an all-gather result (copied to agOut).
-  bool readOne(void* agOut, size_t agBytes);
+  // Read one message from the root (the caller holds the reader role, not mu_): point-to-point
+  // deliveries go to the mailbox, all-gather results to agResults_.
+  void readOne();
+  // Wait until `ready()` (called under mu_) holds, taking the reader role while nobody else has it,
+  // so a thread blocked in a socket read never holds mu_ and other threads' sends proceed.
+  template <typename Ready>
+  void waitFor(Ready ready);
   int rank_;
   int nranks_;
   int fd_;
-  std::mutex mu_;
+  std::mutex sendMu_;  // one writer of the socket at a time
+  std::mutex agMu_;    // one all-gather round at a time (results arrive in round order)
+  std::mutex mu_;      // mailbox_, agResults_, reading_
+  std::condition_variable cv_;
+  bool reading_ = false;
   std::map<std::pair<int, int>, std::deque<std::vector<char>>> mailbox_;
+  std::deque<std::vector<char>> agResults_;
 };
 
 }  // namespace mscclpp_amd

@@ -112,10 +112,12 @@ inline uint64_t spinBudgetTicks() {
   return t;
 }
 
-// MSCCLPP_AMD_BULK_SCRATCH_MB (default 1024): the bulk scratch allocated at communicator init.
+// MSCCLPP_AMD_BULK_SCRATCH_MB (default 128, the reference's scratch, nccl.cc:180): the bulk scratch
+// allocated once at communicator init and never re-allocated; a bucket whose n regions do not fit
+// runs in several passes (bulkScratchRequired).
 inline size_t bulkScratchInitBytes() {
   const char* e = std::getenv("MSCCLPP_AMD_BULK_SCRATCH_MB");
-  size_t mb = e ? std::strtoull(e, nullptr, 10) : 1024;
+  size_t mb = e ? std::strtoull(e, nullptr, 10) : 128;
   if (mb < 64) mb = 64;
   return mb << 20;
 }
@@ -352,6 +354,12 @@ struct ncclComm {
   //    leave every later replay writing through closed mappings.  Pinned entries are never evicted
   //    (the cap then only bounds the unpinned ones); capture happens in the same calls on every
   //    rank, so every rank pins the same.
+  //  * A registration made for the caller (Communicator::registerMemory, mscclppAmdCommRegisterBuffer)
+  //    is pinned too: the caller keeps the raw peer pointers (an algorithm plugin's context holds
+  //    them for good), so no later eviction may close them.
+  //  * Pinned entries are released only by dropUserRegistrations (mscclppAmdCommDeregisterAll), which
+  //    must not run while a graph that captured them is still replayed, or when the address is
+  //    re-used by a new allocation (the old one was freed, so its pointers were dead already).
   static constexpr size_t kMaxUserRegs = 64;
   struct UserReg {
     uint64_t bufferId = 0;
@@ -367,12 +375,15 @@ struct ncclComm {
   uint64_t allocExchanges = 0, offsetExchanges = 0;
 
   void retireReg(std::map<std::pair<uint64_t, uint64_t>, UserReg>::iterator it) {
+    if (it->second.pinned)
+      info("rank " + std::to_string(rank) + ": pinned registration of allocation " +
+           std::to_string(it->first.first) + " retired (its address now belongs to a new allocation)");
     for (auto& m : it->second.bases.maps)
       if (m) retired.push_back(std::move(m));
     userRegs.erase(it);
   }
 
-  std::array<void*, MSCCLPP_AMD_MAX_RANKS> registerOutput(void* out, hipStream_t stream = nullptr) {
+  std::array<void*, MSCCLPP_AMD_MAX_RANKS> registerOutput(void* out, hipStream_t stream = nullptr, bool pin = false) {
     void* base = nullptr;
     size_t sz = 0;
     HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)out));
@@ -400,6 +411,7 @@ struct ncclComm {
     }
     UserReg& reg = it->second;
     reg.lastUse = ++useClock;
+    if (pin) reg.pinned = true;
     if (stream) {
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive) reg.pinned = true;
@@ -444,11 +456,20 @@ struct ncclComm {
     mscclppAmdRankView v = baseView(rank == root ? send : recv, recv);
     if (rank != root) {
       // the mapping stays referenced until a later broadcast from the same root replaces it (and
-      // is then retired: the kernel below may still be queued)
+      // is then retired: the kernel below may still be queued).  A mapping used under stream
+      // capture is kept until dropUserRegistrations instead: the graph's replays read through it.
       auto m = openIpcHandle(all[root].handle);
       auto& slot = bcastMaps[(size_t)root];
-      if (slot && slot != m) retired.push_back(std::move(slot));
+      bool& captured = bcastCaptured[(size_t)root];  // sticky while the same mapping stays in the slot
+      if (slot && slot != m) {
+        if (captured) bcastPinned.push_back(std::move(slot));
+        else retired.push_back(std::move(slot));
+        captured = false;
+      }
       slot = m;
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (stream && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive)
+        captured = true;
       v.peerInput[root] = (char*)m.get() + all[root].offset;
     }
     const int rc = launchBroadcast(&v, 1, nranks, bytes, root, nblocks, nthreads, spinBudgetTicks(), stream);
@@ -456,6 +477,8 @@ struct ncclComm {
     return rc;
   }
   std::array<std::shared_ptr<void>, MSCCLPP_AMD_MAX_RANKS> bcastMaps;
+  std::array<bool, MSCCLPP_AMD_MAX_RANKS> bcastCaptured{};  // bcastMaps[root] used under capture
+  std::vector<std::shared_ptr<void>> bcastPinned;             // replaced, but a graph may read them
 
   // Drop every cached mapping of peers' user buffers (collective).  Scratch, token and flag
   // mappings stay.  After this, the next use of any buffer registers it afresh.
@@ -464,6 +487,8 @@ struct ncclComm {
     boot->barrier();  // no rank still runs a kernel that uses a mapping being closed
     while (!userRegs.empty()) retireReg(userRegs.begin());
     for (auto& m : bcastMaps) m.reset();
+    bcastCaptured = {};
+    bcastPinned.clear();
     retired.clear();
     boot->barrier();
   }
@@ -519,9 +544,9 @@ struct ncclComm {
       return launchAllReduceLL(algo, &v, 1, nranks, bytes, dtype, op, nblocks, nthreads, spinBudgetTicks(), stream);
     }
     if (algo == MSCCLPP_AMD_ALGO_FULLMESH || algo == MSCCLPP_AMD_ALGO_RSAG) {
-      // a bucket up to 1 GiB fits in one pass with the default 1 GiB bulk scratch
+      // the scratch allocated at init bounds a pass; larger buckets take several passes
       size_t need = bytes + 16 * (size_t)nranks * 64;
-      const size_t cap = (size_t)1 << 30;
+      const size_t cap = bulkBytes;
       if (need > cap) need = cap;
       ensure(bulkScratch, bulkBytes, peerBulk, need);
       v.scratch = bulkScratch;
@@ -542,9 +567,8 @@ struct ncclComm {
     }
     if (algo == MSCCLPP_AMD_ALGO_RSAG_PIPELINE) {
       // every remote store lands in the bulk scratch: no user-buffer registration at all
-      const size_t stageCap = (size_t)1 << 30;
       size_t need = 2 * bytes + 16 * (size_t)nranks * 64;
-      if (need > stageCap) need = stageCap;
+      if (need > bulkBytes) need = bulkBytes;  // fewer stages, never a re-allocation
       ensure(bulkScratch, bulkBytes, peerBulk, need);
       v.scratch = bulkScratch;
       v.scratchBytes = bulkBytes;
@@ -582,7 +606,7 @@ struct ncclComm {
     const size_t total = blockBytes * nranks;
     mscclppAmdRankView v = baseView(in, out);
     size_t need = total + 16 * (size_t)nranks * 64;
-    const size_t cap = (size_t)1 << 30;
+    const size_t cap = bulkBytes;
     if (need > cap) need = cap;
     ensure(bulkScratch, bulkBytes, peerBulk, need);
     v.scratch = bulkScratch;
@@ -611,6 +635,7 @@ struct ncclComm {
     }
     userRegs.clear();
     for (auto& m : bcastMaps) m.reset();
+    bcastPinned.clear();
     peerLL = peerBulk = peerTok = PeerBufs();
     retired.clear();
     if (llScratch) (void)hipFree(llScratch);

@@ -429,7 +429,8 @@ std::vector<void*> Communicator::registerMemory(void* ptr) {
     return res;
   }
   std::lock_guard<std::mutex> lk(comm_->mu);
-  auto peers = comm_->registerOutput(ptr);  // collective IPC exchange, cached per allocation
+  // collective IPC exchange, cached per allocation; pinned: the caller keeps these pointers
+  auto peers = comm_->registerOutput(ptr, nullptr, /*pin=*/true);
   for (int r = 0; r < comm_->nranks; ++r) res[(size_t)r] = peers[(size_t)r];
   return res;
 }

@@ -24,4 +24,5 @@ def built():
     _build.build_library()
     _build.build_audit()
     _build.build_tests()
+    _build.build_diag()
     return True

@@ -33,6 +33,36 @@ static void rankMain(int rank, int n, BootstrapId id, int rounds, int* bad) {
       b.send(&out, sizeof(out), next, it);
       b.recv(&in, sizeof(in), prev, it);
       if (in != prev * 100 + it) ++*bad;
+      if (it % 5 == 0) {
+        // every rank sends 1 MiB to every peer before receiving any: the relay must keep reading
+        // from a rank it cannot yet write to (a blocking relay stalls once the socket buffers fill)
+        std::vector<std::vector<int>> big(n, std::vector<int>(1 << 18));
+        for (int q = 0; q < n; ++q) {
+          if (q == rank) continue;
+          for (size_t k = 0; k < big[q].size(); ++k) big[q][k] = rank * 7 + q * 13 + (int)k + it;
+          b.send(big[q].data(), big[q].size() * sizeof(int), q, 100000 + it);
+        }
+        std::vector<int> got(1 << 18);
+        for (int q = 0; q < n; ++q) {
+          if (q == rank) continue;
+          b.recv(got.data(), got.size() * sizeof(int), q, 100000 + it);
+          for (size_t k = 0; k < got.size(); k += 4099)
+            if (got[k] != q * 7 + rank * 13 + (int)k + it) ++*bad;
+        }
+        // a second thread waits in recv for a message its peer sends only after an all-gather that
+        // needs this rank's main thread: the waiting recv must not hold up this rank's all-gather
+        int late = -1;
+        std::thread waiter([&] { b.recv(&late, sizeof(late), prev, 200000 + it); });
+        std::vector<int> one(1), every(n);
+        one[0] = rank;
+        b.allGather(one.data(), every.data(), sizeof(int));
+        for (int r = 0; r < n; ++r)
+          if (every[r] != r) ++*bad;
+        const int v = 9000 + rank;
+        b.send(&v, sizeof(v), next, 200000 + it);
+        waiter.join();
+        if (late != 9000 + prev) ++*bad;
+      }
     }
     b.barrier();
   } catch (const std::exception& e) {

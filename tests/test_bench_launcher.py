@@ -118,3 +118,53 @@ def test_checker_expectations_per_algorithm(built, n):
         seq = O.reduce_seq(m.F16, O.SUM, [words[(o + k) % n] for k in range(n)])
         exp[owner == o] = seq[owner == o]
     assert np.array_equal(chk.expected("rsag_pipeline", nb, nt, 1, S, 0), exp)
+
+
+def _probe(put, getput):
+    return {"allpairs_put_out_GBs": put, "allpairs_getput_GBs": getput}
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_multi_line_roofline_prices_the_kernels_pattern(n):
+    """the N>1 line's roofline carries bound / achieved / peak / frac, zero-copy
+    is priced against gets + puts driven together, the scratch kernels against puts, and a frac
+    above 1 (a probe that under-drove the links) is flagged, with no slack."""
+    import bench
+
+    S, kern_ms = 48 << 20, 0.2
+    wire_gbs = 2 * (n - 1) * S / n / (kern_ms * 1e-3) / 1e9
+    for algo, key in (("rsag_zc", "allpairs_getput_GBs"), ("fullmesh", "allpairs_put_out_GBs")):
+        probe = _probe(2 * wire_gbs, 3 * wire_gbs)
+        roof, xg = bench.multi_roofline(n, S, algo, kern_ms * 1.05e-3, kern_ms, probe, False)
+        for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+            assert k in roof
+        assert roof["peak"] == probe[key] and roof["frac"] == pytest.approx(wire_gbs / probe[key], rel=1e-3)
+        assert roof["frac"] <= 1 and xg["probe_consistent"] is True
+        # the same kernel time against a probe slower than the kernel itself: inconsistent
+        roof, xg = bench.multi_roofline(n, S, algo, kern_ms * 1.05e-3, kern_ms, _probe(0.99 * wire_gbs, 0.99 * wire_gbs),
+                                        False)
+        assert roof["frac"] > 1 and xg["probe_consistent"] is False
+    _, xg = bench.multi_roofline(n, S, "fullmesh", 1e-4, 0.1, {"error": "no probe"}, True)
+    assert xg["probe_consistent"] is False
+
+
+def test_cpu_baselines_state_their_cores():
+    """cpu_baseline objects (N=1 and N>1): value / unit / cores / kind / sample, cores = threads used."""
+    import bench
+
+    for d in (bench.cpu_baseline_sum(4, 1 << 20, 0.05, threads=3), bench.cpu_baseline_self_reduce(1 << 20, 0.05, 2)):
+        assert set(d) >= {"value", "unit", "cores", "kind", "sample"} and d["value"] > 0
+    assert bench.cpu_baseline_sum(8, 1 << 20, 0.05, threads=3)["cores"] == 3
+    assert "8-way sum" in bench.cpu_baseline_sum(8, 1 << 20, 0.05, threads=2)["sample"]
+
+
+def test_cpu_threaded_sum_matches_the_oracle():
+    """The threaded sum computes exactly what the oracle's one-call form does."""
+    import bench
+    import oracle_lib as O
+
+    nbytes, n = 1 << 20, 3
+    ins = [O.lcg(O.F16, nbytes // 2, r, 0).view(np.uint32) for r in range(n)]
+    want = O.reduce_seq(O.F16, O.SUM, ins)
+    got = bench._threaded_sum_for_test(n, nbytes, threads=5)
+    assert np.array_equal(got, want)

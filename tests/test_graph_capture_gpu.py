@@ -7,6 +7,7 @@ semaphore counters live in device memory and advance inside the kernels, so noth
 stale between replays.  Buffers are registered by one eager call before the capture (a new buffer
 costs a host exchange, which has no place inside a capture)."""
 import multiprocessing as mp
+import ctypes
 import queue
 import traceback
 
@@ -163,6 +164,9 @@ def _churn_worker(rank, n, uid, q):
         torch.cuda.set_device(0)
         comm = m.Communicator(rank, n, uid)
         count = 6 << 20  # 12 MiB: above the caching allocator's 10 MiB packing, so its own segment
+        # a buffer registered for the caller (an algorithm plugin keeps these raw peer pointers)
+        z = torch.zeros(count, dtype=torch.int16, device="cuda")
+        pz = comm.register_buffer(z)
         x = torch.zeros(count, dtype=torch.float16, device="cuda")
         y = torch.zeros_like(x)
         comm.all_reduce(x, y, algo="rsag_zc")
@@ -174,6 +178,19 @@ def _churn_worker(rank, n, uid, q):
             comm.all_reduce(x, y, algo="rsag_zc")  # pins x's and y's registrations
         torch.cuda.synchronize()
         pinned = comm.registration_stats()[0]
+        # a captured broadcast from root 0, then an eager one from another root buffer: the eager
+        # call replaces the root's mapping, which the graph still reads through on replay
+        bsrc = torch.zeros(count, dtype=torch.int32, device="cuda")
+        bsrc2 = torch.zeros_like(bsrc)
+        brecv = torch.zeros_like(bsrc)
+        comm.broadcast(bsrc, brecv, root=0)
+        torch.cuda.synchronize()
+        gb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gb, stream=side):
+            comm.broadcast(bsrc, brecv, root=0, stream=side)
+        torch.cuda.synchronize()
+        comm.broadcast(bsrc2, brecv, root=0)
+        torch.cuda.synchronize()
         # more fresh allocations than the registration cache holds (64), each its own segment
         keep = []
         for i in range(70):
@@ -195,7 +212,29 @@ def _churn_worker(rank, n, uid, q):
             e = _expected(O, "rsag_zc", 0, count, ins, rank, n)
             res["bad"] = int(np.count_nonzero(y.cpu().contiguous().view(torch.uint8).numpy() != e))
             res["err"] = comm.device_error()
-        del g, keep
+        # the captured broadcast replays through the root's old mapping, on new data
+        if rank == 0:
+            bsrc.copy_(torch.arange(count, dtype=torch.int32, device="cuda"))
+        brecv.fill_(-1)
+        torch.cuda.synchronize()
+        comm.barrier()
+        gb.replay()
+        torch.cuda.synchronize()
+        comm.barrier()
+        want = torch.arange(count, dtype=torch.int32, device="cuda")
+        res["bcast_bad"] = int((brecv != want).sum().item())
+        # the caller's registration is still mapped after the churn: write a pattern into the next
+        # rank's z through the pointer registered before it (a plugin's use), check on the owner
+        src = torch.full((count,), 100 + rank, dtype=torch.int16, device="cuda")
+        L = m.lib()
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        m.check(L.mscclppAmdCopyJobsPolicy((vp * 1)(src.data_ptr()), (vp * 1)(pz[(rank + 1) % n]),
+                                           (sz * 1)(2 * count), 1, 64, 0, 0, m.stream_ptr()), "copy jobs")
+        torch.cuda.synchronize()
+        comm.barrier()
+        res["registered_bad"] = int((z != 100 + (rank - 1) % n).sum().item())
+        res["err2"] = comm.device_error()
+        del g, gb, keep
         comm.barrier()
         comm.destroy()
         q.put((rank, res, None))
@@ -232,3 +271,4 @@ def test_captured_buffers_survive_registration_churn(built):
     for rank in range(n):
         assert got[rank]["pinned"] >= 1 and got[rank]["regs"] == 64 + got[rank]["pinned"], got
         assert got[rank]["bad"] == 0 and got[rank]["err"] == 0, got
+        assert got[rank]["bcast_bad"] == 0 and got[rank]["registered_bad"] == 0 and got[rank]["err2"] == 0, got
