@@ -11,6 +11,7 @@
 #include <string>
 
 #include "mscclpp_amd/core.hpp"
+#include "mscclpp_amd/mscclpp_amd.h"
 
 namespace mscclpp_amd {
 
@@ -26,12 +27,14 @@ std::shared_ptr<T> gpuCallocShared(size_t nelems = 1) {
   gpuCheck(hipMemset(p, 0, nelems * sizeof(T)), "hipMemset");
   return std::shared_ptr<T>(static_cast<T*>(p), [](T* q) { (void)hipFree(q); });
 }
+// Uncached memory comes from the library's process-lifetime pool (mscclppAmdMallocUncached, zeroed;
+// released back to the pool, never to HIP, while the process runs: DESIGN.md §21).
 template <typename T>
 std::shared_ptr<T> gpuCallocUncachedShared(size_t nelems = 1) {
   void* p = nullptr;
-  gpuCheck(hipExtMallocWithFlags(&p, nelems * sizeof(T), hipDeviceMallocUncached), "hipExtMallocWithFlags");
-  gpuCheck(hipMemset(p, 0, nelems * sizeof(T)), "hipMemset");
-  return std::shared_ptr<T>(static_cast<T*>(p), [](T* q) { (void)hipFree(q); });
+  if (mscclppAmdMallocUncached(&p, nelems * sizeof(T)) != 0)
+    throw Error("mscclppAmdMallocUncached failed", ErrorCode::SystemError);
+  return std::shared_ptr<T>(static_cast<T*>(p), [](T* q) { (void)mscclppAmdFree(q); });
 }
 }  // namespace detail
 

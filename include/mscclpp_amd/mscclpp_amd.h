@@ -88,26 +88,31 @@ typedef struct {
 } mscclppAmdRankView;
 
 /* ---- memory ------------------------------------------------------------------------------- */
+/* Uncached memory (hipDeviceMallocUncached, zeroed; the reference's GpuBuffer on AMD,
+ * gpu_utils.cc:139-147) comes from a process-lifetime pool: mscclppAmdFree hands a pooled block back
+ * to the pool (after a device synchronize, as hipFree does), never to HIP, so no later allocation is
+ * placed where uncached memory was.  mscclppAmdFree hipFree's anything else.
+ * mscclppAmdUncachedPoolStats: bytes allocated from HIP, in use, and free in the pool. */
 int mscclppAmdMallocUncached(void** ptr, size_t bytes);
 int mscclppAmdMalloc(void** ptr, size_t bytes);
 int mscclppAmdFree(void* ptr);
+int mscclppAmdUncachedPoolStats(size_t* held, size_t* inUse, size_t* freeBytes);
 int mscclppAmdFlagsInit(uint32_t* flags, void* stream);
 
 /* ---- 1-GPU microbench (BASELINE config 2) ------------------------------------------------- */
 /* out = x (op) unpack(pack(y, flag)); pkts: 2*bytes of (uncached) device memory; bytes % 16 == 0.
- * nblocks <= 0 selects the default grid.  budgetTicks: spin budget in 10 ns ticks. */
+ * nblocks <= 0 selects the default shape (up to 4 MiB: one 256-lane workgroup per 4 KiB, one round;
+ * larger: 256-lane workgroups with 8 KiB per round, up to 1024 of them); nblocks > 0 runs the large
+ * form on that grid (<= 1024).  budgetTicks: spin budget in 10 ns ticks. */
 int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts, void* out, size_t bytes, int dtype, int op,
                              uint32_t* flags, int nblocks, uint64_t budgetTicks, uint32_t* err, void* stream);
+/* The default shape for `bytes`: waves per workgroup, KiB per wave and round, workgroups, skewed. */
+int mscclppAmdSelfReduceLL16DefaultShape(size_t bytes, int* waves, int* units, int* nblocks, int* skew);
 
-/* Tuning / ceiling helpers used by the benchmark (fp16 SUM).  Variant 0 = the product kernel
- * (partner tiles consumed one round late), 1 = the unskewed round-1 form, 2 / 3 = 4 / 1 KiB of
- * payload per wave and round, 4 / 5 = variants 0 / 1 adding the number of first-poll misses to
- * pollMiss[0] (diagnostic).  mscclppAmdCopy is a plain streaming copy (HBM ceiling);
+/* Ceiling helpers used by the benchmark.  mscclppAmdCopy is a plain streaming copy (HBM ceiling);
  * mscclppAmdCopyJobs runs njobs copies in ONE launch, blocksPerJob workgroups each (the xGMI probe:
- * all peers' links driven from one kernel on one stream). */
-int mscclppAmdSelfReduceLL16Variant(const void* x, const void* y, void* pkts, void* out, size_t bytes, uint32_t* flags,
-                                    int nblocks, int variant, uint64_t budgetTicks, uint32_t* err, uint32_t* pollMiss,
-                                    void* stream);
+ * all peers' links driven from one kernel on one stream).  (Kernel shape sweeps and first-poll miss
+ * counts of the self-reduce live in the test diagnostics library, tests/bin/libselfreduce_diag.so.) */
 int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblocks, void* stream);
 int mscclppAmdCopyJobs(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs, int blocksPerJob,
                        void* stream);

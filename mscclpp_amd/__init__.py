@@ -113,7 +113,7 @@ def lib():
         "mscclppAmdCopy": [vp, vp, sz, i32, vp],
         "mscclppAmdCopyJobs": [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz), i32, i32, vp],
         "mscclppAmdCopyJobsPolicy": [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz), i32, i32, i32, i32, vp],
-        "mscclppAmdSelfReduceLL16Variant": [vp, vp, vp, vp, sz, vp, i32, i32, u64, vp, vp, vp],
+        "mscclppAmdSelfReduceLL16DefaultShape": [sz, vp, vp, vp, vp],
         "ncclCommSplit": [vp, i32, i32, ctypes.POINTER(vp), vp],
         "mscclppAmdBroadcastLaunch": [ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, u64, vp],
         "ncclGetUniqueId": [ctypes.POINTER(UniqueId)],

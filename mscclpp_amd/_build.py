@@ -120,14 +120,24 @@ def build_tests():
 
 
 DIAG_LIB = os.path.join(TESTBIN, "libxcdprobe.so")
+SR_DIAG_LIB = os.path.join(TESTBIN, "libselfreduce_diag.so")
+LL_DIAG_LIB = os.path.join(TESTBIN, "libll_diag.so")
 
 
 def build_diag():
-    """Test diagnostics with device code (tests/diag/xcd_probe.hip: per-XCD readback) -> tests/bin/."""
+    """Test diagnostics with device code -> tests/bin/: the per-XCD readback (tests/diag/xcd_probe.hip)
+    and the self-reduce kernel with its shape / poll-miss entry (kernels/self_reduce.hip built with
+    MSCCLPP_AMD_DIAG, symbols bound inside the library so it can sit beside the product one)."""
     os.makedirs(TESTBIN, exist_ok=True)
     src = os.path.join(ROOT, "tests", "diag", "xcd_probe.hip")
     if _newer(DIAG_LIB, [src]):
         _run([HIPCC, "--offload-arch=" + ARCH, "-O2", "-std=c++17", "-shared", "-fPIC", src, "-o", DIAG_LIB])
+    for src, lib in (("self_reduce.hip", SR_DIAG_LIB), ("allreduce_ll.hip", LL_DIAG_LIB)):
+        src = os.path.join(CSRC, "kernels", src)
+        if _newer(lib, [src] + _headers()):
+            _run([HIPCC, "--offload-arch=" + ARCH, "-x", "hip", "-O3", "-std=c++17", "-fPIC", "-shared",
+                  "-DMSCCLPP_AMD_DIAG", "-I" + INCLUDE, "-I" + os.path.join(CSRC, "kernels"), "-Wl,-Bsymbolic", src,
+                  "-o", lib])
     return DIAG_LIB
 
 

@@ -75,8 +75,8 @@ Fifo::Fifo(int size) : size_(size) {
 Fifo::~Fifo() {
   (void)hipHostFree((void*)triggers_);
   (void)hipHostFree((void*)tail_);
-  (void)hipFree(head_);
-  (void)hipFree(tailCache_);
+  freeDevice(head_);
+  freeDevice(tailCache_);
 }
 
 bool Fifo::poll(ProxyTrigger& t) {

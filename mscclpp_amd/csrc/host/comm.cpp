@@ -32,7 +32,7 @@ int mscclppAmdMalloc(void** ptr, size_t bytes) {
 
 int mscclppAmdFree(void* ptr) {
   return guarded([&] {
-    if (ptr) HIPCHECK(hipFree(ptr));
+    if (ptr && !releaseUncached(ptr)) HIPCHECK(hipFree(ptr));
     return (int)ncclSuccess;
   });
 }

@@ -122,12 +122,14 @@ inline size_t bulkScratchInitBytes() {
   return mb << 20;
 }
 
-inline void* allocUncached(size_t bytes) {
-  void* p = nullptr;
-  HIPCHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
-  HIPCHECK(hipMemset(p, 0, bytes));
-  return p;
-}
+// Uncached device memory (hipDeviceMallocUncached, zeroed) from the process-lifetime pool
+// (uncached_pool.cpp: never returned to HIP while the process runs).  freeDevice
+// returns a pooled block to the pool and hipFree's anything else; releaseUncached is false for a
+// pointer the pool does not own.
+void* allocUncached(size_t bytes);
+bool releaseUncached(void* p);
+void freeDevice(void* p);
+void uncachedPoolStats(size_t* held, size_t* inUse, size_t* freeBytes);
 
 inline int dtypeFromNccl(ncclDataType_t t) {
   switch (t) {
@@ -638,11 +640,11 @@ struct ncclComm {
     bcastPinned.clear();
     peerLL = peerBulk = peerTok = PeerBufs();
     retired.clear();
-    if (llScratch) (void)hipFree(llScratch);
-    if (bulkScratch) (void)hipFree(bulkScratch);
-    for (void* p : outgrown) (void)hipFree(p);
+    freeDevice(llScratch);
+    freeDevice(bulkScratch);
+    for (void* p : outgrown) freeDevice(p);
     outgrown.clear();
-    if (tokens) (void)hipFree(tokens);
+    freeDevice(tokens);
     if (expected) (void)hipFree(expected);
     if (flags) (void)hipFree(flags);
     if (err) (void)hipFree(err);

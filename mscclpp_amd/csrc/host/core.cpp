@@ -401,7 +401,7 @@ std::shared_future<Semaphore> Communicator::buildSemaphore(const Connection& con
   if (!connection.valid()) throw Error("buildSemaphore: empty connection", ErrorCode::InvalidUsage);
   // my token: 8 bytes of uncached device memory (semaphore.cc:32-43), registered and sent
   void* tok = host::allocUncached(64);
-  std::shared_ptr<void> tokAlloc(tok, [](void* p) { (void)hipFree(p); });
+  std::shared_ptr<void> tokAlloc(tok, [](void* p) { host::freeDevice(p); });
   RegisteredMemory local = registerMemory(tok, sizeof(uint64_t), Transport::CudaIpc);
   auto boot = bootstrap();
   boot->send(local.serialize(), remoteRank, semTag(tag));
@@ -455,7 +455,7 @@ Host2DeviceSemaphore::Host2DeviceSemaphore(Communicator& communicator, const Con
     : Host2DeviceSemaphore(communicator.buildSemaphore(connection, connection.remoteRank(), connection.tag()).get()) {}
 
 Host2DeviceSemaphore::~Host2DeviceSemaphore() {
-  if (expectedInboundToken_) (void)hipFree(expectedInboundToken_);
+  if (expectedInboundToken_) freeDevice(expectedInboundToken_);
 }
 
 Connection& Host2DeviceSemaphore::connection() { return semaphore_.connection(); }
@@ -487,7 +487,7 @@ MemoryDevice2DeviceSemaphore::MemoryDevice2DeviceSemaphore(Communicator& communi
           communicator.buildSemaphore(connection, connection.remoteRank(), connection.tag()).get()) {}
 
 MemoryDevice2DeviceSemaphore::~MemoryDevice2DeviceSemaphore() {
-  if (expectedInboundToken_) (void)hipFree(expectedInboundToken_);
+  if (expectedInboundToken_) freeDevice(expectedInboundToken_);
 }
 
 Connection& MemoryDevice2DeviceSemaphore::connection() { return semaphore_.connection(); }

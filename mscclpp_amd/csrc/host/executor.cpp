@@ -475,9 +475,9 @@ struct mscclppAmdExecutor {
     comm->boot->barrier();  // every rank closed its mappings of our scratch before it is freed
     for (auto& kv : contexts) {
       Context& c = kv.second;
-      if (c.scratch) (void)hipFree(c.scratch);
-      if (c.sems) (void)hipFree(c.sems);
-      for (auto& p : c.plans) (void)hipFree(p.second.dev);
+      if (c.scratch) freeDevice(c.scratch);
+      if (c.sems) freeDevice(c.sems);
+      for (auto& p : c.plans) freeDevice(p.second.dev);
     }
     contexts.clear();
   }
@@ -486,10 +486,10 @@ struct mscclppAmdExecutor {
     dropContexts();
     peerTokens = PeerBufs();
     comm->boot->barrier();
-    (void)hipFree(tokens);
-    (void)hipFree(expected);
-    (void)hipFree(syncers);
-    (void)hipFree(err);
+    freeDevice(tokens);
+    freeDevice(expected);
+    freeDevice(syncers);
+    freeDevice(err);
   }
 
   Context& context(mscclppAmdExecutionPlan& plan, void* send, void* recv, uint64_t sendBytes, uint64_t recvBytes) {

@@ -226,11 +226,11 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
     comm->boot->barrier();  // peers no longer touch my data / tokens
     peers = PeerBufs();     // peers free these buffers now: close our mappings of them
     peerTok = PeerBufs();
-    (void)hipFree(err);
-    (void)hipFree(dh);
-    (void)hipFree(tok);
-    (void)hipFree(expct);
-    (void)hipFree(data);
+    freeDevice(err);
+    freeDevice(dh);
+    freeDevice(tok);
+    freeDevice(expct);
+    freeDevice(data);
     return (int)ncclSuccess;
   });
 }
@@ -319,15 +319,15 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
       numa = proxy.proxyNumaNode();
       proxy.stopProxy();
       (void)hipStreamDestroy(st);
-      (void)hipFree(dOffs);
-      (void)hipFree(dch);
+      freeDevice(dOffs);
+      freeDevice(dch);
       comm->boot->barrier();  // every peer is done with my buffers before the mappings close
     }
     out[0] = (t1 - t0) * 1e6 / iters;
     out[1] = (ok && e == 0) ? 1.0 : 0.0;
     out[2] = (double)numa;
-    (void)hipFree(src);
-    (void)hipFree(dst);
+    freeDevice(src);
+    freeDevice(dst);
     return (int)ncclSuccess;
   });
 }
@@ -491,13 +491,13 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     (void)hipStreamDestroy(st);
     comm->boot->barrier();  // peers no longer touch my buffers / tokens
     peerBuff = peerScratch = peerTok = PeerBufs();
-    (void)hipFree(gb);
-    (void)hipFree(err);
+    freeDevice(gb);
+    freeDevice(err);
     (void)hipHostFree(flushDone);
-    (void)hipFree(tok);
-    (void)hipFree(expct);
-    (void)hipFree(scratch);
-    (void)hipFree(buff);
+    freeDevice(tok);
+    freeDevice(expct);
+    freeDevice(scratch);
+    freeDevice(buff);
     return (int)ncclSuccess;
   });
 }

@@ -85,6 +85,50 @@ __device__ __forceinline__ u32x2 unit_get(__amdgpu_buffer_rsrc_t pk, uint32_t pb
   }
   return w;
 }
+// First poll of unit `pbyte` in every peer's region (peer p's at p * stride of `base`): all loads
+// are issued, unconditionally and in one basic block, before any value is compared, so they are in
+// flight together (a compare right after each load, or a load under a branch, made the compiler wait
+// for it before issuing the next: one memory round trip per peer).  A slot that is not a peer (own
+// rank, p >= nranks) is loaded through a zero-length buffer resource: out of range, it returns zeros
+// without touching memory.  Returns the mask of peers whose packet had not landed; w[p] holds the
+// payload of the others.
+__device__ __forceinline__ void poll_issue(const uint8_t* base, uint32_t stride, uint32_t pbyte, uint32_t peers,
+                                           u32x4* raw) {
+#pragma unroll
+  for (int p = 0; p < kMaxRanks; ++p) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0,
+                                                     ((peers >> p) & 1u) ? 0xFFFFFFFFu : 0u, 0x00020000);
+    raw[p] = load16<kSystem>(r, (uint32_t)p * stride + pbyte);
+  }
+}
+__device__ __forceinline__ uint32_t poll_eval(const u32x4* raw, uint32_t flag, uint32_t peers, u32x2* w) {
+  uint32_t missing = 0;
+#pragma unroll
+  for (int p = 0; p < kMaxRanks; ++p) {
+    w[p] = u32x2{raw[p].x, raw[p].z};
+    if (raw[p].y != flag || raw[p].w != flag) missing |= 1u << p;
+  }
+  return missing & peers;
+}
+__device__ __forceinline__ uint32_t poll_units(const uint8_t* base, uint32_t stride, uint32_t pbyte, uint32_t flag,
+                                               uint32_t peers, u32x2* w) {
+  u32x4 raw[kMaxRanks];
+  poll_issue(base, stride, pbyte, peers, raw);
+  return poll_eval(raw, flag, peers, w);
+}
+// A unit whose first poll missed: spin until it lands (the caller keeps the values of the units
+// that were ready, so only the missing ones are read again).
+__device__ __forceinline__ u32x2 unit_wait(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, bool single,
+                                           uint64_t budget, uint32_t* err) {
+  u32x2 w;
+  SpinGuard g(budget);
+  do {
+    __builtin_amdgcn_s_sleep(1);
+    if (unit_try(pk, pbyte, flag, w, single)) return w;
+  } while (!g.expired());
+  report_error(err, kErrPacketTimeout);
+  return u32x2{0, 0};
+}
 // 8-byte payload at byte `off` of `base`, of which `valid` bytes are inside the buffer
 __device__ __forceinline__ u32x2 payload_ld(__amdgpu_buffer_rsrc_t r, const uint8_t* base, uint64_t off, uint32_t valid) {
   if (valid >= 8) return load8<kPlain>(r, (uint32_t)off);
@@ -108,17 +152,20 @@ __device__ __forceinline__ void payload_st(__amdgpu_buffer_rsrc_t r, uint8_t* ba
     if ((uint32_t)i < valid) base[off + i] = (uint8_t)((i < 4 ? v.x : v.y) >> ((i % 4) * 8));
 }
 
-template <int DT, int OP, int NV>
+constexpr int kUnroll = 4;  // units per lane handled together in the multi-pass loops
+
+// V (0 in the product): bits that switch a part back to its round-2 form, for same-process A/B
+// timing through the diagnostics build (MSCCLPP_AMD_DIAG): 1 = step 1 one unit per pass, 2 = step 3
+// one unit per pass, 4 = polls tested as issued and every peer re-read after a miss, 8 = a scalar
+// flag load ahead of everything else.
+template <int DT, int OP, int NV, int V = 0>
 __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16Geom g, int nranks, uint64_t budget) {
   const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
   const int rank = v.rank;
   const int nPeers = nranks - 1;
   const uint32_t T = blockDim.x, tid = threadIdx.x, G = gridDim.x, b = blockIdx.x;
-  const uint32_t flag = v.flags[b];
-  const uint64_t base = (flag & 1u) ? g.hbOdd : g.hbEven;  // numScratchBuff = 2 (allreduce_packet.cu:60)
   const uint8_t* in = (const uint8_t*)v.input;
   uint8_t* out = (uint8_t*)v.output;
-  uint8_t* scr = (uint8_t*)v.scratch + base;
   const auto rin = make_rsrc(in);
   const auto rout = make_rsrc(out);
   const uint64_t sliceBytes = g.wpr * 4;
@@ -128,21 +175,63 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
     return e < g.bytes ? e : g.bytes;
   };
   const uint32_t npk = (uint32_t)g.ppr;          // packets (units) per slice
+  const uint32_t peers = ((1u << nranks) - 1u) & ~(1u << rank);
   const uint32_t bpp = G / (uint32_t)nPeers;     // blocks per peer for steps 1 and 3
   const bool inPeerGroup = b < bpp * (uint32_t)nPeers;
   const int peerIdx = inPeerGroup ? (int)(b / bpp) : 0;
   const int remote = peerIdx < rank ? peerIdx : peerIdx + 1;
   const uint32_t lb = inPeerGroup ? b % bpp : 0;
   trace_stamp(g.trace, 0);
+  // The flag is a vector load issued right before the first unit of step 1, so the two are in flight
+  // together: no round trip of its own before the first put (a scalar flag load was waited for
+  // before the payload load was issued).
+  uint32_t flagv;
+  if constexpr ((V & 8) != 0)
+    flagv = v.flags[b];
+  else
+    flagv = __hip_atomic_load(v.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t soff1 = (uint64_t)remote * sliceBytes;
+  const uint64_t send1 = sliceEnd(remote);
+  const uint32_t j1 = lb * T + tid;
+  u32x2 w1{0, 0};
+  if (inPeerGroup && j1 < npk) w1 = payload_ld(rin, in, soff1 + (uint64_t)j1 * 8, clamp_valid(send1, soff1 + (uint64_t)j1 * 8, 8));
+  const uint32_t flag = wave_uniform(flagv);
+  const uint64_t base = (flag & 1u) ? g.hbOdd : g.hbEven;  // numScratchBuff = 2 (allreduce_packet.cu:60)
+  uint8_t* scr = (uint8_t*)v.scratch + base;
 
   // step 1: put my copy of slice `remote` into rank `remote`'s scratch at rank*ppr packets (:89-90)
   if (inPeerGroup) {
     const auto rdst = make_rsrc((uint8_t*)v.peerScratch[remote] + base + (uint64_t)rank * g.ppr * 16);
-    const uint64_t soff = (uint64_t)remote * sliceBytes;
-    const uint64_t send = sliceEnd(remote);
-    for (uint32_t j = lb * T + tid; j < npk; j += bpp * T) {
-      const uint64_t off = soff + (uint64_t)j * 8;
-      unit_put<kSystem>(rdst, j * 16u, payload_ld(rin, in, off, clamp_valid(send, off, 8)), flag, false);
+    const uint32_t stride = bpp * T;
+    if (j1 < npk) unit_put<kSystem>(rdst, j1 * 16u, w1, flag, false);
+    // further passes kUnroll units per lane at a time: every payload load issued before any put, so
+    // the passes overlap instead of paying one load round trip each.  A lane whose unit is not a
+    // whole 8 bytes inside the buffer loads the slice's first unit instead (ignored) and takes the
+    // byte-wise path at its put.
+    auto whole = [&](uint64_t off) { return off + 8 <= send1; };
+    if constexpr ((V & 1) != 0) {
+      for (uint32_t j = j1 + stride; j < npk; j += stride) {
+        const uint64_t off = soff1 + (uint64_t)j * 8;
+        unit_put<kSystem>(rdst, j * 16u, payload_ld(rin, in, off, clamp_valid(send1, off, 8)), flag, false);
+      }
+    } else
+    for (uint32_t j0 = j1 + stride; j0 < npk; j0 += kUnroll * stride) {
+      u32x2 w[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t j = j0 + (uint32_t)u * stride;
+        const uint64_t off = soff1 + (uint64_t)j * 8;
+        w[u] = load8<kPlain>(rin, (uint32_t)(j < npk && whole(off) ? off : soff1));
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t j = j0 + (uint32_t)u * stride;
+        if (j < npk) {
+          const uint64_t off = soff1 + (uint64_t)j * 8;
+          const u32x2 x = whole(off) ? w[u] : payload_ld(rin, in, off, clamp_valid(send1, off, 8));
+          unit_put<kSystem>(rdst, j * 16u, x, flag, false);
+        }
+      }
     }
   }
 
@@ -157,22 +246,35 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
     for (uint32_t j = b * T + tid; j < npk; j += G * T) {
       const uint64_t off = soff + (uint64_t)j * 8;
       const uint32_t valid = clamp_valid(send, off, 8);
-      Accum<DT, OP, 2> sum(payload_ld(rin, in, off, valid));  // upcastVector (:98-99)
+      // every peer's packet polled once and the own payload loaded, all loads in flight together
+      // (issued before any value is looked at, so no wait separates them); only the peers whose
+      // packet had not landed are polled again (the values of the others are kept), then the sum
+      // runs in the reference order
       u32x2 w[kMaxRanks];
-      bool ready = true;
-#pragma unroll
-      for (int p = 0; p < kMaxRanks; ++p)
-        if (p < nranks && p != rank) ready &= unit_try(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, w[p], false);
-      if (ready) {
+      uint32_t missing = 0;
+      u32x2 own;
+      if constexpr ((V & 4) != 0) {
+        own = payload_ld(rin, in, off, valid);
+        bool ready = true;
 #pragma unroll
         for (int p = 0; p < kMaxRanks; ++p)
-          if (p < nranks && p != rank) sum.add(w[p]);
+          if (p < nranks && p != rank) ready &= unit_try(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, w[p], false);
+        if (!ready) missing = peers;  // round 2: every peer read again
       } else {
-        for (int p = 0; p < nranks; ++p) {
-          if (p == rank) continue;
-          sum.add(unit_get(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, false, budget, v.err));
-        }
+        u32x4 raw[kMaxRanks];
+        poll_issue(scr, (uint32_t)(g.ppr * 16), j * 16u, peers, raw);
+        own = payload_ld(rin, in, off, valid);
+        missing = poll_eval(raw, flag, peers, w);
       }
+      Accum<DT, OP, 2> sum(own);  // upcastVector (:98-99)
+      if (missing) {
+#pragma unroll
+        for (int p = 0; p < kMaxRanks; ++p)
+          if ((missing >> p) & 1u) w[p] = unit_wait(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, false, budget, v.err);
+      }
+#pragma unroll
+      for (int p = 0; p < kMaxRanks; ++p)
+        if ((peers >> p) & 1u) sum.add(w[p]);
       const u32x2 acc = sum.template get<u32x2>();  // downcastVector (:107-108)
       payload_st(rout, out, off, acc, valid);
       // broadcast: a runtime loop, so one descriptor is live at a time (SGPR budget)
@@ -192,36 +294,71 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
     const auto rres = make_rsrc(scr + g.roff + (uint64_t)remote * g.ppr * 16);
     const uint64_t soff = (uint64_t)remote * sliceBytes;
     const uint64_t send = sliceEnd(remote);
-    for (uint32_t j = lb * T + tid; j < npk; j += bpp * T) {
-      const uint64_t off = soff + (uint64_t)j * 8;
-      const u32x2 w = unit_get(rres, j * 16u, flag, false, budget, v.err);
-      payload_st(rout, out, off, w, clamp_valid(send, off, 8));
+    const uint32_t stride = bpp * T;
+    // kUnroll units per lane at a time: all their polls issued before any is looked at
+    if constexpr ((V & 2) != 0) {
+      for (uint32_t j = lb * T + tid; j < npk; j += stride) {
+        const uint64_t off = soff + (uint64_t)j * 8;
+        payload_st(rout, out, off, unit_get(rres, j * 16u, flag, false, budget, v.err), clamp_valid(send, off, 8));
+      }
+    } else
+    for (uint32_t j0 = lb * T + tid; j0 < npk; j0 += kUnroll * stride) {
+      u32x4 raw[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t j = j0 + (uint32_t)u * stride;
+        raw[u] = load16<kSystem>(rres, (j < npk ? j : j0) * 16u);
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t j = j0 + (uint32_t)u * stride;
+        if (j < npk) {
+          const uint64_t off = soff + (uint64_t)j * 8;
+          u32x2 w{raw[u].x, raw[u].z};
+          if (raw[u].y != flag || raw[u].w != flag) w = unit_wait(rres, j * 16u, flag, false, budget, v.err);
+          payload_st(rout, out, off, w, clamp_valid(send, off, 8));
+        }
+      }
     }
   }
   trace_stamp(g.trace, 3);
   bump_flags(v.flags, flag);
 }
 
-template <int DT, int OP, int NV>
+template <int DT, int OP, int NV, int V = 0>  // V: as allreduceLL16Kernel's (bits 4 and 8)
 __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Geom g, int nranks, uint64_t budget) {
   const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
   const int rank = v.rank;
   const uint32_t T = blockDim.x, G = gridDim.x;
   const uint32_t gtid = blockIdx.x * T + threadIdx.x;
-  const uint32_t flag = v.flags[blockIdx.x];
-  const uint64_t base = (flag & 1u) ? v.scratchBytes / 2 : 0;
   const uint8_t* in = (const uint8_t*)v.input;
   uint8_t* out = (uint8_t*)v.output;
   const auto rin = make_rsrc(in);
   const auto rout = make_rsrc(out);
   const uint64_t region = g.W * 8;  // LL8 bytes one source rank occupies in a peer's scratch half
+  const uint32_t peers = ((1u << nranks) - 1u) & ~(1u << rank);
   trace_stamp(g.trace, 0);
+  // The flag is a vector load issued right before this lane's first payload load, so the two are in
+  // flight together (one memory round trip before the first put, where a scalar flag load was waited
+  // for before the payload load was issued); the payload is also the own term of that unit's sum.
+  uint32_t flagv;
+  if constexpr ((V & 8) != 0)
+    flagv = v.flags[blockIdx.x];
+  else
+    flagv = __hip_atomic_load(v.flags + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  u32x2 w0{0, 0};
+  if (gtid < g.units) {
+    const bool single = 2ull * gtid + 1 >= g.W;
+    w0 = payload_ld(rin, in, (uint64_t)gtid * 8, clamp_valid(g.bytes, (uint64_t)gtid * 8, single ? 4 : 8));
+  }
+  const uint32_t flag = wave_uniform(flagv);
+  const uint64_t base = (flag & 1u) ? v.scratchBytes / 2 : 0;
 
   // put my whole buffer into every peer's scratch at rank*W packets (allreduce_allpair_packet.cu:39-42)
   for (uint32_t j = gtid; j < g.units; j += G * T) {
     const bool single = 2ull * j + 1 >= g.W;
     const uint64_t off = (uint64_t)j * 8;
-    const u32x2 w = payload_ld(rin, in, off, clamp_valid(g.bytes, off, single ? 4 : 8));
+    const u32x2 w = j == gtid ? w0 : payload_ld(rin, in, off, clamp_valid(g.bytes, off, single ? 4 : 8));
 #pragma unroll 1
     for (int q = 0; q < nranks; ++q) {
       if (q == rank) continue;
@@ -237,22 +374,36 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
     const bool single = 2ull * j + 1 >= g.W;
     const uint64_t off = (uint64_t)j * 8;
     const uint32_t valid = clamp_valid(g.bytes, off, single ? 4 : 8);
-    Accum<DT, OP, 2> sum(payload_ld(rin, in, off, valid));  // upcastVector (:54)
+    Accum<DT, OP, 2> sum(j == gtid ? w0 : payload_ld(rin, in, off, valid));  // upcastVector (:54)
     u32x2 w[kMaxRanks];
-    bool ready = true;
-#pragma unroll
-    for (int p = 0; p < kMaxRanks; ++p)
-      if (p < nranks && p != rank) ready &= unit_try(rscr, (uint32_t)(p * region) + j * 16u, flag, w[p], single);
-    if (ready) {
+    // peers whose packet had not landed at the first poll: only those are re-polled.  The waves
+    // without the lone trailing LL8 packet (all but at most one) poll 16-byte units with every load
+    // issued before any value is looked at; the one that has it takes the per-lane path.
+    const uint32_t jw = wave_uniform(j);  // the wave's first unit (lanes hold consecutive units)
+    const bool waveSingle = (g.W & 1) && 2ull * (jw + 63) + 1 >= g.W;
+    uint32_t missing = 0;
+    if constexpr ((V & 4) != 0) {
+      bool ready = true;
 #pragma unroll
       for (int p = 0; p < kMaxRanks; ++p)
-        if (p < nranks && p != rank) sum.add(w[p]);
+        if (p < nranks && p != rank) ready &= unit_try(rscr, (uint32_t)(p * region) + j * 16u, flag, w[p], single);
+      if (!ready) missing = peers;  // round 2: every peer read again
+    } else if (!waveSingle) {
+      missing = poll_units((const uint8_t*)v.scratch + base, (uint32_t)region, j * 16u, flag, peers, w);
     } else {
-      for (int p = 0; p < nranks; ++p) {
-        if (p == rank) continue;
-        sum.add(unit_get(rscr, (uint32_t)(p * region) + j * 16u, flag, single, budget, v.err));
-      }
+#pragma unroll
+      for (int p = 0; p < kMaxRanks; ++p)
+        if (((peers >> p) & 1u) && !unit_try(rscr, (uint32_t)(p * region) + j * 16u, flag, w[p], single))
+          missing |= 1u << p;
     }
+    if (missing) {
+#pragma unroll
+      for (int p = 0; p < kMaxRanks; ++p)
+        if ((missing >> p) & 1u) w[p] = unit_wait(rscr, (uint32_t)(p * region) + j * 16u, flag, single, budget, v.err);
+    }
+#pragma unroll
+    for (int p = 0; p < kMaxRanks; ++p)
+      if ((peers >> p) & 1u) sum.add(w[p]);
     payload_st(rout, out, off, sum.template get<u32x2>(), valid);  // downcastVector (:61)
   }
   trace_stamp(g.trace, 2);
@@ -351,23 +502,23 @@ size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype) {
 
 static thread_local int g_ll_launch_status = 0;
 
-template <int DT, int OP, int NV>
+template <int DT, int OP, int NV, int V = 0>
 static void launchLL16T(const Views<NV>& vw, int nviews, const LL16Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
                         hipStream_t s) {
-  if (!grid_coresident(allreduceLL16Kernel<DT, OP, NV>, nthreads, (long)nblocks * nviews)) {
+  if (!grid_coresident(allreduceLL16Kernel<DT, OP, NV, V>, nthreads, (long)nblocks * nviews)) {
     g_ll_launch_status = 5;  // ncclInvalidUsage: the grid cannot be resident at once: its packet waits would deadlock
     return;
   }
-  hipLaunchKernelGGL((allreduceLL16Kernel<DT, OP, NV>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
+  hipLaunchKernelGGL((allreduceLL16Kernel<DT, OP, NV, V>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
 }
-template <int DT, int OP, int NV>
+template <int DT, int OP, int NV, int V = 0>
 static void launchLL8T(const Views<NV>& vw, int nviews, const LL8Geom& g, int nranks, int nblocks, int nthreads, uint64_t budget,
                        hipStream_t s) {
-  if (!grid_coresident(allreduceLL8Kernel<DT, OP, NV>, nthreads, (long)nblocks * nviews)) {
+  if (!grid_coresident(allreduceLL8Kernel<DT, OP, NV, V>, nthreads, (long)nblocks * nviews)) {
     g_ll_launch_status = 5;  // ncclInvalidUsage: the grid cannot be resident at once: its packet waits would deadlock
     return;
   }
-  hipLaunchKernelGGL((allreduceLL8Kernel<DT, OP, NV>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
+  hipLaunchKernelGGL((allreduceLL8Kernel<DT, OP, NV, V>), dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, g, nranks, budget);
 }
 
 template <int DT, int OP>
@@ -471,3 +622,41 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
 }
 
 }  // namespace mscclpp_amd
+
+#ifdef MSCCLPP_AMD_DIAG
+// Same-process A/B timing of the LL kernels' variants (fp16 SUM; the diagnostics library
+// tests/bin/libll_diag.so only): algo MSCCLPP_AMD_ALGO_PACKET / _ALLPAIR, variant bits as V above
+// (0, 1, 2, 3, 4, 7, 8, 15), views of nviews in-process ranks (or one), default launch shape for 0.
+uint64_t* g_mscclppAmdTrace = nullptr;
+using namespace mscclpp_amd;
+extern "C" int mscclppAmdDiagAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int nranks,
+                                         size_t bytes, int nblocks, int nthreads, int variant, uint64_t budget,
+                                         void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (nviews != nranks || nranks < 2 || nranks > kMaxRanks) return 4;
+  Views<kMaxRanks> vw{};
+  for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
+  g_ll_launch_status = 0;
+  if (algo == MSCCLPP_AMD_ALGO_PACKET) {
+    ll16Defaults(nranks, bytes, nblocks, nthreads);
+    LL16Geom g = ll16Geometry(nranks, bytes, kF16);
+    if (views[0].scratchBytes < ll16ScratchRequired(nranks, bytes, kF16)) return 5;
+    g.hbOdd = views[0].scratchBytes / 2;
+    g.hbEven = 0;
+#define LV(VV) if (variant == VV) launchLL16T<kF16, kSum, kMaxRanks, VV>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+    LV(0) LV(1) LV(2) LV(3) LV(4) LV(7) LV(8) LV(15)
+#undef LV
+  } else if (algo == MSCCLPP_AMD_ALGO_ALLPAIR) {
+    ll8Defaults(nranks, bytes, nblocks, nthreads);
+    const LL8Geom g = ll8Geometry(bytes, kF16);
+    if (views[0].scratchBytes < ll8ScratchRequired(nranks, bytes, kF16)) return 5;
+#define LV(VV) if (variant == VV) launchLL8T<kF16, kSum, kMaxRanks, VV>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+    LV(0) LV(4) LV(8) LV(12)
+#undef LV
+  } else {
+    return 4;
+  }
+  if (g_ll_launch_status) return g_ll_launch_status;
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+#endif

@@ -29,18 +29,26 @@ namespace mscclpp_amd {
 //
 // COUNT: diagnostic build that adds the number of packets whose first poll missed to pollMiss[0]
 // (one atomic per wave and round), to measure the re-poll traffic the skew removes.
-template <int DT, int OP, int U, bool SKEW, bool COUNT>
-__global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
-                                                               uint8_t* pkts, uint8_t* __restrict__ out, uint64_t bytes,
-                                                               uint32_t* flags, uint64_t budget, uint32_t* err,
-                                                               uint32_t* pollMiss) {
-  constexpr uint32_t kWaves = 4;
+//
+// W waves per workgroup, U KiB of payload per wave and round.  Large buckets: W = 4, U = 2 on 1024
+// workgroups.  Small buckets are latency-bound (a few dependent memory round trips): 1 KiB per wave
+// and one round, so the chain is X / Y loads -> packet stores -> partner's polls -> output stores,
+// with no drain round (SKEW only pays from 3 rounds on).
+// The flag is read by a vector load issued with the first payload loads, so its latency overlaps
+// theirs instead of preceding them (a scalar flag load made the kernel wait for it before issuing
+// anything else).
+template <int DT, int OP, int W, int U, bool SKEW, bool COUNT>
+__global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t* __restrict__ x,
+                                                                  const uint8_t* __restrict__ y, uint8_t* pkts,
+                                                                  uint8_t* __restrict__ out, uint64_t bytes,
+                                                                  uint32_t* flags, uint64_t budget, uint32_t* err,
+                                                                  uint32_t* pollMiss) {
+  constexpr uint32_t kWaves = W;
   constexpr uint64_t kTileBytes = (uint64_t)kWaves * U * 1024;  // payload bytes per workgroup and round
   __shared__ __attribute__((aligned(16))) uint8_t ldsP[kWaves][U][1024];
   __shared__ __attribute__((aligned(16))) uint8_t ldsC[kWaves][U][1024];
   const uint32_t G = gridDim.x, b = blockIdx.x;
-  const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
-  const uint32_t flag = flags[b];
+  const uint32_t wave = wave_uniform(threadIdx.x / 64), lane = threadIdx.x % 64;  // wave-uniform: scalar rsrc
   const uint64_t ntiles = (bytes + kTileBytes - 1) / kTileBytes;
   const uint64_t rounds = (ntiles + G - 1) / G;
   const uint32_t partner = b ^ 1u;
@@ -54,20 +62,24 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
       if (c + lane * 16 < bytes) yw[k] = load16<kNonTemporal>(make_rsrc(y + c), lane * 16);
     }
   };
+  u32x4 a[U];
+  auto load_x = [&](uint64_t tp) {
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t c = chunk(tp, k);
+      if (c + lane * 16 < bytes) a[k] = load16<kNonTemporal>(make_rsrc(x + c), lane * 16);
+    }
+  };
+  const uint32_t flagv = __hip_atomic_load(flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (b < ntiles) load_y(b);
+  if (!SKEW && partner < G && partner < ntiles) load_x(partner);  // round 0's consumed tile
+  const uint32_t flag = wave_uniform(flagv);
   for (uint64_t i = 0; i < rounds + (SKEW ? 1 : 0); ++i) {
     const uint64_t t = i * G + b;                          // packed this round (i < rounds)
     const uint64_t tp = (SKEW ? i - 1 : i) * G + partner;  // consumed this round
     const bool pack = i < rounds && t < ntiles;
     const bool consume = (!SKEW || i > 0) && partner < G && tp < ntiles;
-    u32x4 a[U];
-    if (consume) {
-#pragma unroll
-      for (int k = 0; k < U; ++k) {
-        const uint64_t c = chunk(tp, k);
-        if (c + lane * 16 < bytes) a[k] = load16<kNonTemporal>(make_rsrc(x + c), lane * 16);
-      }
-    }
+    if (consume && (SKEW || i > 0)) load_x(tp);
     // ---- pack: payload -> LDS -> packet-major stores (packets j and 64 + j of each 1 KiB chunk)
     if (pack) {
 #pragma unroll
@@ -86,20 +98,24 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
     }
     // ---- consume a partner tile: packet-major polls -> LDS -> payload-major sum and store
     if (consume) {
+      // every poll of the tile issued before any is looked at (a readiness test right after each
+      // load made the compiler wait for it before issuing the next).  Lanes past the end of the
+      // buffer re-read the chunk's first packet (ignored); a chunk wholly past the end (uniform)
+      // loads through a zero-length resource: out of range, zeros, no memory access.
       u32x4 v[2 * U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const uint64_t c = chunk(tp, k);
+        const auto rp = __builtin_amdgcn_make_buffer_rsrc(pkts + 2 * c, 0, c < bytes ? 0xFFFFFFFFu : 0u, 0x00020000);
+        v[2 * k] = load16<kSystem>(rp, c + lane * 8 < bytes ? lane * 16 : 0u);
+        v[2 * k + 1] = load16<kSystem>(rp, c + 512 + lane * 8 < bytes ? 1024 + lane * 16 : 0u);
+      }
       bool ok = true;
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const uint64_t c = chunk(tp, k);
-        const auto rp = make_rsrc(pkts + 2 * c);
-        if (c + lane * 8 < bytes) {
-          v[2 * k] = load16<kSystem>(rp, lane * 16);
-          ok &= LL16Packet::ready(v[2 * k], flag);
-        }
-        if (c + 512 + lane * 8 < bytes) {
-          v[2 * k + 1] = load16<kSystem>(rp, 1024 + lane * 16);
-          ok &= LL16Packet::ready(v[2 * k + 1], flag);
-        }
+        if (c + lane * 8 < bytes) ok &= LL16Packet::ready(v[2 * k], flag);
+        if (c + 512 + lane * 8 < bytes) ok &= LL16Packet::ready(v[2 * k + 1], flag);
       }
       if constexpr (COUNT) {
         uint32_t miss = 0;
@@ -148,24 +164,59 @@ __global__ void __launch_bounds__(256) selfReduceLL16LdsKernel(const uint8_t* __
   bump_flags(flags, flag);
 }
 
+// Launch shape of the product kernel for `bytes` (nblocks > 0: the caller's grid for the large form),
+// from the shape sweep (tools/sweep_self_reduce.py, profiles/r3_sweep_self_reduce.json):
+//  * up to 4 MiB: 4 waves x 1 KiB per workgroup, one workgroup per 4 KiB tile (one round): 3.9 us at
+//    64-256 KiB against 4.6 us with one-wave workgroups per KiB and 5.0 us for the large form;
+//  * larger: 4 waves x 2 KiB per workgroup, up to 1024 workgroups (4 per CU, all resident);
+//    partner tiles consumed one round late from 3 rounds on (48 MiB: the skew cut the first-poll
+//    misses from 13.9 % to 0.8 % of the packets and the traffic to 1.004 x 7 S); with one or two
+//    rounds the skew's drain round would be an extra round, so the tile is consumed in its round.
+struct SelfReduceShape {
+  int waves, units, nblocks;
+  bool skew;
+};
+static SelfReduceShape selfReduceShape(uint64_t bytes, int nblocks) {
+  SelfReduceShape sh{};
+  const uint64_t tiles4k = (bytes + 4095) / 4096;
+  if (nblocks <= 0 && tiles4k <= 1024) {
+    sh.waves = 4;
+    sh.units = 1;
+    sh.nblocks = (int)tiles4k;
+  } else {
+    sh.waves = 4;
+    sh.units = 2;
+    const uint64_t tiles = (bytes + 8191) / 8192;
+    sh.nblocks = nblocks > 0 ? nblocks : (int)(tiles < 1024 ? tiles : 1024);
+  }
+  if (sh.nblocks % 2) sh.nblocks += 1;
+  const uint64_t tile = (uint64_t)sh.waves * sh.units * 1024;
+  const uint64_t rounds = ((bytes + tile - 1) / tile + sh.nblocks - 1) / sh.nblocks;
+  sh.skew = rounds >= 3;
+  return sh;
+}
+
+template <int DT, int OP, int W, int U, bool SKEW, bool COUNT>
+static void launchSelfReduceShape(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
+                                  int nblocks, uint64_t budget, uint32_t* err, uint32_t* pollMiss, hipStream_t stream) {
+  hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, W, U, SKEW, COUNT>), dim3(nblocks), dim3(64 * W), 0, stream,
+                     (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
+                     pollMiss);
+}
+
 template <int DT, int OP>
 static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                              int nblocks, uint64_t budget, uint32_t* err, hipStream_t stream) {
-  // LDS-staged packets, 2 KiB of payload per wave and round, partner tiles consumed one round late.
-  // Exactly two rounds per workgroup (e.g. 16 MiB on 1024 workgroups): the skew's drain round is a
-  // third round, and consuming in the same round is faster there (22.1 vs 25.2 us at 16 MiB; one
-  // round or four and more: the skewed form is as fast or faster, tools/sweep_self_reduce.py).
-  constexpr uint64_t kTile = 4 * 2 * 1024;  // 4 waves x U=2 KiB
-  const uint64_t tiles = (bytes + kTile - 1) / kTile;
-  const uint64_t rounds = (tiles + (uint64_t)nblocks - 1) / (uint64_t)nblocks;
-  if (rounds == 2)
-    hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, false, false>), dim3(nblocks), dim3(256), 0, stream,
-                       (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
-                       (uint32_t*)nullptr);
+  const SelfReduceShape sh = selfReduceShape(bytes, nblocks);
+  if (sh.units == 1)
+    launchSelfReduceShape<DT, OP, 4, 1, false, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
+                                                      stream);
+  else if (sh.skew)
+    launchSelfReduceShape<DT, OP, 4, 2, true, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
+                                                     stream);
   else
-    hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, 2, true, false>), dim3(nblocks), dim3(256), 0, stream,
-                       (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
-                       (uint32_t*)nullptr);
+    launchSelfReduceShape<DT, OP, 4, 2, false, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
+                                                      stream);
 }
 
 // Streaming copy (read S, write S) used by the benchmark to measure the achievable HBM ceiling on
@@ -221,31 +272,41 @@ __global__ void __launch_bounds__(256) copyJobsKernel(CopyJobs jobs, uint32_t bl
 
 using namespace mscclpp_amd;
 
-// Tuning / diagnostic entry (fp16 SUM): variant 0 = the product form (skewed, 2 KiB per wave and
-// round), 1 = unskewed (round-1 form), 2 = skewed with 4 KiB per wave and round, 3 = skewed with
-// 1 KiB; 4 / 5 = variants 0 / 1 counting first-poll misses into pollMiss[0] (must not be null).
-extern "C" int mscclppAmdSelfReduceLL16Variant(const void* x, const void* y, void* pkts, void* out, size_t bytes,
-                                               uint32_t* flags, int nblocks, int variant, uint64_t budgetTicks,
-                                               uint32_t* err, uint32_t* pollMiss, void* streamPtr) {
+#ifdef MSCCLPP_AMD_DIAG
+// Tuning / diagnostic entry (fp16 SUM), built only into the test diagnostics library
+// (tests/bin/libselfreduce_diag.so, mscclpp_amd/_build.py build_diag): any (waves, units, skew) shape
+// on any grid, and with count = 1 the number of packets whose first poll missed added to
+// pollMiss[0] (must not be null).
+extern "C" int mscclppAmdSelfReduceLL16Shape(const void* x, const void* y, void* pkts, void* out, size_t bytes,
+                                             uint32_t* flags, int nblocks, int waves, int units, int skew, int count,
+                                             uint64_t budgetTicks, uint32_t* err, uint32_t* pollMiss, void* streamPtr) {
   hipStream_t s = (hipStream_t)streamPtr;
-  if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > 1024) return 4;
-  if ((variant == 4 || variant == 5) && !pollMiss) return 4;
+  if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > 4096) return 4;
+  if (count && !pollMiss) return 4;
   if (nblocks % 2) nblocks += 1;
-#define SRV(U, SKEW, COUNT)                                                                                       \
-  hipLaunchKernelGGL((selfReduceLL16LdsKernel<kF16, kSum, U, SKEW, COUNT>), dim3(nblocks), dim3(256), 0, s,       \
-                     (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, (uint64_t)bytes, flags, \
-                     budgetTicks, err, pollMiss)
-  switch (variant) {
-    case 0: SRV(2, true, false); break;
-    case 1: SRV(2, false, false); break;
-    case 2: SRV(4, true, false); break;
-    case 3: SRV(1, true, false); break;
-    case 4: SRV(2, true, true); break;
-    case 5: SRV(2, false, true); break;
-    default: return 4;
+#define SRS(W, U, SK, C)                                                                                      \
+  if (waves == W && units == U && (skew != 0) == SK && (count != 0) == C) {                                   \
+    launchSelfReduceShape<kF16, kSum, W, U, SK, C>(x, y, pkts, out, bytes, flags, nblocks, budgetTicks, err,  \
+                                                   pollMiss, s);                                             \
+    return hipGetLastError() == hipSuccess ? 0 : 1;                                                           \
   }
-#undef SRV
-  return hipGetLastError() == hipSuccess ? 0 : 1;
+#define SRS_SK(W, U) SRS(W, U, true, false) SRS(W, U, false, false) SRS(W, U, true, true) SRS(W, U, false, true)
+  SRS_SK(1, 1) SRS_SK(2, 1) SRS_SK(2, 2) SRS_SK(4, 1) SRS_SK(4, 2) SRS_SK(8, 1) SRS_SK(8, 2)
+#undef SRS_SK
+#undef SRS
+  return 4;
+}
+#endif
+
+// The launch shape the product entry point picks for `bytes` with nblocks = 0 (tests, tools).
+extern "C" int mscclppAmdSelfReduceLL16DefaultShape(size_t bytes, int* waves, int* units, int* nblocks, int* skew) {
+  if (!waves || !units || !nblocks || !skew) return 4;
+  const SelfReduceShape sh = selfReduceShape(bytes, 0);
+  *waves = sh.waves;
+  *units = sh.units;
+  *nblocks = sh.nblocks;
+  *skew = sh.skew ? 1 : 0;
+  return 0;
 }
 
 extern "C" int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblocks, void* streamPtr) {
@@ -303,13 +364,8 @@ extern "C" int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts
                                         void* streamPtr) {
   hipStream_t stream = (hipStream_t)streamPtr;
   if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0) return 4;
-  if (nblocks <= 0) {
-    // one 8 KiB payload tile per workgroup and round; 1024 workgroups = 4 per CU (16 KiB LDS each),
-    // all resident, so every partner pair is co-resident
-    const uint64_t tiles = (bytes + 8191) / 8192;
-    nblocks = (int)(tiles < 1024 ? tiles : 1024);
-  }
-  if (nblocks % 2) nblocks += 1;
+  // nblocks <= 0: the default shape (selfReduceShape); otherwise the large form on that grid, at most
+  // 1024 workgroups = 4 per CU (16 KiB LDS each), all resident, so every partner pair is co-resident
   if (nblocks > 1024) return 4;
   MSCCLPP_AMD_DISPATCH_ALL(dtype, op, launchSelfReduce, x, y, pkts, out, (uint64_t)bytes, flags, nblocks, budgetTicks, err, stream);
   return hipGetLastError() == hipSuccess ? 0 : 1;

@@ -69,7 +69,18 @@ def test_self_reduce_matches_reference_device_code(built, ref, dt, op):
     m.self_reduce_ll16(xd.view(tdt), yd.view(tdt), pk.ptr, out.view(tdt), flags, err, op=op)
     torch.cuda.synchronize()
     assert int(err[0].item()) == 0
-    assert torch.equal(out, rout), "sum words differ from the reference's device code"
+    got_w = out.cpu().numpy().view(np.uint32)
+    ref_w = rout.cpu().numpy().view(np.uint32)
+    if dt == O.F32 and op == O.SUM:
+        # NaN + x: LLVM may commute an fadd, so which NaN operand's payload survives is the
+        # compiler's choice per instantiation (the reference's own code is no exception): NaN words
+        # must be NaN on both sides, every other word bit-identical
+        nan = (ref_w & 0x7FFFFFFF) > 0x7F800000
+        assert np.all((got_w[nan] & 0x7FFFFFFF) > 0x7F800000), "a NaN of the reference is not NaN here"
+        bad = np.nonzero(got_w[~nan] != ref_w[~nan])[0]
+    else:
+        bad = np.nonzero(got_w != ref_w)[0]
+    assert bad.size == 0, f"{bad.size} sum words differ from the reference's device code, first {bad[:4]}"
     got_pk = m.device_view(pk.ptr, 2 * nbytes)
     ref_pk = m.device_view(rpk.ptr, 2 * nbytes)
     assert torch.equal(got_pk, ref_pk), "LL16 packet image differs from copyToPackets<LL16Packet>"

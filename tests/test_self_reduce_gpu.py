@@ -51,8 +51,13 @@ def _assert_equal_words(got, exp, dt):
 
 @pytest.mark.parametrize("dt,op", [(O.F16, O.SUM), (O.BF16, O.SUM), (O.F32, O.SUM), (O.I32, O.SUM),
                                    (O.F16, O.MIN), (O.BF16, O.MIN), (O.F32, O.MIN)])
-@pytest.mark.parametrize("nbytes,special", [(64 << 10, True), ((1 << 20) + 48, False), (4 << 20, True),
-                                            ((12 << 20) + 16, False)])  # two rounds per workgroup: unskewed form
+@pytest.mark.parametrize("nbytes,special", [
+    (16, True), (1040, False), ((7 << 10) + 48, True),   # 1 KiB per wave, one round, ragged tails
+    (64 << 10, True), ((1 << 20) + 48, False),
+    (4 << 20, True),                                     # the largest one-round grid: 1024 workgroups
+    ((4 << 20) + 16, False),                             # 2 KiB per wave, one round
+    ((12 << 20) + 16, False),                            # two rounds per workgroup: unskewed form
+    ((24 << 20) + 16, True)])                            # three rounds and more: partner tiles one round late
 def test_self_reduce_bit_exact(built, dt, op, nbytes, special):
     import mscclpp_amd as m
 
@@ -84,3 +89,19 @@ def test_self_reduce_rejects_unaligned(built):
     with pytest.raises(m.MscclppError) as e:
         m.self_reduce_ll16(x, x, x.data_ptr(), x, flags, err)
     assert e.value.code == 4
+
+
+@pytest.mark.parametrize("nbytes,units,skew", [(16, 1, 0), (4 << 20, 1, 0), ((4 << 20) + 16, 2, 0),
+                                               ((12 << 20) + 16, 2, 0), ((24 << 20) + 16, 2, 1)])
+def test_self_reduce_default_shape(built, nbytes, units, skew):
+    """The launch shape the product entry picks (1 KiB per wave up to 4 MiB, the skew from three
+    rounds per workgroup on)."""
+    import ctypes
+
+    import mscclpp_amd as m
+
+    w, u, nb, sk = (ctypes.c_int() for _ in range(4))
+    m.check(m.lib().mscclppAmdSelfReduceLL16DefaultShape(nbytes, ctypes.byref(w), ctypes.byref(u), ctypes.byref(nb),
+                                                         ctypes.byref(sk)), "default shape")
+    assert (w.value, u.value, sk.value) == (4, units, skew) and nb.value % 2 == 0 and nb.value <= 1024
+

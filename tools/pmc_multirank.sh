@@ -10,4 +10,4 @@ timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/fetch" -o r
   python3 "$ROOT/tools/inprocess_pmc_run.py" > "$OUT/fetch.log" 2>&1
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/write" -o run --output-format csv -- \
   python3 "$ROOT/tools/inprocess_pmc_run.py" > "$OUT/write.log" 2>&1
-echo done
+python3 "$ROOT/tools/summarize_pmc_multirank.py" "$OUT" "${1:-r3}"

@@ -1,7 +1,12 @@
-"""GPU tuning sweep for the 1-GPU LL16 self-reduce (fp16 SUM, 48 MiB): kernel variants x grid,
-interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24), the first-poll miss count
-of the skewed and unskewed forms (variants 4 / 5), and the streaming-copy HBM ceiling measured in
-the same run.  Variants: mscclppAmdSelfReduceLL16Variant in include/mscclpp_amd/mscclpp_amd.h."""
+"""GPU sweep of the 1-GPU LL16 self-reduce (BASELINE configs[1], fp16 SUM) by launch shape, 64 KiB ..
+48 MiB: the product entry's default shape against alternative (waves per workgroup, KiB per wave and
+round, skew, workgroups) shapes of the same kernel template, run through the test diagnostics library
+(tests/bin/libselfreduce_diag.so, mscclppAmdSelfReduceLL16Shape).  Per-launch time from 20 launches
+captured in one HIP graph (device time, no host launch cost), interleaved rounds in one process;
+every shape is checked bit-exactly first.  With COUNT=1 also the first-poll misses per launch.
+
+    python tools/sweep_self_reduce.py            -> gpurun_out/sweep_self_reduce.json
+"""
 import ctypes
 import json
 import os
@@ -10,85 +15,123 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 import mscclpp_amd as m  # noqa: E402
 
-L = m.lib()
 vp = ctypes.c_void_p
-
-S = int(os.environ.get("BYTES", 48 << 20))
-n = S // 2
+D = ctypes.CDLL(os.path.join(ROOT, "tests", "bin", "libselfreduce_diag.so"))
+D.mscclppAmdSelfReduceLL16Shape.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, vp, vp, vp]
 dev = torch.device("cuda", 0)
-x = torch.rand(n, device=dev).half()
-y = torch.rand(n, device=dev).half()
+torch.cuda.set_device(dev)
+SMAX = 48 << 20
+x = torch.rand(SMAX // 2, device=dev).half()
+y = torch.rand(SMAX // 2, device=dev).half()
 out = torch.empty_like(x)
 flags = torch.ones(m.FLAG_SLOTS, dtype=torch.int32, device=dev)
 err = torch.zeros(16, dtype=torch.int32, device=dev)
 miss = torch.zeros(4, dtype=torch.int32, device=dev)
-pk = m.DeviceBuffer(2 * S, uncached=True)
+pk = m.DeviceBuffer(2 * SMAX)
 ref = (x.float() + y.float()).clamp(-65504, 65504).half()
-s = m.stream_ptr()
 
 
-def run(variant, nb):
-    rc = L.mscclppAmdSelfReduceLL16Variant(vp(x.data_ptr()), vp(y.data_ptr()), vp(pk.ptr), vp(out.data_ptr()), S,
-                                           vp(flags.data_ptr()), nb, variant, 500_000_000, vp(err.data_ptr()),
-                                           vp(miss.data_ptr()), s)
-    assert rc == 0
+def shape_fn(S, w, u, sk, nb, count=0):
+    def f():
+        rc = D.mscclppAmdSelfReduceLL16Shape(vp(x.data_ptr()), vp(y.data_ptr()), vp(pk.ptr), vp(out.data_ptr()), S,
+                                             vp(flags.data_ptr()), nb, w, u, sk, count, 500_000_000,
+                                             vp(err.data_ptr()), vp(miss.data_ptr()), m.stream_ptr())
+        assert rc == 0, rc
+    return f
 
 
-def batch(fn, reps=10):
+def product_fn(S):
+    xs, ys, os_ = x[: S // 2], y[: S // 2], out[: S // 2]
+    return lambda: m.self_reduce_ll16(xs, ys, pk.ptr, os_, flags, err)
+
+
+def graph_us(fn, calls=20, replays=10):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(calls):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(reps):
-        fn()
+    for _ in range(replays):
+        g.replay()
     b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) * 1e3 / reps
+    return a.elapsed_time(b) * 1e3 / (replays * calls)
 
 
-variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3").split(",")]
-grids = [int(g) for g in os.environ.get("GRIDS", "512,1024").split(",")]
-configs = [(v, nb) for v in variants for nb in grids]
-for v, nb in configs:  # correctness of every config once
-    out.zero_()
-    run(v, nb)
-    torch.cuda.synchronize()
-    if int(err[0].item()) != 0 or not torch.equal(out, ref):
-        print("FAILED", v, nb, int(err[0].item()))
-        err.zero_()
-# first-poll misses per launch (packets; each miss re-reads a 16-byte packet at least once)
-misses = {}
-for v, name in ((4, "skewed"), (5, "unskewed")):
-    vals = []
-    for _ in range(5):
-        miss.zero_()
-        run(v, 1024)
+def default_shape(S):
+    w, u, nb, sk = (ctypes.c_int() for _ in range(4))
+    m.check(m.lib().mscclppAmdSelfReduceLL16DefaultShape(S, ctypes.byref(w), ctypes.byref(u), ctypes.byref(nb),
+                                                         ctypes.byref(sk)), "default shape")
+    return w.value, u.value, sk.value, nb.value
+
+
+def candidates(S):
+    """(waves, KiB per wave, skew, workgroups): one round (a workgroup per tile) and two rounds for
+    buckets that fit, and 512 / 1024 / 2048 workgroups with the skew from three rounds on."""
+    c = []
+    for w, u in ((1, 1), (2, 1), (2, 2), (4, 1), (4, 2), (8, 1), (8, 2)):
+        tile = w * u * 1024
+        tiles = -(-S // tile)
+        cap = 1024 * 4 // w  # at most 16 waves per CU
+        for nb in sorted({tiles, -(-tiles // 2)} | {g for g in (512, 1024, 2048) if g < tiles}):
+            if nb < 2 or nb > cap:
+                continue
+            rounds = -(-tiles // nb)
+            c.append((w, u, 1 if rounds >= 3 else 0, nb))
+    return sorted(set(c))
+
+
+sizes = [int(v) for v in os.environ.get("SIZES", ",".join(str((64 << 10) << k) for k in range(7))).split(",")] + \
+    ([48 << 20] if not os.environ.get("SIZES") else [])
+res = {}
+for S in sizes:
+    cands = candidates(S)
+    ok = {}
+    for cnd in cands:
+        out.zero_()
+        shape_fn(S, *cnd)()
         torch.cuda.synchronize()
-        vals.append(int(miss[0].item()))
-    misses[name] = {"packets_per_launch_median": int(np.median(vals)),
-                    "bytes_per_launch_median": int(np.median(vals)) * 16, "of_packets": S // 8}
-res = {c: [] for c in configs}
-cp_src = torch.empty(S, dtype=torch.uint8, device=dev)
-cp_dst = torch.empty(S, dtype=torch.uint8, device=dev)
-copy_t = {nb: [] for nb in (1024, 2048, 4096)}
-for rnd in range(5):
-    for v, nb in configs:
-        res[(v, nb)].append(batch(lambda: run(v, nb), 10))
-    for nb in copy_t:
-        copy_t[nb].append(batch(lambda: L.mscclppAmdCopy(vp(cp_src.data_ptr()), vp(cp_dst.data_ptr()), S, nb, s), 10))
-rows = []
-for (v, nb), t in res.items():
-    med = float(np.median(t))
-    rows.append({"variant": v, "nblocks": nb, "us_med": round(med, 2), "us_min": round(min(t), 2),
-                 "TBps_7S": round(7 * S / med / 1e6, 3)})
-rows.sort(key=lambda r: r["us_med"])
-cp = {nb: {"us_med": round(float(np.median(t)), 2), "TBps_2S": round(2 * S / float(np.median(t)) / 1e6, 3)}
-      for nb, t in copy_t.items()}
-os.makedirs(os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out"), exist_ok=True)
-out_path = os.path.join(os.environ.get("GRAFT_REPO_ROOT", "."), "gpurun_out", "sweep_self_reduce.json")
-json.dump({"rows": rows, "copy": cp, "first_poll_misses": misses}, open(out_path, "w"), indent=1)
-for r in rows:
-    print(r)
-print("copy", cp)
-print("misses", misses)
+        ok[cnd] = int(err[0].item()) == 0 and torch.equal(out[: S // 2], ref[: S // 2])
+        err.zero_()
+    out.zero_()
+    product_fn(S)()
+    torch.cuda.synchronize()
+    prod_ok = torch.equal(out[: S // 2], ref[: S // 2])
+    times = {cnd: [] for cnd in cands}
+    prod = []
+    for _ in range(3):
+        prod.append(graph_us(product_fn(S)))
+        for cnd in cands:
+            times[cnd].append(graph_us(shape_fn(S, *cnd)))
+    row = {"default_shape": "w%d u%d skew%d x%d" % default_shape(S), "product_us": round(float(np.median(prod)), 2),
+           "product_correct": bool(prod_ok),
+           "shapes_us": {"w%d u%d skew%d x%d" % c: round(float(np.median(t)), 2) for c, t in times.items()},
+           "shapes_correct": all(ok.values())}
+    best = min(times, key=lambda c: np.median(times[c]))
+    row["best"] = "w%d u%d skew%d x%d" % best
+    row["best_us"] = round(float(np.median(times[best])), 2)
+    if os.environ.get("COUNT"):
+        d = default_shape(S)
+        miss.zero_()
+        shape_fn(S, d[0], d[1], d[2], d[3], 1)()
+        torch.cuda.synchronize()
+        row["first_poll_misses_default"] = int(miss[0].item())
+    res[f"{S >> 10}KiB"] = row
+    print(json.dumps({f"{S >> 10}KiB": {k: row[k] for k in ("default_shape", "product_us", "best", "best_us",
+                                                             "product_correct", "shapes_correct")}}), flush=True)
+res["empty_kernel_graph_us"] = round(graph_us(lambda: torch.cuda._sleep(0)), 2)
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+json.dump(res, open(os.path.join(ROOT, "gpurun_out", "sweep_self_reduce.json"), "w"), indent=1)
