@@ -1064,19 +1064,22 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         del x, rs, ag
     except Exception as e:
         extras["reduce_scatter_allgather_error"] = str(e)[-300:]
-    progress("extras: fp32 1 GiB rsag")
+    progress("extras: fp32 1 GiB ring-order RS+AG")
     try:
+        # BASELINE configs[4]: both ring-order kernels (the same order-stable sum, own then r+1, ...):
+        # through the 128 MiB bulk scratch in several passes (rsag) and zero-copy (rsag_zc)
         S = 1 << 30
         xs = torch.rand(S // 4, device=dev)
         os_ = torch.empty_like(xs)
-        for _ in range(2):
-            comm.all_reduce(xs, os_, algo="rsag")
-        t = tmax(_time_calls(lambda: comm.all_reduce(xs, os_, algo="rsag"), 5))
-        extras["fp32_1GiB_rsag"] = {"ms": round(t * 1e3, 3), "algbw_GBs": round(S / t / 1e9, 2),
-                                    "busbw_GBs": round(S / t / 1e9 * 2 * (n - 1) / n, 2)}
+        for a in ("rsag", "rsag_zc"):
+            for _ in range(2):
+                comm.all_reduce(xs, os_, algo=a)
+            t = tmax(_time_calls(lambda: comm.all_reduce(xs, os_, algo=a), 5))
+            extras[f"fp32_1GiB_{a}"] = {"ms": round(t * 1e3, 3), "algbw_GBs": round(S / t / 1e9, 2),
+                                        "busbw_GBs": round(S / t / 1e9 * 2 * (n - 1) / n, 2)}
         del xs, os_
     except Exception as e:
-        extras["fp32_1GiB_rsag_error"] = str(e)
+        extras["fp32_1GiB_error"] = str(e)
     progress("extras: graph-captured LL latency sweep")
     try:
         glat = {}
