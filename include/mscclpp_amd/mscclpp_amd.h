@@ -101,9 +101,9 @@ int mscclppAmdFlagsInit(uint32_t* flags, void* stream);
 
 /* ---- 1-GPU microbench (BASELINE config 2) ------------------------------------------------- */
 /* out = x (op) unpack(pack(y, flag)); pkts: 2*bytes of (uncached) device memory; bytes % 16 == 0.
- * nblocks <= 0 selects the default shape (up to 4 MiB: one 256-lane workgroup per 4 KiB, one round;
- * larger: 256-lane workgroups with 8 KiB per round, up to 1024 of them); nblocks > 0 runs the large
- * form on that grid (<= 1024).  budgetTicks: spin budget in 10 ns ticks. */
+ * 256-lane workgroups with 4 KiB per round; nblocks <= 0 selects the default grid (one workgroup per
+ * 4 KiB up to 1024 of them), nblocks > 0 that grid (<= 1024).  budgetTicks: spin budget in 10 ns
+ * ticks. */
 int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts, void* out, size_t bytes, int dtype, int op,
                              uint32_t* flags, int nblocks, uint64_t budgetTicks, uint32_t* err, void* stream);
 /* The default shape for `bytes`: waves per workgroup, KiB per wave and round, workgroups, skewed. */

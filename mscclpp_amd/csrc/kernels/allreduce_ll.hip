@@ -152,12 +152,9 @@ __device__ __forceinline__ void payload_st(__amdgpu_buffer_rsrc_t r, uint8_t* ba
     if ((uint32_t)i < valid) base[off + i] = (uint8_t)((i < 4 ? v.x : v.y) >> ((i % 4) * 8));
 }
 
-constexpr int kUnroll = 4;  // units per lane handled together in the multi-pass loops
-
 // V (0 in the product): bits that switch a part back to its round-2 form, for same-process A/B
-// timing through the diagnostics build (MSCCLPP_AMD_DIAG): 1 = step 1 one unit per pass, 2 = step 3
-// one unit per pass, 4 = polls tested as issued and every peer re-read after a miss, 8 = a scalar
-// flag load ahead of everything else.
+// timing through the diagnostics build (MSCCLPP_AMD_DIAG): 4 = polls tested as issued and every peer
+// re-read after a miss, 8 = a scalar flag load ahead of everything else.
 template <int DT, int OP, int NV, int V = 0>
 __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16Geom g, int nranks, uint64_t budget) {
   const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
@@ -202,36 +199,10 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
   // step 1: put my copy of slice `remote` into rank `remote`'s scratch at rank*ppr packets (:89-90)
   if (inPeerGroup) {
     const auto rdst = make_rsrc((uint8_t*)v.peerScratch[remote] + base + (uint64_t)rank * g.ppr * 16);
-    const uint32_t stride = bpp * T;
-    if (j1 < npk) unit_put<kSystem>(rdst, j1 * 16u, w1, flag, false);
-    // further passes kUnroll units per lane at a time: every payload load issued before any put, so
-    // the passes overlap instead of paying one load round trip each.  A lane whose unit is not a
-    // whole 8 bytes inside the buffer loads the slice's first unit instead (ignored) and takes the
-    // byte-wise path at its put.
-    auto whole = [&](uint64_t off) { return off + 8 <= send1; };
-    if constexpr ((V & 1) != 0) {
-      for (uint32_t j = j1 + stride; j < npk; j += stride) {
-        const uint64_t off = soff1 + (uint64_t)j * 8;
-        unit_put<kSystem>(rdst, j * 16u, payload_ld(rin, in, off, clamp_valid(send1, off, 8)), flag, false);
-      }
-    } else
-    for (uint32_t j0 = j1 + stride; j0 < npk; j0 += kUnroll * stride) {
-      u32x2 w[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t j = j0 + (uint32_t)u * stride;
-        const uint64_t off = soff1 + (uint64_t)j * 8;
-        w[u] = load8<kPlain>(rin, (uint32_t)(j < npk && whole(off) ? off : soff1));
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t j = j0 + (uint32_t)u * stride;
-        if (j < npk) {
-          const uint64_t off = soff1 + (uint64_t)j * 8;
-          const u32x2 x = whole(off) ? w[u] : payload_ld(rin, in, off, clamp_valid(send1, off, 8));
-          unit_put<kSystem>(rdst, j * 16u, x, flag, false);
-        }
-      }
+    for (uint32_t j = j1; j < npk; j += bpp * T) {
+      const uint64_t off = soff1 + (uint64_t)j * 8;
+      const u32x2 w = j == j1 ? w1 : payload_ld(rin, in, off, clamp_valid(send1, off, 8));
+      unit_put<kSystem>(rdst, j * 16u, w, flag, false);
     }
   }
 
@@ -294,31 +265,13 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
     const auto rres = make_rsrc(scr + g.roff + (uint64_t)remote * g.ppr * 16);
     const uint64_t soff = (uint64_t)remote * sliceBytes;
     const uint64_t send = sliceEnd(remote);
-    const uint32_t stride = bpp * T;
-    // kUnroll units per lane at a time: all their polls issued before any is looked at
-    if constexpr ((V & 2) != 0) {
-      for (uint32_t j = lb * T + tid; j < npk; j += stride) {
-        const uint64_t off = soff + (uint64_t)j * 8;
-        payload_st(rout, out, off, unit_get(rres, j * 16u, flag, false, budget, v.err), clamp_valid(send, off, 8));
-      }
-    } else
-    for (uint32_t j0 = lb * T + tid; j0 < npk; j0 += kUnroll * stride) {
-      u32x4 raw[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t j = j0 + (uint32_t)u * stride;
-        raw[u] = load16<kSystem>(rres, (j < npk ? j : j0) * 16u);
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t j = j0 + (uint32_t)u * stride;
-        if (j < npk) {
-          const uint64_t off = soff + (uint64_t)j * 8;
-          u32x2 w{raw[u].x, raw[u].z};
-          if (raw[u].y != flag || raw[u].w != flag) w = unit_wait(rres, j * 16u, flag, false, budget, v.err);
-          payload_st(rout, out, off, w, clamp_valid(send, off, 8));
-        }
-      }
+    // one unit per lane and pass, polled and then waited for: issuing a lane's later passes' polls
+    // together with its first (all reading lines that had not landed yet) measured slower at every
+    // size in the same-process A/B (tools/ll_variants_ab.py, profiles/r3_ll_variants_ab.json)
+    for (uint32_t j = lb * T + tid; j < npk; j += bpp * T) {
+      const uint64_t off = soff + (uint64_t)j * 8;
+      const u32x2 w = unit_get(rres, j * 16u, flag, false, budget, v.err);
+      payload_st(rout, out, off, w, clamp_valid(send, off, 8));
     }
   }
   trace_stamp(g.trace, 3);
@@ -626,7 +579,7 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
 #ifdef MSCCLPP_AMD_DIAG
 // Same-process A/B timing of the LL kernels' variants (fp16 SUM; the diagnostics library
 // tests/bin/libll_diag.so only): algo MSCCLPP_AMD_ALGO_PACKET / _ALLPAIR, variant bits as V above
-// (0, 1, 2, 3, 4, 7, 8, 15), views of nviews in-process ranks (or one), default launch shape for 0.
+// (0, 4, 8, 12), views of nviews in-process ranks, default launch shape for nblocks = nthreads = 0.
 uint64_t* g_mscclppAmdTrace = nullptr;
 using namespace mscclpp_amd;
 extern "C" int mscclppAmdDiagAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int nranks,
@@ -644,7 +597,7 @@ extern "C" int mscclppAmdDiagAllReduceLL(int algo, const mscclppAmdRankView* vie
     g.hbOdd = views[0].scratchBytes / 2;
     g.hbEven = 0;
 #define LV(VV) if (variant == VV) launchLL16T<kF16, kSum, kMaxRanks, VV>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
-    LV(0) LV(1) LV(2) LV(3) LV(4) LV(7) LV(8) LV(15)
+    LV(0) LV(4) LV(8) LV(12)
 #undef LV
   } else if (algo == MSCCLPP_AMD_ALGO_ALLPAIR) {
     ll8Defaults(nranks, bytes, nblocks, nthreads);

@@ -37,7 +37,10 @@ namespace mscclpp_amd {
 // The flag is read by a vector load issued with the first payload loads, so its latency overlaps
 // theirs instead of preceding them (a scalar flag load made the kernel wait for it before issuing
 // anything else).
-template <int DT, int OP, int W, int U, bool SKEW, bool COUNT>
+// LP: cache policy of the X / Y payload loads and the output stores (nt for streaming buckets; the
+// one-round small form reads with the default policy, so a bucket written or read just before --
+// an AllReduce's input straight from its producer kernel -- is served from the caches).
+template <int DT, int OP, int W, int U, bool SKEW, bool COUNT, int LP = kNonTemporal>
 __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t* __restrict__ x,
                                                                   const uint8_t* __restrict__ y, uint8_t* pkts,
                                                                   uint8_t* __restrict__ out, uint64_t bytes,
@@ -59,7 +62,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint64_t c = chunk(t, k);
-      if (c + lane * 16 < bytes) yw[k] = load16<kNonTemporal>(make_rsrc(y + c), lane * 16);
+      if (c + lane * 16 < bytes) yw[k] = load16<LP>(make_rsrc(y + c), lane * 16);
     }
   };
   u32x4 a[U];
@@ -67,7 +70,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       const uint64_t c = chunk(tp, k);
-      if (c + lane * 16 < bytes) a[k] = load16<kNonTemporal>(make_rsrc(x + c), lane * 16);
+      if (c + lane * 16 < bytes) a[k] = load16<LP>(make_rsrc(x + c), lane * 16);
     }
   };
   const uint32_t flagv = __hip_atomic_load(flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -156,7 +159,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
       for (int k = 0; k < U; ++k) {
         const uint64_t c = chunk(tp, k);
         const u32x4 p = *(const u32x4*)&ldsC[wave][k][lane * 16];
-        if (c + lane * 16 < bytes) store16<kNonTemporal>(make_rsrc(out + c), lane * 16, reduce4<DT, OP>(a[k], p));
+        if (c + lane * 16 < bytes) store16<LP>(make_rsrc(out + c), lane * 16, reduce4<DT, OP>(a[k], p));
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -164,42 +167,38 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
   bump_flags(flags, flag);
 }
 
-// Launch shape of the product kernel for `bytes` (nblocks > 0: the caller's grid for the large form),
-// from the shape sweep (tools/sweep_self_reduce.py, profiles/r3_sweep_self_reduce.json):
-//  * up to 4 MiB: 4 waves x 1 KiB per workgroup, one workgroup per 4 KiB tile (one round): 3.9 us at
-//    64-256 KiB against 4.6 us with one-wave workgroups per KiB and 5.0 us for the large form;
-//  * larger: 4 waves x 2 KiB per workgroup, up to 1024 workgroups (4 per CU, all resident);
-//    partner tiles consumed one round late from 3 rounds on (48 MiB: the skew cut the first-poll
-//    misses from 13.9 % to 0.8 % of the packets and the traffic to 1.004 x 7 S); with one or two
-//    rounds the skew's drain round would be an extra round, so the tile is consumed in its round.
+// Launch shape of the product kernel for `bytes` (nblocks > 0: the caller's grid), from the
+// same-process shape sweeps (tools/sweep_self_reduce.py, profiles/r3_sweep_self_reduce.json):
+// 4 waves x 1 KiB per workgroup and round, one workgroup per 4 KiB tile up to 1024 workgroups (4 per
+// CU, all resident, so every partner pair is co-resident).
+//  * one round (up to 4 MiB): payload read and written with the default cache policy (a bucket just
+//    written or read by the caller is served from the caches): 3.6-3.7 us at 64-256 KiB, against
+//    4.6 us with one-wave workgroups per KiB and 5.0 us for round 2's 8 KiB tiles;
+//  * two rounds: unskewed; three and more (48 MiB: 12) partner tiles consumed one round late, nt
+//    payload accesses: 53.0 us at 48 MiB against 54.1 us with round 2's 2 KiB per wave (the skew cut
+//    the first-poll misses from 13.9 % to 0.8 % of the packets and the traffic to 1.004 x 7 S).
 struct SelfReduceShape {
   int waves, units, nblocks;
   bool skew;
+  bool plain;  // default-policy payload accesses (one round)
 };
 static SelfReduceShape selfReduceShape(uint64_t bytes, int nblocks) {
   SelfReduceShape sh{};
-  const uint64_t tiles4k = (bytes + 4095) / 4096;
-  if (nblocks <= 0 && tiles4k <= 1024) {
-    sh.waves = 4;
-    sh.units = 1;
-    sh.nblocks = (int)tiles4k;
-  } else {
-    sh.waves = 4;
-    sh.units = 2;
-    const uint64_t tiles = (bytes + 8191) / 8192;
-    sh.nblocks = nblocks > 0 ? nblocks : (int)(tiles < 1024 ? tiles : 1024);
-  }
+  sh.waves = 4;
+  sh.units = 1;
+  const uint64_t tiles = (bytes + 4095) / 4096;
+  sh.nblocks = nblocks > 0 ? nblocks : (int)(tiles < 1024 ? tiles : 1024);
   if (sh.nblocks % 2) sh.nblocks += 1;
-  const uint64_t tile = (uint64_t)sh.waves * sh.units * 1024;
-  const uint64_t rounds = ((bytes + tile - 1) / tile + sh.nblocks - 1) / sh.nblocks;
+  const uint64_t rounds = (tiles + sh.nblocks - 1) / sh.nblocks;
   sh.skew = rounds >= 3;
+  sh.plain = rounds == 1;
   return sh;
 }
 
-template <int DT, int OP, int W, int U, bool SKEW, bool COUNT>
+template <int DT, int OP, int W, int U, bool SKEW, bool COUNT, int LP = kNonTemporal>
 static void launchSelfReduceShape(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                                   int nblocks, uint64_t budget, uint32_t* err, uint32_t* pollMiss, hipStream_t stream) {
-  hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, W, U, SKEW, COUNT>), dim3(nblocks), dim3(64 * W), 0, stream,
+  hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, W, U, SKEW, COUNT, LP>), dim3(nblocks), dim3(64 * W), 0, stream,
                      (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
                      pollMiss);
 }
@@ -208,14 +207,14 @@ template <int DT, int OP>
 static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                              int nblocks, uint64_t budget, uint32_t* err, hipStream_t stream) {
   const SelfReduceShape sh = selfReduceShape(bytes, nblocks);
-  if (sh.units == 1)
-    launchSelfReduceShape<DT, OP, 4, 1, false, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
-                                                      stream);
+  if (sh.plain)
+    launchSelfReduceShape<DT, OP, 4, 1, false, false, kPlain>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err,
+                                                              nullptr, stream);
   else if (sh.skew)
-    launchSelfReduceShape<DT, OP, 4, 2, true, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
+    launchSelfReduceShape<DT, OP, 4, 1, true, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
                                                      stream);
   else
-    launchSelfReduceShape<DT, OP, 4, 2, false, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
+    launchSelfReduceShape<DT, OP, 4, 1, false, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
                                                       stream);
 }
 
@@ -280,14 +279,21 @@ using namespace mscclpp_amd;
 extern "C" int mscclppAmdSelfReduceLL16Shape(const void* x, const void* y, void* pkts, void* out, size_t bytes,
                                              uint32_t* flags, int nblocks, int waves, int units, int skew, int count,
                                              uint64_t budgetTicks, uint32_t* err, uint32_t* pollMiss, void* streamPtr) {
+  // count == 2: no miss count, default-policy payload loads / stores (the small form's choice)
+  const bool plain = count == 2;
+  if (plain) count = 0;
   hipStream_t s = (hipStream_t)streamPtr;
   if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > 4096) return 4;
   if (count && !pollMiss) return 4;
   if (nblocks % 2) nblocks += 1;
 #define SRS(W, U, SK, C)                                                                                      \
   if (waves == W && units == U && (skew != 0) == SK && (count != 0) == C) {                                   \
-    launchSelfReduceShape<kF16, kSum, W, U, SK, C>(x, y, pkts, out, bytes, flags, nblocks, budgetTicks, err,  \
-                                                   pollMiss, s);                                             \
+    if (plain)                                                                                                \
+      launchSelfReduceShape<kF16, kSum, W, U, SK, C, kPlain>(x, y, pkts, out, bytes, flags, nblocks,          \
+                                                             budgetTicks, err, pollMiss, s);                 \
+    else                                                                                                      \
+      launchSelfReduceShape<kF16, kSum, W, U, SK, C>(x, y, pkts, out, bytes, flags, nblocks, budgetTicks, err, \
+                                                     pollMiss, s);                                           \
     return hipGetLastError() == hipSuccess ? 0 : 1;                                                           \
   }
 #define SRS_SK(W, U) SRS(W, U, true, false) SRS(W, U, false, false) SRS(W, U, true, true) SRS(W, U, false, true)

@@ -5,10 +5,10 @@
 * configs[2]: 8 ranks x 48 MiB fp16 (2048 x 12288) through the bulk fullmesh and zero-copy RS+AG
   kernels -- every rank's output bit-exact against the oracle in the reference's sum orders.
 * configs[3] upper end: 8 ranks x 1 MiB fp16 LL16 two-hop, output and scratch image bit-exact.
-* configs[4]: 8 ranks x 1 GiB fp32 RS+AG in ring order.  The oracle is too slow for 8 GiB of
-  inputs, so the check is size-independent: all eight outputs are identical (one launch wrote them
-  all), and 1 Mi sampled elements plus every slice boundary equal the ring-order fp32 sum
-  x_o + x_{o+1} + ... (o = the slice owner, allreduce_rsag.cu:85-94) computed in numpy, to 0 ulp.
+* configs[4]: 8 ranks x 1 GiB fp32 RS+AG in ring order (scratch-based and zero-copy): all eight
+  outputs identical, EVERY element equal to the ring-order fp32 sum x_o + x_{o+1} + ... (o = the slice
+  owner, allreduce_rsag.cu:85-94) computed by torch on the device in the same order, and 1 Mi sampled
+  elements plus every slice boundary equal the same sum computed in numpy -- 0 ulp.
 All ranks run in one process on one GPU (one launch, blockIdx.y = rank)."""
 import numpy as np
 import pytest
@@ -94,7 +94,12 @@ def test_ll16_8x1MiB_fp16_bit_exact(built):
                 assert np.array_equal(ranks.scratch_tensor(r, sb).cpu().numpy().view(np.uint32), scr[r])
 
 
-def test_rsag_ring_8x1GiB_fp32(built):
+@pytest.mark.parametrize("algo", ["rsag", "rsag_zc"])
+def test_rsag_ring_8x1GiB_fp32(built, algo):
+    """Every one of the 8 x 268 M outputs equals the ring-order fp32 sum x_o + x_{o+1} + ... (o = the
+    slice owner, allreduce_rsag.cu:85-94; allreduce_rsag_zero_copy.cu:88-98) computed elementwise by
+    torch on the device in the same order (IEEE fp32 adds: 0 ulp), and 1 Mi sampled elements plus
+    every slice boundary equal the same sum computed on the CPU in numpy."""
     import mscclpp_amd as m
 
     n, nbytes = 8, 1 << 30
@@ -103,18 +108,27 @@ def test_rsag_ring_8x1GiB_fp32(built):
     free, _ = torch.cuda.mem_get_info()
     if free < 28 << 30:
         pytest.skip("needs ~26 GiB of device memory")
-    ranks = m.InProcessRanks(n, 1 << 16, bulk_scratch_bytes=nbytes)
+    ranks = m.InProcessRanks(n, 1 << 16, bulk_scratch_bytes=nbytes if algo == "rsag" else 0)
     g = torch.Generator(device="cuda")
     ins = []
     for r in range(n):
         g.manual_seed(1000 + r)
         ins.append(torch.rand(count, generator=g, device="cuda") * 2 - 1)
     outs = [torch.empty_like(t) for t in ins]
-    ranks.all_reduce(ins, outs, m.ALGO_RSAG, nblocks=32, nthreads=512)
+    ranks.all_reduce(ins, outs, m.ALGO_NAMES[algo], nblocks=32, nthreads=512)
     torch.cuda.synchronize()
     assert ranks.errors() == [0] * n
     for r in range(1, n):
-        assert torch.equal(outs[r], outs[0]), f"rank {r} differs from rank 0"
+        assert torch.equal(outs[r].view(torch.int32), outs[0].view(torch.int32)), f"rank {r} differs from rank 0"
+    bad = 0
+    for o in range(n):  # every element, in the owner's ring order
+        sl = slice(o * slice_elems, (o + 1) * slice_elems if o < n - 1 else count)
+        acc = ins[o][sl].clone()
+        for k in range(1, n):
+            acc += ins[(o + k) % n][sl]
+        bad += int((acc.view(torch.int32) != outs[0][sl].view(torch.int32)).sum().item())
+        del acc
+    assert bad == 0, f"{bad} of {count} elements differ from the ring-order sum"
     rng = np.random.default_rng(5)
     idx = np.concatenate([rng.integers(0, count, 1 << 20),
                           np.array([k * slice_elems + d for k in range(n) for d in (0, 1, slice_elems - 1)])])

@@ -55,9 +55,9 @@ def _assert_equal_words(got, exp, dt):
     (16, True), (1040, False), ((7 << 10) + 48, True),   # 1 KiB per wave, one round, ragged tails
     (64 << 10, True), ((1 << 20) + 48, False),
     (4 << 20, True),                                     # the largest one-round grid: 1024 workgroups
-    ((4 << 20) + 16, False),                             # 2 KiB per wave, one round
-    ((12 << 20) + 16, False),                            # two rounds per workgroup: unskewed form
-    ((24 << 20) + 16, True)])                            # three rounds and more: partner tiles one round late
+    ((4 << 20) + 16, False),                             # two rounds
+    ((8 << 20) + 16, False),                             # three rounds and more: partner tiles one round late
+    ((24 << 20) + 16, True)])
 def test_self_reduce_bit_exact(built, dt, op, nbytes, special):
     import mscclpp_amd as m
 
@@ -91,11 +91,11 @@ def test_self_reduce_rejects_unaligned(built):
     assert e.value.code == 4
 
 
-@pytest.mark.parametrize("nbytes,units,skew", [(16, 1, 0), (4 << 20, 1, 0), ((4 << 20) + 16, 2, 0),
-                                               ((12 << 20) + 16, 2, 0), ((24 << 20) + 16, 2, 1)])
-def test_self_reduce_default_shape(built, nbytes, units, skew):
-    """The launch shape the product entry picks (1 KiB per wave up to 4 MiB, the skew from three
-    rounds per workgroup on)."""
+@pytest.mark.parametrize("nbytes,nblocks,skew", [(16, 2, 0), (4 << 20, 1024, 0), ((4 << 20) + 16, 1024, 0),
+                                                 ((8 << 20) + 16, 1024, 1), ((24 << 20) + 16, 1024, 1)])
+def test_self_reduce_default_shape(built, nbytes, nblocks, skew):
+    """The launch shape the product entry picks (4 waves x 1 KiB, one workgroup per 4 KiB up to 1024,
+    the skew from three rounds per workgroup on)."""
     import ctypes
 
     import mscclpp_amd as m
@@ -103,5 +103,5 @@ def test_self_reduce_default_shape(built, nbytes, units, skew):
     w, u, nb, sk = (ctypes.c_int() for _ in range(4))
     m.check(m.lib().mscclppAmdSelfReduceLL16DefaultShape(nbytes, ctypes.byref(w), ctypes.byref(u), ctypes.byref(nb),
                                                          ctypes.byref(sk)), "default shape")
-    assert (w.value, u.value, sk.value) == (4, units, skew) and nb.value % 2 == 0 and nb.value <= 1024
+    assert (w.value, u.value, nb.value, sk.value) == (4, 1, nblocks, skew)
 

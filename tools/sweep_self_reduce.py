@@ -91,10 +91,16 @@ def candidates(S):
                 continue
             rounds = -(-tiles // nb)
             c.append((w, u, 1 if rounds >= 3 else 0, nb))
+            if rounds == 1 and w == 4:  # the one-round form with default-policy payload accesses
+                c.append((w, u, 0, nb, 2))
     return sorted(set(c))
 
 
-sizes = [int(v) for v in os.environ.get("SIZES", ",".join(str((64 << 10) << k) for k in range(7))).split(",")] + \
+def name(c):
+    return "w%d u%d skew%d x%d" % c[:4] + (" plain" if len(c) > 4 else "")
+
+
+sizes = [int(v) for v in os.environ.get("SIZES", ",".join(str((64 << 10) << k) for k in range(10))).split(",")] + \
     ([48 << 20] if not os.environ.get("SIZES") else [])
 res = {}
 for S in sizes:
@@ -118,10 +124,10 @@ for S in sizes:
             times[cnd].append(graph_us(shape_fn(S, *cnd)))
     row = {"default_shape": "w%d u%d skew%d x%d" % default_shape(S), "product_us": round(float(np.median(prod)), 2),
            "product_correct": bool(prod_ok),
-           "shapes_us": {"w%d u%d skew%d x%d" % c: round(float(np.median(t)), 2) for c, t in times.items()},
+           "shapes_us": {name(c): round(float(np.median(t)), 2) for c, t in times.items()},
            "shapes_correct": all(ok.values())}
     best = min(times, key=lambda c: np.median(times[c]))
-    row["best"] = "w%d u%d skew%d x%d" % best
+    row["best"] = name(best)
     row["best_us"] = round(float(np.median(times[best])), 2)
     if os.environ.get("COUNT"):
         d = default_shape(S)
