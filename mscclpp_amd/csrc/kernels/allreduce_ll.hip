@@ -154,7 +154,12 @@ __device__ __forceinline__ void payload_st(__amdgpu_buffer_rsrc_t r, uint8_t* ba
 
 // V (0 in the product): bits that switch a part back to its round-2 form, for same-process A/B
 // timing through the diagnostics build (MSCCLPP_AMD_DIAG): 4 = polls tested as issued and every peer
-// re-read after a miss, 8 = a scalar flag load ahead of everything else.
+// re-read after a miss, 8 = a scalar flag load ahead of everything else, 16 = every slice size polls
+// all peers at once.
+// Step 2 issues all of a unit's peer polls at once while a slice has at most kBatchedPollUnits units
+// (LL16 buckets up to 512 KiB at 8 ranks: one memory round trip instead of one per peer, 1.0-1.5 us
+// at 1-512 KiB in the A/B), and polls peer by peer beyond.
+constexpr uint32_t kBatchedPollUnits = 8192;
 template <int DT, int OP, int NV, int V = 0>
 __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16Geom g, int nranks, uint64_t budget) {
   const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
@@ -231,6 +236,15 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
         for (int p = 0; p < kMaxRanks; ++p)
           if (p < nranks && p != rank) ready &= unit_try(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, w[p], false);
         if (!ready) missing = peers;  // round 2: every peer read again
+      } else if (npk > kBatchedPollUnits && (V & 16) == 0) {
+        // large slices: one peer at a time, so later peers' packets have had longer to land (fewer
+        // first-poll misses under load; 1 MiB: measured faster than all polls at once); a peer whose
+        // packet had not landed is polled again below, the others are not re-read
+        own = payload_ld(rin, in, off, valid);
+#pragma unroll
+        for (int p = 0; p < kMaxRanks; ++p)
+          if (((peers >> p) & 1u) && !unit_try(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, w[p], false))
+            missing |= 1u << p;
       } else {
         u32x4 raw[kMaxRanks];
         poll_issue(scr, (uint32_t)(g.ppr * 16), j * 16u, peers, raw);
@@ -597,7 +611,7 @@ extern "C" int mscclppAmdDiagAllReduceLL(int algo, const mscclppAmdRankView* vie
     g.hbOdd = views[0].scratchBytes / 2;
     g.hbEven = 0;
 #define LV(VV) if (variant == VV) launchLL16T<kF16, kSum, kMaxRanks, VV>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
-    LV(0) LV(4) LV(8) LV(12)
+    LV(0) LV(4) LV(8) LV(12) LV(16)
 #undef LV
   } else if (algo == MSCCLPP_AMD_ALGO_ALLPAIR) {
     ll8Defaults(nranks, bytes, nblocks, nthreads);

@@ -2,7 +2,8 @@
 mscclppAmdDiagAllReduceLL): 8 ranks in one launch on one GPU, fp16 SUM, default launch shapes, per-call
 time from 20 calls in one HIP graph, variants interleaved over 5 rounds (box-to-box spread is larger
 than the differences measured).  Variant bits switch a part back to its round-2 form: 4 = polls
-tested as issued and every peer re-read after a miss, 8 = scalar flag load first.  (Bits 1 and 2, a
+tested as issued and every peer re-read after a miss, 8 = scalar flag load first, 16 = LL16 polls
+all peers at once at every slice size (the product does up to 8192 units per slice).  (Bits 1 and 2, a
 batched step 1 / step 3 of LL16, measured slower and were removed; profiles/r3_ll_variants_ab.json
 keeps that run.)  Every variant's output is checked against variant 0's.
 
@@ -27,7 +28,7 @@ D.mscclppAmdDiagAllReduceLL.argtypes = [ctypes.c_int, vp, ctypes.c_int, ctypes.c
 N = 8
 torch.cuda.set_device(0)
 CASES = [("allpair", kb, (0, 4, 8, 12)) for kb in (1, 4, 16)] + \
-        [("packet", kb, (0, 4, 8, 12)) for kb in (1, 16, 128, 256, 512, 1024)]
+        [("packet", kb, (0, 4, 16)) for kb in (1, 16, 128, 256, 512, 1024)]
 
 
 def graph_us(fn, calls=20, replays=10):

@@ -21,7 +21,7 @@ N, MiB = 8, 1 << 20
 KERNELS = {
     "allreduceZeroCopyKernel<0, 0, 8>": ("rsag_zc 32x512, 8 ranks x 48 MiB", 8 * 48 * MiB, 8 * 48 * MiB),
     "allreduceBulkKernel<0, 0, 8, 0, 0>": ("fullmesh 32x512, 8 ranks x 48 MiB", 15 * 48 * MiB, 15 * 48 * MiB),
-    "allreduceLL16Kernel<0, 0, 8>": ("packet default shape, 8 ranks x 1 MiB", 36 * MiB, 36 * MiB),
+    "allreduceLL16Kernel<0, 0, 8, 0>": ("packet default shape, 8 ranks x 1 MiB", 36 * MiB, 36 * MiB),
 }
 
 
