@@ -664,6 +664,8 @@ def bench_multi(args):
         "data": "synthetic (LCG of test/torch/correctness_test.py, seq alternating per step)",
         "config": {"workload": f"allreduce_fp16_{S >> 20}MiB (BASELINE configs[2]: 2048x12288 fp16 bucket per rank)",
                    "bytes": S, "parallelism": f"allreduce{world}", "algo": algo, "nblocks": nb, "nthreads": nt},
+        # ranks sharing fewer GPUs than ranks (a 1-GPU box): every number below is HBM, not xGMI
+        "rehearsal": ndev < world,
         "scaling_note": SCALING_NOTE,
         "busbw": round(algbw * 2 * (n - 1) / n, 2),
         # the bytes all ranks contributed per AllReduce (n buckets of S) over the step time, beside
