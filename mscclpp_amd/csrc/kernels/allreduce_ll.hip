@@ -116,6 +116,14 @@ __device__ __forceinline__ uint32_t poll_units(const uint8_t* base, uint32_t str
   poll_issue(base, stride, pbyte, peers, raw);
   return poll_eval(raw, flag, peers, w);
 }
+// Diagnostics build only (variant bit 32): add n, summed over the wave, to *ctr (first-poll misses).
+template <int V>
+__device__ __forceinline__ void count_misses(uint32_t* ctr, uint32_t n) {
+  if constexpr ((V & 32) != 0) {
+    for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off, 64);
+    if ((threadIdx.x & 63) == 0 && n) __hip_atomic_fetch_add(ctr, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 // A unit whose first poll missed: spin until it lands (the caller keeps the values of the units
 // that were ready, so only the missing ones are read again).
 __device__ __forceinline__ u32x2 unit_wait(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, bool single,
@@ -155,7 +163,7 @@ __device__ __forceinline__ void payload_st(__amdgpu_buffer_rsrc_t r, uint8_t* ba
 // V (0 in the product): bits that switch a part back to its round-2 form, for same-process A/B
 // timing through the diagnostics build (MSCCLPP_AMD_DIAG): 4 = polls tested as issued and every peer
 // re-read after a miss, 8 = a scalar flag load ahead of everything else, 16 = every slice size polls
-// all peers at once.
+// all peers at once, 32 = count first-poll misses into err[8] (step 2 / LL8) and err[9] (step 3).
 // Step 2 issues all of a unit's peer polls at once while a slice has at most kBatchedPollUnits units
 // (LL16 buckets up to 512 KiB at 8 ranks: one memory round trip instead of one per peer, 1.0-1.5 us
 // at 1-512 KiB in the A/B), and polls peer by peer beyond.
@@ -252,6 +260,7 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
         missing = poll_eval(raw, flag, peers, w);
       }
       Accum<DT, OP, 2> sum(own);  // upcastVector (:98-99)
+      count_misses<V>(v.err + 8, (uint32_t)__builtin_popcount(missing));
       if (missing) {
 #pragma unroll
         for (int p = 0; p < kMaxRanks; ++p)
@@ -284,7 +293,10 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
     // size in the same-process A/B (tools/ll_variants_ab.py, profiles/r3_ll_variants_ab.json)
     for (uint32_t j = lb * T + tid; j < npk; j += bpp * T) {
       const uint64_t off = soff + (uint64_t)j * 8;
-      const u32x2 w = unit_get(rres, j * 16u, flag, false, budget, v.err);
+      u32x2 w;
+      const bool landed = unit_try(rres, j * 16u, flag, w, false);
+      count_misses<V>(v.err + 9, landed ? 0u : 1u);
+      if (!landed) w = unit_wait(rres, j * 16u, flag, false, budget, v.err);
       payload_st(rout, out, off, w, clamp_valid(send, off, 8));
     }
   }
@@ -363,6 +375,7 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
         if (((peers >> p) & 1u) && !unit_try(rscr, (uint32_t)(p * region) + j * 16u, flag, w[p], single))
           missing |= 1u << p;
     }
+    count_misses<V>(v.err + 8, (uint32_t)__builtin_popcount(missing));
     if (missing) {
 #pragma unroll
       for (int p = 0; p < kMaxRanks; ++p)
@@ -611,14 +624,14 @@ extern "C" int mscclppAmdDiagAllReduceLL(int algo, const mscclppAmdRankView* vie
     g.hbOdd = views[0].scratchBytes / 2;
     g.hbEven = 0;
 #define LV(VV) if (variant == VV) launchLL16T<kF16, kSum, kMaxRanks, VV>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
-    LV(0) LV(4) LV(8) LV(12) LV(16)
+    LV(0) LV(4) LV(8) LV(12) LV(16) LV(32) LV(48)
 #undef LV
   } else if (algo == MSCCLPP_AMD_ALGO_ALLPAIR) {
     ll8Defaults(nranks, bytes, nblocks, nthreads);
     const LL8Geom g = ll8Geometry(bytes, kF16);
     if (views[0].scratchBytes < ll8ScratchRequired(nranks, bytes, kF16)) return 5;
 #define LV(VV) if (variant == VV) launchLL8T<kF16, kSum, kMaxRanks, VV>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
-    LV(0) LV(4) LV(8) LV(12)
+    LV(0) LV(4) LV(8) LV(12) LV(32)
 #undef LV
   } else {
     return 4;

@@ -40,7 +40,7 @@ namespace mscclpp_amd {
 // LP: cache policy of the X / Y payload loads and the output stores (nt for streaming buckets; the
 // one-round small form reads with the default policy, so a bucket written or read just before --
 // an AllReduce's input straight from its producer kernel -- is served from the caches).
-template <int DT, int OP, int W, int U, bool SKEW, bool COUNT, int LP = kNonTemporal>
+template <int DT, int OP, int W, int U, int SKEW, bool COUNT, int LP = kNonTemporal>
 __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t* __restrict__ x,
                                                                   const uint8_t* __restrict__ y, uint8_t* pkts,
                                                                   uint8_t* __restrict__ out, uint64_t bytes,
@@ -75,14 +75,14 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
   };
   const uint32_t flagv = __hip_atomic_load(flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (b < ntiles) load_y(b);
-  if (!SKEW && partner < G && partner < ntiles) load_x(partner);  // round 0's consumed tile
+  if (SKEW == 0 && partner < G && partner < ntiles) load_x(partner);  // round 0's consumed tile
   const uint32_t flag = wave_uniform(flagv);
-  for (uint64_t i = 0; i < rounds + (SKEW ? 1 : 0); ++i) {
-    const uint64_t t = i * G + b;                          // packed this round (i < rounds)
-    const uint64_t tp = (SKEW ? i - 1 : i) * G + partner;  // consumed this round
+  for (uint64_t i = 0; i < rounds + SKEW; ++i) {
+    const uint64_t t = i * G + b;                           // packed this round (i < rounds)
+    const uint64_t tp = (i - (uint64_t)SKEW) * G + partner;  // consumed this round (i >= SKEW)
     const bool pack = i < rounds && t < ntiles;
-    const bool consume = (!SKEW || i > 0) && partner < G && tp < ntiles;
-    if (consume && (SKEW || i > 0)) load_x(tp);
+    const bool consume = i >= (uint64_t)SKEW && partner < G && tp < ntiles;
+    if (consume && (SKEW > 0 || i > 0)) load_x(tp);
     // ---- pack: payload -> LDS -> packet-major stores (packets j and 64 + j of each 1 KiB chunk)
     if (pack) {
 #pragma unroll
@@ -174,12 +174,14 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
 //  * one round (up to 4 MiB): payload read and written with the default cache policy (a bucket just
 //    written or read by the caller is served from the caches): 3.6-3.7 us at 64-256 KiB, against
 //    4.6 us with one-wave workgroups per KiB and 5.0 us for round 2's 8 KiB tiles;
-//  * two rounds: unskewed; three and more (48 MiB: 12) partner tiles consumed one round late, nt
-//    payload accesses: 53.0 us at 48 MiB against 54.1 us with round 2's 2 KiB per wave (the skew cut
-//    the first-poll misses from 13.9 % to 0.8 % of the packets and the traffic to 1.004 x 7 S).
+//  * two rounds: unskewed; 3-7 rounds: partner tiles consumed one round late; from 8 rounds (48 MiB:
+//    12) two rounds late; nt payload accesses.  The skew gives a packet time to land before its first
+//    poll: at 48 MiB 2.7 % of the packets miss it with two rounds (6.6 % with one, 13.9 % with none),
+//    52.7 us against 53.1 us (one round late) and 54.1 us (round 2's 2 KiB per wave); with 4 rounds
+//    the second drain round costs more than it saves (16 MiB: 24.5 against 21.8 us).
 struct SelfReduceShape {
   int waves, units, nblocks;
-  bool skew;
+  int skew;    // rounds between packing a tile and its partner consuming it
   bool plain;  // default-policy payload accesses (one round)
 };
 static SelfReduceShape selfReduceShape(uint64_t bytes, int nblocks) {
@@ -190,12 +192,12 @@ static SelfReduceShape selfReduceShape(uint64_t bytes, int nblocks) {
   sh.nblocks = nblocks > 0 ? nblocks : (int)(tiles < 1024 ? tiles : 1024);
   if (sh.nblocks % 2) sh.nblocks += 1;
   const uint64_t rounds = (tiles + sh.nblocks - 1) / sh.nblocks;
-  sh.skew = rounds >= 3;
+  sh.skew = rounds >= 8 ? 2 : rounds >= 3 ? 1 : 0;
   sh.plain = rounds == 1;
   return sh;
 }
 
-template <int DT, int OP, int W, int U, bool SKEW, bool COUNT, int LP = kNonTemporal>
+template <int DT, int OP, int W, int U, int SKEW, bool COUNT, int LP = kNonTemporal>
 static void launchSelfReduceShape(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                                   int nblocks, uint64_t budget, uint32_t* err, uint32_t* pollMiss, hipStream_t stream) {
   hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, W, U, SKEW, COUNT, LP>), dim3(nblocks), dim3(64 * W), 0, stream,
@@ -208,13 +210,16 @@ static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out
                              int nblocks, uint64_t budget, uint32_t* err, hipStream_t stream) {
   const SelfReduceShape sh = selfReduceShape(bytes, nblocks);
   if (sh.plain)
-    launchSelfReduceShape<DT, OP, 4, 1, false, false, kPlain>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err,
+    launchSelfReduceShape<DT, OP, 4, 1, 0, false, kPlain>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err,
                                                               nullptr, stream);
-  else if (sh.skew)
-    launchSelfReduceShape<DT, OP, 4, 1, true, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
+  else if (sh.skew == 2)
+    launchSelfReduceShape<DT, OP, 4, 1, 2, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
+                                                  stream);
+  else if (sh.skew == 1)
+    launchSelfReduceShape<DT, OP, 4, 1, 1, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
                                                      stream);
   else
-    launchSelfReduceShape<DT, OP, 4, 1, false, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
+    launchSelfReduceShape<DT, OP, 4, 1, 0, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
                                                       stream);
 }
 
@@ -273,9 +278,9 @@ using namespace mscclpp_amd;
 
 #ifdef MSCCLPP_AMD_DIAG
 // Tuning / diagnostic entry (fp16 SUM), built only into the test diagnostics library
-// (tests/bin/libselfreduce_diag.so, mscclpp_amd/_build.py build_diag): any (waves, units, skew) shape
-// on any grid, and with count = 1 the number of packets whose first poll missed added to
-// pollMiss[0] (must not be null).
+// (tests/bin/libselfreduce_diag.so, mscclpp_amd/_build.py build_diag): any (waves, units, skew depth
+// 0 / 1, or 2 for 4 waves) shape on any grid, and with count = 1 the number of packets whose first
+// poll missed added to pollMiss[0] (must not be null).
 extern "C" int mscclppAmdSelfReduceLL16Shape(const void* x, const void* y, void* pkts, void* out, size_t bytes,
                                              uint32_t* flags, int nblocks, int waves, int units, int skew, int count,
                                              uint64_t budgetTicks, uint32_t* err, uint32_t* pollMiss, void* streamPtr) {
@@ -287,7 +292,7 @@ extern "C" int mscclppAmdSelfReduceLL16Shape(const void* x, const void* y, void*
   if (count && !pollMiss) return 4;
   if (nblocks % 2) nblocks += 1;
 #define SRS(W, U, SK, C)                                                                                      \
-  if (waves == W && units == U && (skew != 0) == SK && (count != 0) == C) {                                   \
+  if (waves == W && units == U && skew == SK && (count != 0) == C) {                                          \
     if (plain)                                                                                                \
       launchSelfReduceShape<kF16, kSum, W, U, SK, C, kPlain>(x, y, pkts, out, bytes, flags, nblocks,          \
                                                              budgetTicks, err, pollMiss, s);                 \
@@ -296,8 +301,9 @@ extern "C" int mscclppAmdSelfReduceLL16Shape(const void* x, const void* y, void*
                                                      pollMiss, s);                                           \
     return hipGetLastError() == hipSuccess ? 0 : 1;                                                           \
   }
-#define SRS_SK(W, U) SRS(W, U, true, false) SRS(W, U, false, false) SRS(W, U, true, true) SRS(W, U, false, true)
+#define SRS_SK(W, U) SRS(W, U, 1, false) SRS(W, U, 0, false) SRS(W, U, 1, true) SRS(W, U, 0, true)
   SRS_SK(1, 1) SRS_SK(2, 1) SRS_SK(2, 2) SRS_SK(4, 1) SRS_SK(4, 2) SRS_SK(8, 1) SRS_SK(8, 2)
+  SRS(4, 1, 2, false) SRS(4, 1, 2, true) SRS(4, 2, 2, false) SRS(4, 2, 2, true)
 #undef SRS_SK
 #undef SRS
   return 4;
@@ -311,7 +317,7 @@ extern "C" int mscclppAmdSelfReduceLL16DefaultShape(size_t bytes, int* waves, in
   *waves = sh.waves;
   *units = sh.units;
   *nblocks = sh.nblocks;
-  *skew = sh.skew ? 1 : 0;
+  *skew = sh.skew;
   return 0;
 }
 

@@ -57,7 +57,8 @@ def _assert_equal_words(got, exp, dt):
     (4 << 20, True),                                     # the largest one-round grid: 1024 workgroups
     ((4 << 20) + 16, False),                             # two rounds
     ((8 << 20) + 16, False),                             # three rounds and more: partner tiles one round late
-    ((24 << 20) + 16, True)])
+    ((24 << 20) + 16, True),
+    ((32 << 20) + 16, False)])                           # eight rounds and more: two rounds late
 def test_self_reduce_bit_exact(built, dt, op, nbytes, special):
     import mscclpp_amd as m
 
@@ -92,10 +93,12 @@ def test_self_reduce_rejects_unaligned(built):
 
 
 @pytest.mark.parametrize("nbytes,nblocks,skew", [(16, 2, 0), (4 << 20, 1024, 0), ((4 << 20) + 16, 1024, 0),
-                                                 ((8 << 20) + 16, 1024, 1), ((24 << 20) + 16, 1024, 1)])
+                                                 ((8 << 20) + 16, 1024, 1), ((24 << 20) + 16, 1024, 1),
+                                                 ((32 << 20) + 16, 1024, 2), (48 << 20, 1024, 2)])
 def test_self_reduce_default_shape(built, nbytes, nblocks, skew):
     """The launch shape the product entry picks (4 waves x 1 KiB, one workgroup per 4 KiB up to 1024,
-    the skew from three rounds per workgroup on)."""
+    partner tiles consumed one round late from three rounds per workgroup on, two rounds late from
+    eight)."""
     import ctypes
 
     import mscclpp_amd as m

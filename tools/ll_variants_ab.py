@@ -85,6 +85,19 @@ for algo, kb, variants in CASES:
             t[var].append(graph_us(call(var)))
     row = {f"v{var}": round(float(np.median(t[var])), 2) for var in variants}
     row["correct"] = all(ok.values())
+    # first-poll misses of one call (variant 32: counts into err[8] / err[9] of every rank)
+    for e in ranks.err:
+        e.zero_()
+    call(32)()
+    torch.cuda.synchronize()
+    units = -(-S // 8) // (N if algo == "packet" else 1)  # 8-byte units per slice (LL16) or buffer (LL8)
+    polls = N * (N - 1) * units
+    m8 = sum(int(e[8].item()) for e in ranks.err)
+    m9 = sum(int(e[9].item()) for e in ranks.err)
+    row["first_poll_misses"] = {"reduce": m8, "unpack": m9, "polls_each": polls,
+                                "reduce_frac": round(m8 / polls, 4), "unpack_frac": round(m9 / polls, 4)}
+    for e in ranks.err:
+        e.zero_()
     res[f"{algo}:{kb}KiB"] = row
     print(json.dumps({f"{algo}:{kb}KiB": row}), flush=True)
     del ranks

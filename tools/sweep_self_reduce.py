@@ -93,6 +93,8 @@ def candidates(S):
             c.append((w, u, 1 if rounds >= 3 else 0, nb))
             if rounds == 1 and w == 4:  # the one-round form with default-policy payload accesses
                 c.append((w, u, 0, nb, 2))
+            if rounds >= 4 and w == 4:  # partner tiles consumed two rounds late
+                c.append((w, u, 2, nb))
     return sorted(set(c))
 
 
@@ -129,12 +131,17 @@ for S in sizes:
     best = min(times, key=lambda c: np.median(times[c]))
     row["best"] = name(best)
     row["best_us"] = round(float(np.median(times[best])), 2)
-    if os.environ.get("COUNT"):
-        d = default_shape(S)
-        miss.zero_()
-        shape_fn(S, d[0], d[1], d[2], d[3], 1)()
-        torch.cuda.synchronize()
-        row["first_poll_misses_default"] = int(miss[0].item())
+    if os.environ.get("COUNT") or S == 48 << 20:
+        misses = {}
+        for cnd in cands:
+            if len(cnd) > 4:
+                continue
+            miss.zero_()
+            shape_fn(S, *cnd, 1)()
+            torch.cuda.synchronize()
+            misses[name(cnd)] = int(miss[0].item())
+        row["first_poll_misses"] = misses
+        row["packets"] = S // 8
     res[f"{S >> 10}KiB"] = row
     print(json.dumps({f"{S >> 10}KiB": {k: row[k] for k in ("default_shape", "product_us", "best", "best_us",
                                                              "product_correct", "shapes_correct")}}), flush=True)
