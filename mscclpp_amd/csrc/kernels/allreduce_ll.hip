@@ -137,6 +137,31 @@ __device__ __forceinline__ u32x2 unit_wait(__amdgpu_buffer_rsrc_t pk, uint32_t p
   report_error(err, kErrPacketTimeout);
   return u32x2{0, 0};
 }
+// Wave-level readiness probe (LL16 step 3 from kSentinelUnits units per slice): one lane polls the
+// last unit the wave covers in this pass (one line) until it has landed, so the wave's full poll that
+// follows finds its packets there instead of re-reading lines that had not landed.  A peer stores a
+// wave's 64 units with one instruction, so they land together.  On expiry it returns and the
+// per-unit waits report the error.
+__device__ __forceinline__ void sentinel_wait(__amdgpu_buffer_rsrc_t pk, uint32_t j, uint32_t npk, uint32_t flag,
+                                              uint64_t budget) {
+  const uint32_t j0 = wave_uniform(j);  // the wave's first unit (lanes hold consecutive units)
+  const uint32_t js = j0 + 63 < npk ? j0 + 63 : npk - 1;
+  const bool lead = (threadIdx.x & 63) == 0;
+  auto probe = [&]() {
+    uint32_t ok = 0;
+    if (lead) {
+      const u32x4 a = load16<kSystem>(pk, js * 16u);
+      ok = a.y == flag && a.w == flag;
+    }
+    return wave_uniform(ok) != 0;
+  };
+  if (probe()) return;
+  SpinGuard g(budget);
+  do {
+    __builtin_amdgcn_s_sleep(1);
+    if (probe()) return;
+  } while (!g.expired());
+}
 // 8-byte payload at byte `off` of `base`, of which `valid` bytes are inside the buffer
 __device__ __forceinline__ u32x2 payload_ld(__amdgpu_buffer_rsrc_t r, const uint8_t* base, uint64_t off, uint32_t valid) {
   if (valid >= 8) return load8<kPlain>(r, (uint32_t)off);
@@ -163,11 +188,19 @@ __device__ __forceinline__ void payload_st(__amdgpu_buffer_rsrc_t r, uint8_t* ba
 // V (0 in the product): bits that switch a part back to its round-2 form, for same-process A/B
 // timing through the diagnostics build (MSCCLPP_AMD_DIAG): 4 = polls tested as issued and every peer
 // re-read after a miss, 8 = a scalar flag load ahead of everything else, 16 = every slice size polls
-// all peers at once, 32 = count first-poll misses into err[8] (step 2 / LL8) and err[9] (step 3).
+// all peers at once, 32 = count first-poll misses into err[8] (step 2 / LL8) and err[9] (step 3),
+// 64 = step 3's sentinel at every slice size, 512 = no sentinel at any size.
 // Step 2 issues all of a unit's peer polls at once while a slice has at most kBatchedPollUnits units
 // (LL16 buckets up to 512 KiB at 8 ranks: one memory round trip instead of one per peer, 1.0-1.5 us
 // at 1-512 KiB in the A/B), and polls peer by peer beyond.
 constexpr uint32_t kBatchedPollUnits = 8192;
+// Step 3 waits on a one-line sentinel before a wave's first pass from this many units per slice (LL16
+// buckets from 512 KiB at 8 ranks): there 15-47 % of step 3's first polls found the peer's reduced
+// packet not yet landed and each re-read it (LL16 read 1.057x its algorithmic bytes at 1 MiB); with
+// the sentinel none miss, and 1 MiB runs 13.8 us instead of 14.1.  Below it the sentinel's extra
+// round trip costs 0.2 us (1-256 KiB) more than the re-reads it saves
+// (tools/ll_variants_ab.py, profiles/r3d_ll_sentinel_ab.json).
+constexpr uint32_t kSentinelUnits = 8192;
 template <int DT, int OP, int NV, int V = 0>
 __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16Geom g, int nranks, uint64_t budget) {
   const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
@@ -291,8 +324,10 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
     // one unit per lane and pass, polled and then waited for: issuing a lane's later passes' polls
     // together with its first (all reading lines that had not landed yet) measured slower at every
     // size in the same-process A/B (tools/ll_variants_ab.py, profiles/r3_ll_variants_ab.json)
+    const bool sentinel = (V & 512) == 0 && ((V & 64) != 0 || npk >= kSentinelUnits);
     for (uint32_t j = lb * T + tid; j < npk; j += bpp * T) {
       const uint64_t off = soff + (uint64_t)j * 8;
+      if (sentinel && j < (lb + 1) * T) sentinel_wait(rres, j, npk, flag, budget);  // the wave's first pass
       u32x2 w;
       const bool landed = unit_try(rres, j * 16u, flag, w, false);
       count_misses<V>(v.err + 9, landed ? 0u : 1u);
@@ -624,7 +659,7 @@ extern "C" int mscclppAmdDiagAllReduceLL(int algo, const mscclppAmdRankView* vie
     g.hbOdd = views[0].scratchBytes / 2;
     g.hbEven = 0;
 #define LV(VV) if (variant == VV) launchLL16T<kF16, kSum, kMaxRanks, VV>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
-    LV(0) LV(4) LV(8) LV(12) LV(16) LV(32) LV(48)
+    LV(0) LV(4) LV(8) LV(12) LV(16) LV(32) LV(48) LV(64) LV(96) LV(512) LV(544)
 #undef LV
   } else if (algo == MSCCLPP_AMD_ALGO_ALLPAIR) {
     ll8Defaults(nranks, bytes, nblocks, nthreads);

@@ -279,18 +279,19 @@ using namespace mscclpp_amd;
 #ifdef MSCCLPP_AMD_DIAG
 // Tuning / diagnostic entry (fp16 SUM), built only into the test diagnostics library
 // (tests/bin/libselfreduce_diag.so, mscclpp_amd/_build.py build_diag): any (waves, units, skew depth
-// 0 / 1, or 2 for 4 waves) shape on any grid, and with count = 1 the number of packets whose first
+// 0 / 1, or 2 for 4 waves) shape on any grid, and with count bit 0 the number of packets whose first
 // poll missed added to pollMiss[0] (must not be null).
 extern "C" int mscclppAmdSelfReduceLL16Shape(const void* x, const void* y, void* pkts, void* out, size_t bytes,
                                              uint32_t* flags, int nblocks, int waves, int units, int skew, int count,
                                              uint64_t budgetTicks, uint32_t* err, uint32_t* pollMiss, void* streamPtr) {
-  // count == 2: no miss count, default-policy payload loads / stores (the small form's choice)
-  const bool plain = count == 2;
-  if (plain) count = 0;
   hipStream_t s = (hipStream_t)streamPtr;
   if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > 4096) return 4;
-  if (count && !pollMiss) return 4;
+  if ((count & 1) && !pollMiss) return 4;
   if (nblocks % 2) nblocks += 1;
+  // count: bit 0 = count first-poll misses, bit 1 = default-policy payload loads / stores (the small
+  // form's choice)
+  const bool plain = (count & 2) != 0;
+  count &= 1;
 #define SRS(W, U, SK, C)                                                                                      \
   if (waves == W && units == U && skew == SK && (count != 0) == C) {                                          \
     if (plain)                                                                                                \

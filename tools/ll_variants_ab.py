@@ -3,7 +3,9 @@ mscclppAmdDiagAllReduceLL): 8 ranks in one launch on one GPU, fp16 SUM, default 
 time from 20 calls in one HIP graph, variants interleaved over 5 rounds (box-to-box spread is larger
 than the differences measured).  Variant bits switch a part back to its round-2 form: 4 = polls
 tested as issued and every peer re-read after a miss, 8 = scalar flag load first, 16 = LL16 polls
-all peers at once at every slice size (the product does up to 8192 units per slice).  (Bits 1 and 2, a
+all peers at once at every slice size (the product does up to 8192 units per slice), 64 = LL16 step 3
+waits on a one-line sentinel before a wave's first pass at every size, 512 = at no size (the product:
+from 8192 units per slice).  (Bits 1 and 2, a
 batched step 1 / step 3 of LL16, measured slower and were removed; profiles/r3_ll_variants_ab.json
 keeps that run.)  Every variant's output is checked against variant 0's.
 
@@ -27,8 +29,9 @@ D.mscclppAmdDiagAllReduceLL.argtypes = [ctypes.c_int, vp, ctypes.c_int, ctypes.c
                                         ctypes.c_int, ctypes.c_int, ctypes.c_uint64, vp]
 N = 8
 torch.cuda.set_device(0)
-CASES = [("allpair", kb, (0, 4, 8, 12)) for kb in (1, 4, 16)] + \
-        [("packet", kb, (0, 4, 16)) for kb in (1, 16, 128, 256, 512, 1024)]
+CASES = [("allpair", kb, (0, 4, 8)) for kb in (1, 4, 16)] + \
+        [("packet", kb, (0, 4, 64, 512)) for kb in (1, 16, 128, 256, 512, 1024)]
+COUNTED = {"allpair": (0,), "packet": (0, 64, 512)}  # miss counts of these (variant | 32)
 
 
 def graph_us(fn, calls=20, replays=10):
@@ -86,18 +89,20 @@ for algo, kb, variants in CASES:
     row = {f"v{var}": round(float(np.median(t[var])), 2) for var in variants}
     row["correct"] = all(ok.values())
     # first-poll misses of one call (variant 32: counts into err[8] / err[9] of every rank)
-    for e in ranks.err:
-        e.zero_()
-    call(32)()
-    torch.cuda.synchronize()
     units = -(-S // 8) // (N if algo == "packet" else 1)  # 8-byte units per slice (LL16) or buffer (LL8)
     polls = N * (N - 1) * units
-    m8 = sum(int(e[8].item()) for e in ranks.err)
-    m9 = sum(int(e[9].item()) for e in ranks.err)
-    row["first_poll_misses"] = {"reduce": m8, "unpack": m9, "polls_each": polls,
-                                "reduce_frac": round(m8 / polls, 4), "unpack_frac": round(m9 / polls, 4)}
-    for e in ranks.err:
-        e.zero_()
+    for base in COUNTED[algo]:
+        key = "first_poll_misses" + (f"_v{base}" if base else "")
+        for e in ranks.err:
+            e.zero_()
+        call(base | 32)()
+        torch.cuda.synchronize()
+        m8 = sum(int(e[8].item()) for e in ranks.err)
+        m9 = sum(int(e[9].item()) for e in ranks.err)
+        row[key] = {"reduce": m8, "unpack": m9, "polls_each": polls,
+                    "reduce_frac": round(m8 / polls, 4), "unpack_frac": round(m9 / polls, 4)}
+        for e in ranks.err:
+            e.zero_()
     res[f"{algo}:{kb}KiB"] = row
     print(json.dumps({f"{algo}:{kb}KiB": row}), flush=True)
     del ranks

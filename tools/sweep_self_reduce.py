@@ -134,10 +134,8 @@ for S in sizes:
     if os.environ.get("COUNT") or S == 48 << 20:
         misses = {}
         for cnd in cands:
-            if len(cnd) > 4:
-                continue
             miss.zero_()
-            shape_fn(S, *cnd, 1)()
+            shape_fn(S, *cnd[:4], (cnd[4] if len(cnd) > 4 else 0) | 1)()  # count bit 0, plain bit 1
             torch.cuda.synchronize()
             misses[name(cnd)] = int(miss[0].item())
         row["first_poll_misses"] = misses
