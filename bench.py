@@ -176,13 +176,15 @@ def committed_multirank_pmc(kernel):
                                    "source": os.path.basename(files[-1])}
 
 
-def host_proxy_baseline():
-    """BASELINE config 1 (host-proxy path, 2 ranks, 4 KiB) -- spawned before this process touches the GPU."""
+def host_proxy_baseline(n=2):
+    """The reference's host-proxy path (test/allgather_test_host_offloading.cu, 4 KiB) on n ranks --
+    spawned before this process touches the GPU.  N=1: BASELINE config 1 (2 ranks, loopback); N>1:
+    the same loop at the job's world size, one rank per GPU (2 cores per rank)."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     try:
         import host_proxy_baseline as H
 
-        return H.run(2, 4096, timeout=240)
+        return H.run(n, 4096, timeout=240)
     except Exception as e:  # recorded, never fatal for the headline line
         return {"error": str(e)[-400:]}
 
@@ -480,7 +482,7 @@ def bench_multi(args):
     # oracle's n-way sum of the bucket on this box's cores
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = {"host_proxy": host_proxy_baseline(), "sum": cpu_baseline_sum(world, args.bytes, args.cpu_seconds)}
+        cpu = {"host_proxy": host_proxy_baseline(world), "sum": cpu_baseline_sum(world, args.bytes, args.cpu_seconds)}
     ndev = torch.cuda.device_count()
     if ndev < world:  # rehearsal on a smaller box: ranks share devices (never the case on the 8-GPU node)
         local = local % ndev
