@@ -349,6 +349,20 @@ def same_run_ceilings(m, S, x, y, pk, out, flags, err, kern_ms, reps=20):
     torch.cuda.synchronize()
     copy_us = a.elapsed_time(b) * 1e3 / reps
     copy_gbs = 2 * S / (copy_us * 1e-6) / 1e9
+
+    def stream():  # the self-reduce's exact 7*S access mix with no hand-off (mscclppAmdSelfReduceStream)
+        m.check(L.mscclppAmdSelfReduceStream(vp(x.data_ptr()), vp(y.data_ptr()), vp(pk.ptr), vp(dst.data_ptr()), S,
+                                             m.stream_ptr()), "stream mix")
+
+    stream()
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(reps):
+        stream()
+    b.record()
+    torch.cuda.synchronize()
+    mix_us = a.elapsed_time(b) * 1e3 / reps
+    mix_gbs = 7 * S / (mix_us * 1e-6) / 1e9
     scrub = torch.empty(512 << 20, dtype=torch.uint8, device=x.device)
 
     def one_pair(cold):
@@ -370,6 +384,10 @@ def same_run_ceilings(m, S, x, y, pk, out, flags, err, kern_ms, reps=20):
     return {"copy_ceiling_GBs": round(copy_gbs, 1), "copy_ceiling_frac": round(copy_gbs / HBM_PEAK_GBS, 4),
             "copy_us": round(copy_us, 2),
             "frac_of_copy_ceiling": round(seven / (kern_ms * 1e-3) / 1e9 / copy_gbs, 4),
+            "mix_ceiling_GBs": round(mix_gbs, 1), "mix_ceiling_frac": round(mix_gbs / HBM_PEAK_GBS, 4),
+            "mix_us": round(mix_us, 2), "frac_of_mix_ceiling": round(seven / (kern_ms * 1e-3) / 1e9 / mix_gbs, 4),
+            "mix_note": "mix: the kernel's own 7*S accesses on the same buffers, grid and rounds with no flags, "
+                        "polls or LDS (mscclppAmdSelfReduceStream)",
             "cold": {"kernel_us": round(res["cold"], 2),
                      "achieved": round(seven / (res["cold"] * 1e-6) / 1e9, 1),
                      "frac": round(seven / (res["cold"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),

@@ -122,6 +122,11 @@ int mscclppAmdCopyJobs(const void* const* srcs, void* const* dsts, const size_t*
  * with nt or agent loads.  4 = a combination not carried. */
 int mscclppAmdCopyJobsPolicy(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs,
                              int blocksPerJob, int loadPolicy, int storePolicy, void* stream);
+/* The self-reduce's exact memory accesses (Y read, packets stored and the partner's read two rounds
+ * late, X read, O written: 7 * bytes over the same buffers, grid and rounds) with no flags, readiness
+ * tests or LDS: the streaming ceiling of that access mix.  bytes: a multiple of 8 KiB; pkts: 2 * bytes.
+ * The output is meaningless. */
+int mscclppAmdSelfReduceStream(const void* x, const void* y, void* pkts, void* out, size_t bytes, void* stream);
 
 /* ---- explicit-view AllReduce ------------------------------------------------------------- */
 /* Launch `algo` for `nviews` ranks of an `nranks`-rank AllReduce in ONE kernel launch (views[i]

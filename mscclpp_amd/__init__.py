@@ -111,6 +111,7 @@ def lib():
         "mscclppAmdCommRegisterBuffer": [vp, vp, ctypes.POINTER(vp)],
         "mscclppAmdCommDeregisterAll": [vp],
         "mscclppAmdCopy": [vp, vp, sz, i32, vp],
+        "mscclppAmdSelfReduceStream": [vp, vp, vp, vp, sz, vp],
         "mscclppAmdCopyJobs": [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz), i32, i32, vp],
         "mscclppAmdCopyJobsPolicy": [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz), i32, i32, i32, i32, vp],
         "mscclppAmdSelfReduceLL16DefaultShape": [sz, vp, vp, vp, vp],

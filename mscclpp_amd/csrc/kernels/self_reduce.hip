@@ -242,6 +242,37 @@ __global__ void __launch_bounds__(256) copyKernel(const uint8_t* __restrict__ sr
   }
 }
 
+// Same-traffic streaming ceiling of the self-reduce (benchmark only): the large form's exact memory
+// accesses -- per wave and round, 1 KiB of Y read, 2 KiB of packets stored packet-major (two 1 KiB
+// instructions, system scope), the partner's 2 KiB of packets from two rounds earlier read (system
+// scope), 1 KiB of X read and 1 KiB of O written, all on the same buffers, grid and rounds -- with no
+// flags, readiness tests, re-polls or LDS.  Its time is what the memory system gives this 7*S access
+// mix; the product kernel's time against it is the cost of the hand-off itself.  (The packets read
+// are whatever is there: the output is meaningless.)
+__global__ void __launch_bounds__(256) selfReduceStreamKernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
+                                                              uint8_t* pkts, uint8_t* __restrict__ out, uint64_t bytes) {
+  constexpr uint64_t kTile = 4096;  // 4 waves x 1 KiB
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  const uint64_t ntiles = bytes / kTile;
+  const uint64_t rounds = (ntiles + G - 1) / G;
+  for (uint64_t i = 0; i < rounds; ++i) {
+    const uint64_t t = i * G + b;
+    if (t >= ntiles) break;
+    const uint64_t tp = ((i >= 2 ? i - 2 : i + rounds - 2) * G + (b ^ 1u)) % ntiles;  // partner, two rounds late
+    const uint64_t c = t * kTile + wave * 1024, cp = tp * kTile + wave * 1024;
+    const u32x4 yv = load16<kNonTemporal>(make_rsrc(y + c), lane * 16);
+    const u32x4 xv = load16<kNonTemporal>(make_rsrc(x + cp), lane * 16);
+    const auto rpp = make_rsrc(pkts + 2 * cp);
+    const u32x4 p0 = load16<kSystem>(rpp, lane * 16);
+    const u32x4 p1 = load16<kSystem>(rpp, 1024 + lane * 16);
+    const auto rp = make_rsrc(pkts + 2 * c);
+    store16<kSystem>(rp, lane * 16, u32x4{yv.x, 0u, yv.y, 0u});  // flag 0: no call ever waits for it
+    store16<kSystem>(rp, 1024 + lane * 16, u32x4{yv.z, 0u, yv.w, 0u});
+    store16<kNonTemporal>(make_rsrc(out + cp), lane * 16, u32x4{xv.x ^ p0.x, xv.y ^ p0.z, xv.z ^ p1.x, xv.w ^ p1.z});
+  }
+}
+
 // Several independent copies in ONE launch: workgroups [j*B, (j+1)*B) move job j.  The xGMI probe
 // uses it so that all peers' links are driven by one kernel on one stream (one hardware queue),
 // instead of one stream per peer that the pool's GPU_MAX_HW_QUEUES=4 would serialise.  Remote
@@ -332,6 +363,17 @@ extern "C" int mscclppAmdCopy(const void* src, void* dst, size_t bytes, int nblo
 
 extern "C" int mscclppAmdCopyJobsPolicy(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs,
                                         int blocksPerJob, int loadPolicy, int storePolicy, void* streamPtr);
+
+extern "C" int mscclppAmdSelfReduceStream(const void* x, const void* y, void* pkts, void* out, size_t bytes,
+                                          void* streamPtr) {
+  // the product's large-form grid: one workgroup per 4 KiB tile, at most 1024
+  if (!x || !y || !pkts || !out || bytes == 0 || bytes % 8192) return 4;
+  const uint64_t tiles = bytes / 4096;
+  const int nblocks = (int)(tiles < 1024 ? tiles : 1024);
+  hipLaunchKernelGGL(selfReduceStreamKernel, dim3(nblocks), dim3(256), 0, (hipStream_t)streamPtr, (const uint8_t*)x,
+                     (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, (uint64_t)bytes);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
 
 extern "C" int mscclppAmdCopyJobs(const void* const* srcs, void* const* dsts, const size_t* bytes, int njobs,
                                   int blocksPerJob, void* streamPtr) {

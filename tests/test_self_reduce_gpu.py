@@ -108,3 +108,28 @@ def test_self_reduce_default_shape(built, nbytes, nblocks, skew):
                                                          ctypes.byref(sk)), "default shape")
     assert (w.value, u.value, nb.value, sk.value) == (4, 1, nblocks, skew)
 
+
+
+@pytest.mark.parametrize("nbytes", [8 << 10, (8 << 20) + (8 << 10)])
+def test_self_reduce_stream_mirror_in_bounds(built, nbytes):
+    """The benchmark's same-traffic ceiling kernel (mscclppAmdSelfReduceStream) stores every packet of
+    the packet buffer (flag word 0) and nothing past the packet buffer or the output; sizes that are
+    not a multiple of 8 KiB are rejected."""
+    import mscclpp_amd as m
+
+    guard = 1 << 16
+    x = torch.randint(-2**15, 2**15, (nbytes // 2,), dtype=torch.int16, device="cuda")
+    y = torch.randint(-2**15, 2**15, (nbytes // 2,), dtype=torch.int16, device="cuda")
+    out = torch.full(((nbytes + guard) // 4,), -1, dtype=torch.int32, device="cuda")
+    pk = torch.full(((2 * nbytes + guard) // 4,), -1, dtype=torch.int32, device="cuda")
+    L = m.lib()
+    m.check(L.mscclppAmdSelfReduceStream(x.data_ptr(), y.data_ptr(), pk.data_ptr(), out.data_ptr(), nbytes,
+                                         m.stream_ptr()), "stream mirror")
+    torch.cuda.synchronize()
+    words = pk.cpu().numpy().view(np.uint32)
+    flags = words[: 2 * nbytes // 4].reshape(-1, 4)[:, [1, 3]]
+    assert np.all(flags == 0)  # every packet of the 2 * nbytes buffer was stored
+    assert np.all(words[2 * nbytes // 4:] == 0xFFFFFFFF)
+    assert np.all(out.cpu().numpy().view(np.uint32)[nbytes // 4:] == 0xFFFFFFFF)
+    assert L.mscclppAmdSelfReduceStream(x.data_ptr(), y.data_ptr(), pk.data_ptr(), out.data_ptr(), nbytes - 4096,
+                                        m.stream_ptr()) == 4
