@@ -28,6 +28,12 @@ def _bench(extra_env):
 def test_skipped_handshake_is_caught(built):
     good = _bench({})
     assert good["correct"] is True and good["correct_bitexact"]["timed_last_step"] is True
+    # the N>1 line is complete: roofline, the CPU sum and the host-proxy loop
+    # at the job's world size, each with its cores
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(good["roofline"])
+    assert good["cpu_baseline"]["cores"] >= 1 and "2-way sum" in good["cpu_baseline"]["sample"]
+    hp = good["host_proxy_baseline"]
+    assert hp.get("ranks") == 2 and hp.get("cores") == 4 and hp.get("correct") is True, hp
     bad = _bench({"MSCCLPP_AMD_DEBUG_SKIP_HANDSHAKE": "1"})
     assert bad["correct"] is False
     assert any(v is False for k, v in bad["correct_bitexact"].items() if k.startswith("fullmesh"))
