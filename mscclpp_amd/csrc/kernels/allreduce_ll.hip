@@ -567,16 +567,20 @@ static void launchLL8(const mscclppAmdRankView* views, int nviews, const LL8Geom
 // are (n-1)*4 blocks below 32 KiB and (n-1)*8 above).  Restated for this kernel from the fabric-free
 // sweep (tools/inprocess_ll_probe.py, profiles/r2g_inprocess_ll_probe.json, 8 ranks): steps 1 and 3
 // move a peer's slice with G/(n-1) blocks, and every extra pass over it adds a poll round trip, so
-// the blocks per peer cover the slice in one pass, from 4 up to 16 per peer and at most 56 in all;
-// 512 lanes below 32 KiB and from 256 KiB, 256 between.
+// the blocks per peer cover the slice in one pass, from 4 up to max(16, 48 / (n-1)) per peer and at
+// most 56 in all; 512 lanes below 32 KiB and from 256 KiB, 256 between.  (Round 3, the same sweep at 2,
+// 3 and 4 ranks, profiles/r3f_inprocess_ll_probe_n{2,3,4}.json: with few peers the round-2 cap of 16
+// blocks per peer left a large slice to several passes -- 2 ranks at 1 MiB 19.3 us on 16 blocks, 9.5 us
+// on 56; 3 ranks 14.0 us on 32, 10.7 on 48; 4 ranks already at its best on 48.)
 static void ll16Defaults(int nranks, size_t bytes, int& nblocks, int& nthreads) {
   const int nPeers = nranks - 1;
   const LL16Geom g = ll16Geometry(nranks, bytes, kF16);
   if (nthreads <= 0) nthreads = (bytes < (32u << 10) || bytes >= (256u << 10)) ? 512 : 256;
   if (nblocks <= 0) {
+    const uint64_t bppMax = 48 / nPeers > 16 ? 48 / nPeers : 16;
     uint64_t bpp = (g.units + nthreads - 1) / nthreads;  // blocks per peer for one pass
     if (bpp < 4) bpp = 4;
-    if (bpp > 16) bpp = 16;
+    if (bpp > bppMax) bpp = bppMax;
     while (bpp > 1 && bpp * nPeers > 56) --bpp;
     nblocks = (int)(bpp * nPeers);
   }

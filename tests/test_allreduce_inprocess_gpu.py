@@ -53,6 +53,8 @@ LL_CASES = [
     (2, O.F16, 4096, False), (4, O.F16, 8192, True), (8, O.F16, 16384, True), (8, O.BF16, 16384, True),
     (8, O.F32, 8192, False), (8, O.I32, 8192, False), (3, O.F16, 3000, False), (8, O.F16, 1000, False),
     (8, O.F16, 777, False), (5, O.F32, 1001, False), (8, O.F16, 262144, False),
+    # LL16 step 3's sentinel (from 8192 units per slice) with a ragged last wave and several passes
+    (3, O.F16, 100003, True), (5, O.BF16, 165074, False), (7, O.F32, 114787, False),
 ]
 
 
