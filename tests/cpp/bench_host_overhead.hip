@@ -35,6 +35,24 @@
   } while (0)
 
 __global__ void emptyKernel() {}
+// the LL kernels' argument block: one rank view + geometry + rank count + spin budget
+struct BigArgs {
+  mscclppAmdRankView v;
+  uint64_t geom[6];
+  int n;
+  uint64_t budget;
+};
+__global__ void emptyKernelBigArgs(BigArgs a) {
+  if (a.n < 0) a.v.err[0] = 1;  // never true: keeps the argument live
+}
+template <int N>
+struct Words {
+  uint64_t w[N];
+};
+template <int N>
+__global__ void emptyKernelWords(Words<N> a) {
+  if (a.w[N - 1] == 1) a.w[0] = 0;  // never true
+}
 
 struct PerCall {
   double host, drain;  // us per call: issuing loop alone; issuing loop + the device catching up
@@ -67,6 +85,20 @@ static int worker(int rank, int n, ncclUniqueId id, int iters) {
   HIP_OK(hipMalloc(&out, count * 2));
   HIP_OK(hipMemset(in, 0, count * 2));
   const PerCall empty = perCall([&] { hipLaunchKernelGGL(emptyKernel, dim3(1), dim3(64), 0, s); }, iters, s);
+  BigArgs big{};
+  big.n = n;
+  const PerCall emptyBig =
+      perCall([&] { hipLaunchKernelGGL(emptyKernelBigArgs, dim3(1), dim3(64), 0, s, big); }, iters, s);
+  Words<1> w1{};
+  Words<8> w8{};
+  Words<16> w16{};
+  Words<32> w32{};
+  const double a8 = perCall([&] { hipLaunchKernelGGL(emptyKernelWords<1>, dim3(1), dim3(64), 0, s, w1); }, iters, s).host;
+  const double a64 = perCall([&] { hipLaunchKernelGGL(emptyKernelWords<8>, dim3(1), dim3(64), 0, s, w8); }, iters, s).host;
+  const double a128 =
+      perCall([&] { hipLaunchKernelGGL(emptyKernelWords<16>, dim3(1), dim3(64), 0, s, w16); }, iters, s).host;
+  const double a256 =
+      perCall([&] { hipLaunchKernelGGL(emptyKernelWords<32>, dim3(1), dim3(64), 0, s, w32); }, iters, s).host;
   NCCL_OK(mscclppAmdCommBarrier(comm));
   const PerCall nccl = perCall([&] { ncclAllReduce(in, out, count, ncclFloat16, ncclSum, comm, s); }, iters, s);
   NCCL_OK(mscclppAmdCommBarrier(comm));
@@ -78,9 +110,12 @@ static int worker(int rank, int n, ncclUniqueId id, int iters) {
   NCCL_OK(mscclppAmdCommGetDeviceError(comm, &err, 0));
   if (rank == 0)
     std::printf("{\"ranks\": %d, \"bytes\": %zu, \"iters\": %d, \"empty_launch_us\": [%.2f, %.2f], "
+                "\"empty_launch_%zuB_args_us\": [%.2f, %.2f], \"empty_launch_host_us_by_arg_bytes\": "
+                "{\"8\": %.2f, \"64\": %.2f, \"128\": %.2f, \"256\": %.2f}, "
                 "\"ncclAllReduce_us\": [%.2f, %.2f], \"named_allpair_us\": [%.2f, %.2f], \"device_error\": %u, "
                 "\"note\": \"[host issuing loop, host loop + drain] per call\"}\n",
-                n, count * 2, iters, empty.host, empty.drain, nccl.host, nccl.drain, named.host, named.drain, err);
+                n, count * 2, iters, empty.host, empty.drain, sizeof(BigArgs), emptyBig.host, emptyBig.drain, a8, a64, a128, a256, nccl.host,
+                nccl.drain, named.host, named.drain, err);
   std::fflush(stdout);
   NCCL_OK(ncclCommDestroy(comm));
   return err ? 5 : 0;
