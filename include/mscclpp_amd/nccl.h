@@ -25,6 +25,7 @@ extern "C" {
 
 typedef struct ncclComm* ncclComm_t;
 #define NCCL_COMM_NULL NULL
+typedef struct ncclWindow* ncclWindow_t; /* nccl.h:18 */
 
 #define NCCL_UNIQUE_ID_BYTES 128
 typedef struct {
@@ -149,6 +150,11 @@ typedef struct ncclSimInfo_v22200 {
 /* nccl.cc:840 */ ncclResult_t ncclGroupSimulateEnd(ncclSimInfo_t* simInfo);
 /* nccl.cc:846 */ ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
 /* nccl.cc:852 */ ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle);
+/* nccl.cc:511 / :516 (unavailable there): the path maps buffers lazily on first use, so a window is
+ * the buffer's address handed back, as ncclCommRegister does; deregistering it is a no-op. */
+/* nccl.cc:511 */ ncclResult_t ncclCommWindowRegister(ncclComm_t comm, void* buff, size_t size, ncclWindow_t* win,
+                                                      int winFlags);
+/* nccl.cc:516 */ ncclResult_t ncclCommWindowDeregister(ncclComm_t comm, ncclWindow_t win);
 /* nccl.cc:823 */ ncclResult_t ncclGroupStart(void);
 /* nccl.cc:832 */ ncclResult_t ncclGroupEnd(void);
 /* nccl.cc:858 */ ncclResult_t ncclMemAlloc(void** ptr, size_t size);

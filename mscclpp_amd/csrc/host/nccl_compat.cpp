@@ -2,8 +2,9 @@
 // libmscclpp_amd.so can stand in for librccl.so under LD_PRELOAD / LD_AUDIT:
 //
 //  * native here: ncclBroadcast / ncclBcast (zero-copy pull from the root), ncclCommSplit
-//    (nccl.cc:405-435), ncclCommInitRankScalable with one id, ncclCommRegister / Deregister (the
-//    path registers buffers lazily on first use, so these only hand the pointer back);
+//    (nccl.cc:405-435), ncclCommInitRankScalable with one id, ncclCommRegister / Deregister and
+//    ncclCommWindowRegister / Deregister (the path registers buffers lazily on first use, so these
+//    only hand the pointer back);
 //  * forwarded to the vendor library when MSCCLPP_AMD_NCCL_LIB_PATH (or the reference's
 //    MSCCLPP_NCCL_LIB_PATH) names it -- the reference's dlopen fallback, nccl.cc:72-160, :323-346:
 //    ncclReduce, ncclSend/Recv, ncclAllToAll(v), ncclRedOpCreatePreMulSum/Destroy,
@@ -288,6 +289,17 @@ ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, vo
 
 ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle) {
   if (!comm || !handle) return ncclInvalidArgument;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommWindowRegister(ncclComm_t comm, void* buff, size_t size, ncclWindow_t* win, int) {
+  if (!comm || !buff || !size || !win) return ncclInvalidArgument;
+  *win = reinterpret_cast<ncclWindow_t>(buff);  // mapped lazily by the algorithm that first uses it
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommWindowDeregister(ncclComm_t comm, ncclWindow_t win) {
+  if (!comm || !win) return ncclInvalidArgument;
   return ncclSuccess;
 }
 

@@ -97,3 +97,30 @@ def test_vendor_fallback_absent_means_invalid_usage(built):
     h = vp()
     assert L.ncclCommRegister(None, None, 0, ctypes.byref(h)) == 4
     assert L.ncclGroupStart() == 0 and L.ncclGroupEnd() == 0
+
+
+# Every entry point src/ext/nccl/nccl.cc defines (NCCL_API functions of the reference's shim).
+REFERENCE_NCCL_SYMBOLS = """ncclAllGather ncclAllReduce ncclAllToAll ncclAllToAllv ncclBcast ncclBroadcast ncclCommAbort
+ncclCommCount ncclCommCuDevice ncclCommDeregister ncclCommDestroy ncclCommFinalize ncclCommGetAsyncError
+ncclCommInitAll ncclCommInitRank ncclCommInitRankConfig ncclCommInitRankScalable ncclCommRegister ncclCommSplit
+ncclCommUserRank ncclCommWindowDeregister ncclCommWindowRegister ncclGetErrorString ncclGetLastError
+ncclGetUniqueId ncclGetVersion ncclGroupEnd ncclGroupSimulateEnd ncclGroupStart ncclMemAlloc ncclMemFree
+ncclRecv ncclRedOpCreatePreMulSum ncclRedOpDestroy ncclReduce ncclReduceScatter ncclSend""".split()
+
+
+def test_exports_every_reference_nccl_entry_point(built):
+    """The drop-in exports every function of the reference's NCCL shim (a binary built against its
+    nccl.h resolves all of them), and the window registration hands the buffer back like
+    ncclCommRegister (nccl.cc:511-519)."""
+    import mscclpp_amd as m
+
+    ours = subprocess.run(["nm", "-D", "--defined-only", m.LIB_PATH], stdout=subprocess.PIPE, text=True).stdout
+    have = {ln.split()[-1] for ln in ours.splitlines() if " T " in ln}
+    assert not (set(REFERENCE_NCCL_SYMBOLS) - have), sorted(set(REFERENCE_NCCL_SYMBOLS) - have)
+    L = m.lib()
+    vp = ctypes.c_void_p
+    L.ncclCommWindowRegister.argtypes = [vp, vp, ctypes.c_size_t, ctypes.POINTER(vp), ctypes.c_int]
+    L.ncclCommWindowDeregister.argtypes = [vp, vp]
+    w = vp()
+    assert L.ncclCommWindowRegister(None, None, 0, ctypes.byref(w), 0) == 4
+    assert L.ncclCommWindowDeregister(None, None) == 4
