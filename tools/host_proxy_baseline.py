@@ -8,6 +8,7 @@ import json
 import multiprocessing as mp
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -55,11 +56,19 @@ def run(n=2, size=4096, timeout=180):
     for p in ps:
         p.start()
     got = {}
-    for _ in range(n):
-        rank, res, err = q.get(timeout=timeout)
-        if err:
-            raise RuntimeError(err)
-        got[rank] = res
+    deadline = time.monotonic() + timeout
+    try:
+        for _ in range(n):
+            rank, res, err = q.get(timeout=max(1.0, deadline - time.monotonic()))
+            if err:
+                raise RuntimeError(err)
+            got[rank] = res
+    except BaseException:
+        for p in ps:  # a rank that failed or stalled: none of its peers may keep spinning on the GPU
+            p.kill()
+        for p in ps:
+            p.join(timeout=30)
+        raise
     for p in ps:
         p.join(timeout=30)
     r0 = got[0]
