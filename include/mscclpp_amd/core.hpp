@@ -114,8 +114,11 @@ class RegisteredMemory {
 };
 
 // ---- connection (core.hpp:630-689) --------------------------------------------------------------
-// A host-driven CudaIpc connection to one peer: a non-blocking HIP stream on this GPU whose copies
-// (hipMemcpyAsync, the copy engines) write into the peer's mapped memory.
+// A host-driven CudaIpc connection to one peer: copies (hipMemcpyAsync, the copy engines) on a
+// non-blocking HIP stream of this GPU write into the peer's mapped memory.  All connections of a
+// communicator share that stream (as the reference's CUDA build does), so flush() also waits for the
+// other connections' copies: HIP multiplexes a process's streams onto four hardware queues, and a
+// per-connection stream could land behind a kernel spinning for its own data.
 class Connection {
  public:
   Connection() = default;
@@ -130,7 +133,7 @@ class Connection {
   Transport remoteTransport() const;
   int remoteRank() const;
   int tag() const;
-  hipStream_t stream() const;  // the connection's copy stream
+  hipStream_t stream() const;  // the communicator's shared copy stream
   struct Impl;
   explicit Connection(std::shared_ptr<Impl> impl) : pimpl_(std::move(impl)) {}
   bool valid() const { return (bool)pimpl_; }

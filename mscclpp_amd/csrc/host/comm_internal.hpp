@@ -243,6 +243,10 @@ struct ncclComm {
   // present when MSCCLPP_AMD_NCCL_LIB_PATH names librccl (nccl_compat.cpp)
   void* fallback = nullptr;
   hipStream_t errStream = nullptr;  // ncclCommGetAsyncError's reads
+  // the copy stream every host-channel Connection of this communicator shares (core.cpp connect);
+  // owned by the connections, created by the first one
+  std::weak_ptr<void> ipcStream;
+  std::mutex ipcStreamMu;
   static constexpr size_t kPipeSemsWords = 3 * 256 + 64;
   uint64_t* pipeSems = nullptr;      // rsag_pipeline's intra-launch counters (3 x 256 + done count)
   std::shared_ptr<mscclpp_amd::Executor> executor;

@@ -204,19 +204,32 @@ RegisteredMemory RegisteredMemory::deserialize(const std::vector<char>& data) {
 // values of updateAndSync are staged in a pinned ring, one slot per value (HIP reads a pinned source
 // when the copy runs, not when it is queued, so one shared word could publish a later value early);
 // a slot is reused only after a stream synchronize retired the copies of the previous lap.
-struct Connection::Impl {
-  int remoteRank = -1;
-  int tag = 0;
-  int device = 0;
+// The copy stream of a communicator's connections.  One stream for all of them (the reference's CUDA
+// branch, connection.cc:126-130), not one per connection (its HIP branch): HIP multiplexes a
+// process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues, and a connection stream that lands
+// on the queue of a kernel spinning for that connection's data never runs -- the PortChannel
+// all-to-all hung with 4 ranks on one GPU.
+struct SharedCopyStream {
   hipStream_t stream = nullptr;
-  uint64_t* slots = nullptr;
-  uint64_t nvals = 0;
-  static constexpr uint64_t kSlots = 1024;
-  ~Impl() {
+  ~SharedCopyStream() {
     if (stream) {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
     }
+  }
+};
+
+struct Connection::Impl {
+  int remoteRank = -1;
+  int tag = 0;
+  int device = 0;
+  std::shared_ptr<SharedCopyStream> copy;
+  hipStream_t stream = nullptr;  // copy->stream
+  uint64_t* slots = nullptr;
+  uint64_t nvals = 0;
+  static constexpr uint64_t kSlots = 1024;
+  ~Impl() {
+    if (stream) (void)hipStreamSynchronize(stream);
     if (slots) (void)hipHostFree(slots);
   }
   void drain(int64_t timeoutUsec) {
@@ -373,7 +386,22 @@ std::shared_future<Connection> Communicator::connect(const EndpointConfig& local
   auto boot = bootstrap();
   boot->send(&mine, (int)sizeof(mine), remoteRank, connTag(tag));
   const int device = comm_->device;
-  return std::async(std::launch::deferred, [boot, remoteRank, tag, device] {
+  std::shared_ptr<SharedCopyStream> copy;
+  {
+    std::lock_guard<std::mutex> lk(comm_->ipcStreamMu);
+    copy = std::static_pointer_cast<SharedCopyStream>(comm_->ipcStream.lock());
+    if (!copy) {
+      copy = std::make_shared<SharedCopyStream>();
+      int cur = 0;
+      gpuCheck(hipGetDevice(&cur), "hipGetDevice");
+      gpuCheck(hipSetDevice(device), "hipSetDevice");
+      const hipError_t e = hipStreamCreateWithFlags(&copy->stream, hipStreamNonBlocking);
+      gpuCheck(hipSetDevice(cur), "hipSetDevice");
+      gpuCheck(e, "hipStreamCreateWithFlags");
+      comm_->ipcStream = copy;
+    }
+  }
+  return std::async(std::launch::deferred, [boot, remoteRank, tag, device, copy] {
            EndpointWire peer{};
            boot->recv(&peer, (int)sizeof(peer), remoteRank, connTag(tag));
            if (peer.transport != (int32_t)Transport::CudaIpc)
@@ -385,7 +413,8 @@ std::shared_future<Connection> Communicator::connect(const EndpointConfig& local
            int cur = 0;
            gpuCheck(hipGetDevice(&cur), "hipGetDevice");
            gpuCheck(hipSetDevice(device), "hipSetDevice");
-           gpuCheck(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+           impl->copy = copy;
+           impl->stream = copy->stream;
            gpuCheck(hipHostMalloc((void**)&impl->slots, Connection::Impl::kSlots * sizeof(uint64_t),
                                   hipHostMallocDefault),
                     "hipHostMalloc");

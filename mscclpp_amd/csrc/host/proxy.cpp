@@ -136,9 +136,15 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
     Host2DeviceSemaphoreDeviceHandle* dh = nullptr;
     HIPCHECK(hipMalloc((void**)&dh, hh.size() * sizeof(hh[0])));
     HIPCHECK(hipMemcpy(dh, hh.data(), hh.size() * sizeof(hh[0]), hipMemcpyHostToDevice));
+    // One copy stream for every peer (the reference's CUDA branch, connection.cc:126-130), not one per
+    // peer (its HIP branch): HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES (4) hardware
+    // queues, and a stream that lands on the queue of the spinning offload kernel never runs -- with 4
+    // ranks on one GPU the per-peer form hung in the first iteration.
+    hipStream_t copyStream = nullptr;
+    HIPCHECK(hipStreamCreateWithFlags(&copyStream, hipStreamNonBlocking));
     std::vector<Conn> conns(n);
     for (int r = 0; r < n; ++r)
-      if (r != rank) HIPCHECK(hipStreamCreateWithFlags(&conns[r].stream, hipStreamNonBlocking));
+      if (r != rank) conns[r].stream = copyStream;
     uint32_t* err = nullptr;
     HIPCHECK(hipMalloc((void**)&err, 64));
     HIPCHECK(hipMemset(err, 0, 64));
@@ -215,11 +221,8 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
     out[2] = (ok && e == 0 && proxyFailure.empty()) ? 1.0 : 0.0;
     out[3] = (double)proxy.numaNode();
     proxy.stop();
-    for (int r = 0; r < n; ++r)
-      if (conns[r].stream) {
-        (void)hipStreamSynchronize(conns[r].stream);
-        (void)hipStreamDestroy(conns[r].stream);
-      }
+    (void)hipStreamSynchronize(copyStream);
+    (void)hipStreamDestroy(copyStream);
     (void)hipGraphExecDestroy(inst);
     (void)hipGraphDestroy(graph);
     (void)hipStreamDestroy(st);

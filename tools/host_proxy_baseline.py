@@ -28,7 +28,9 @@ def worker(rank, n, uid, size, q):
                                                     ctypes.POINTER(ctypes.c_double)]
         comm = m.Communicator(rank, n, uid)
         out = (ctypes.c_double * 4)()
+        print(f"[host_proxy rank {rank}/{n}] host-offload loop", file=sys.stderr, flush=True)
         m.check(L.mscclppAmdHostOffloadAllGather(comm.comm, size, 10, 10, out), "host offload")
+        print(f"[host_proxy rank {rank}/{n}] PortChannel all-to-all", file=sys.stderr, flush=True)
         res = {"us_per_kernel_nograph": out[0], "us_per_kernel_graph": out[1], "correct": out[2] == 1.0,
                "proxy_numa_node": int(out[3])}
         pc = {}
