@@ -1,6 +1,6 @@
 """Fabric-free latency of the LL AllReduce kernels (BASELINE configs[3] sizes): n ranks in ONE launch
 on one GPU (blockIdx.y = rank, every peer buffer local HBM), fp16, 1 KiB .. 1 MiB, one-hop LL8
-(`allpair`) and two-hop LL16 (`packet`), default launch shapes and the alternatives ALLPAIR_SHAPES / PACKET_SHAPES list ("28x512,...").  Time per
+(`allpair`, up to ALLPAIR_MAX_KB, default 64) and two-hop LL16 (`packet`), default launch shapes and the alternatives ALLPAIR_SHAPES / PACKET_SHAPES list ("28x512,...").  Time per
 call from 20 calls captured in one HIP graph, replayed 10 times (no host launch cost), so what is
 left is the kernel's own latency: its dispatch, the packet stores and the polls of each hop.
 
@@ -59,7 +59,7 @@ def graph_us(fn, calls=20, replays=10):
 rows = []
 for algo, name in ((m.ALGO_ALLPAIR, "allpair"), (m.ALGO_PACKET, "packet")):
     for sz in sizes:
-        if algo == m.ALGO_ALLPAIR and sz > (64 << 10):
+        if algo == m.ALGO_ALLPAIR and sz > (int(os.environ.get("ALLPAIR_MAX_KB", 64)) << 10):
             continue
         c = sz // 2
         ins = [a[:c] for a in ins_all]
