@@ -250,10 +250,12 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
     const int n = comm->nranks, rank = comm->rank;
     if (n < 2) return (int)ncclInvalidArgument;
     const size_t bytes = chunk * n;
-    uint32_t *src = nullptr, *dst = nullptr;
-    HIPCHECK(hipMalloc((void**)&src, bytes));
-    HIPCHECK(hipMalloc((void**)&dst, bytes));
-    HIPCHECK(hipMemset(dst, 0, bytes));
+    // GpuBuffer, as the reference's PortChannel tests allocate (port_channel_tests.cu:209, :241):
+    // uncached on AMD, so the copy engine, the peers' copies and every XCD see one copy of the data.
+    // With cached hipMalloc buffers and 4 ranks sharing one GPU, a peer's copy could sit in an XCD's
+    // L2 when the owner read the buffer back (1 run in 3 lost every peer's chunk on one rank).
+    uint32_t* src = (uint32_t*)allocUncached(bytes);
+    uint32_t* dst = (uint32_t*)allocUncached(bytes);  // zeroed
     std::vector<uint32_t> h(bytes / 4);
     for (size_t i = 0; i < h.size(); ++i) h[i] = (uint32_t)(rank * 0x01000000u + i);  // src chunk q for peer q
     HIPCHECK(hipMemcpy(src, h.data(), bytes, hipMemcpyHostToDevice));
@@ -308,17 +310,24 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
       // check: peer p's chunk addressed to me (its src chunk `rank`) sits at offset p*chunk of my dst
       std::vector<uint32_t> back(bytes / 4);
       HIPCHECK(hipMemcpy(back.data(), dst, bytes, hipMemcpyDeviceToHost));
-      for (int p = 0; p < n && ok; ++p) {
+      std::string bad;
+      for (int p = 0; p < n; ++p) {
         if (p == rank) continue;
+        size_t wrong = 0, first = 0;
         for (size_t i = 0; i < chunk / 4; ++i) {
           const size_t srcElem = (size_t)rank * (chunk / 4) + i;
-          if (back[(size_t)p * (chunk / 4) + i] != (uint32_t)(p * 0x01000000u + srcElem)) {
-            ok = false;
-            break;
-          }
+          if (back[(size_t)p * (chunk / 4) + i] != (uint32_t)(p * 0x01000000u + srcElem) && wrong++ == 0) first = i;
+        }
+        if (wrong) {
+          ok = false;
+          bad += " from rank " + std::to_string(p) + ": " + std::to_string(wrong) + " words wrong (first " +
+                 std::to_string(first) + ", holds " + std::to_string(back[(size_t)p * (chunk / 4) + first]) + ")";
         }
       }
       HIPCHECK(hipMemcpy(&e, comm->err, 4, hipMemcpyDeviceToHost));
+      if (!ok || e)
+        warn("PortChannel all-to-all mode " + std::to_string(mode) + ", rank " + std::to_string(rank) + " of " +
+             std::to_string(n) + ": error word " + std::to_string(e) + bad);
       numa = proxy.proxyNumaNode();
       proxy.stopProxy();
       (void)hipStreamDestroy(st);
