@@ -18,7 +18,7 @@ sys.path.insert(0, {root!r})
 import mscclpp_amd as m
 out = {{}}
 for n, size in ((8, 1024), (8, 16384), (8, 16385), (8, 1 << 20), (8, (1 << 20) + 1), (8, 48 << 20), (4, 48 << 20),
-                (2, 4096)):
+                (2, 4096), (2, 262144), (2, 262145), (2, 1 << 20), (2, 48 << 20), (4, 65536)):
     out[f"ar/{{n}}/{{size}}"] = m.tuned_config("allreduce", n, size)
     out[f"sel/{{n}}/{{size}}"] = m.lib().mscclppAmdSelectAlgo(n, size, 0)
 out["ag"] = m.tuned_config("allgather", 8, 1 << 20)
@@ -48,6 +48,11 @@ def test_builtin_table_restates_the_amd_thresholds(built):
     assert q["sel/8/1024"] == 2 and q["sel/8/16385"] == 1 and q["sel/8/50331648"] == 3
     assert q["ag"][0] == "default_allgather_fullmesh2"
     assert q["bcast"] is None
+    # 2 ranks: one-hop LL8 up to 256 KiB (the same bytes on the one link as LL16, one hop fewer)
+    assert q["ar/2/262144"][0] == "default_allreduce_allpair_packet" and q["sel/2/262144"] == 2
+    assert q["ar/2/262145"][0] == "default_allreduce_packet" and q["ar/2/1048576"][0] == "default_allreduce_packet"
+    assert q["ar/2/50331648"][0] == "default_allreduce_fullmesh"
+    assert q["ar/4/65536"][0] == "default_allreduce_packet"  # other scales: the reference's thresholds
 
 
 def test_user_profile_overrides_by_scale(built, tmp_path):
