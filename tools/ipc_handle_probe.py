@@ -1,3 +1,8 @@
+"""A buffer freed and re-allocated at the same address: does hipIpcGetMemHandle give the same handle?
+(it does not, so the importers' handle-keyed cache maps the new allocation.)
+
+    python tools/ipc_handle_probe.py
+"""
 import ctypes
 H = ctypes.CDLL("libamdhip64.so")
 vp = ctypes.c_void_p
