@@ -113,8 +113,10 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
     const size_t perRank = dataSize / n;
     const size_t nelems = dataSize / 4;
     // data: element i = i+1 in my part, 0 elsewhere (:64-79)
-    int* data = nullptr;
-    HIPCHECK(hipMalloc((void**)&data, dataSize));
+    // uncached (the library's pool) where the reference cudaMallocs (:66): with several ranks on one
+    // GPU (tests, rehearsals) a peer's copy into cached memory can sit in another XCD's L2 when this
+    // rank reads the buffer back (seen in the PortChannel harness below); across GPUs both behave alike
+    int* data = (int*)allocUncached(dataSize);
     std::vector<int> h(nelems, 0);
     for (size_t i = 0; i < nelems; ++i)
       if (i / (perRank / 4) == (size_t)rank) h[i] = (int)(i + 1);
