@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
 // Launch shape of the product kernel for `bytes` (nblocks > 0: the caller's grid), from the
 // same-process shape sweeps (tools/sweep_self_reduce.py, profiles/r3_sweep_self_reduce.json):
 // 4 waves x 1 KiB per workgroup and round, one workgroup per 4 KiB tile up to 1024 workgroups (4 per
-// CU, all resident, so every partner pair is co-resident).
+// CU, all resident, so every partner pair is co-resident); 8 waves per workgroup for 1-4 MiB.
 //  * one round (up to 4 MiB): payload read and written with the default cache policy (a bucket just
 //    written or read by the caller is served from the caches): 3.6-3.7 us at 64-256 KiB, against
 //    4.6 us with one-wave workgroups per KiB and 5.0 us for round 2's 8 KiB tiles;
@@ -186,8 +186,20 @@ struct SelfReduceShape {
 };
 static SelfReduceShape selfReduceShape(uint64_t bytes, int nblocks) {
   SelfReduceShape sh{};
-  sh.waves = 4;
   sh.units = 1;
+  if (nblocks <= 0 && bytes > (1u << 20) && bytes <= (4u << 20)) {
+    // 1-4 MiB: one round of 8-wave workgroups (8 KiB tiles, at most 512 of them) -- half as many
+    // workgroups to dispatch as 4-wave ones: 2 MiB 5.76 against 5.95 us, 3 MiB 7.0 / 7.25,
+    // 4 MiB 7.95 / 8.43 (profiles/r3l_sweep_self_reduce_1_8MiB.json); at 1 MiB the 4-wave form is
+    // ahead (4.53 / 4.76), from 6 MiB they are even
+    sh.waves = 8;
+    const uint64_t tiles8 = (bytes + 8191) / 8192;
+    sh.nblocks = (int)tiles8 + (int)(tiles8 % 2);
+    sh.skew = 0;
+    sh.plain = true;
+    return sh;
+  }
+  sh.waves = 4;
   const uint64_t tiles = (bytes + 4095) / 4096;
   sh.nblocks = nblocks > 0 ? nblocks : (int)(tiles < 1024 ? tiles : 1024);
   if (sh.nblocks % 2) sh.nblocks += 1;
@@ -209,7 +221,10 @@ template <int DT, int OP>
 static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                              int nblocks, uint64_t budget, uint32_t* err, hipStream_t stream) {
   const SelfReduceShape sh = selfReduceShape(bytes, nblocks);
-  if (sh.plain)
+  if (sh.waves == 8)
+    launchSelfReduceShape<DT, OP, 8, 1, 0, false, kPlain>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err,
+                                                              nullptr, stream);
+  else if (sh.plain)
     launchSelfReduceShape<DT, OP, 4, 1, 0, false, kPlain>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err,
                                                               nullptr, stream);
   else if (sh.skew == 2)

@@ -92,13 +92,14 @@ def test_self_reduce_rejects_unaligned(built):
     assert e.value.code == 4
 
 
-@pytest.mark.parametrize("nbytes,nblocks,skew", [(16, 2, 0), (4 << 20, 1024, 0), ((4 << 20) + 16, 1024, 0),
-                                                 ((8 << 20) + 16, 1024, 1), ((24 << 20) + 16, 1024, 1),
-                                                 ((32 << 20) + 16, 1024, 2), (48 << 20, 1024, 2)])
-def test_self_reduce_default_shape(built, nbytes, nblocks, skew):
+@pytest.mark.parametrize("nbytes,waves,nblocks,skew", [
+    (16, 4, 2, 0), (1 << 20, 4, 256, 0), ((1 << 20) + 48, 8, 130, 0), (4 << 20, 8, 512, 0),
+    ((4 << 20) + 16, 4, 1024, 0), ((8 << 20) + 16, 4, 1024, 1), ((24 << 20) + 16, 4, 1024, 1),
+    ((32 << 20) + 16, 4, 1024, 2), (48 << 20, 4, 1024, 2)])
+def test_self_reduce_default_shape(built, nbytes, waves, nblocks, skew):
     """The launch shape the product entry picks (4 waves x 1 KiB, one workgroup per 4 KiB up to 1024,
-    partner tiles consumed one round late from three rounds per workgroup on, two rounds late from
-    eight)."""
+    8-wave workgroups for one round of 8 KiB tiles above 1 MiB up to 4 MiB, partner tiles consumed
+    one round late from three rounds per workgroup on, two rounds late from eight)."""
     import ctypes
 
     import mscclpp_amd as m
@@ -106,7 +107,7 @@ def test_self_reduce_default_shape(built, nbytes, nblocks, skew):
     w, u, nb, sk = (ctypes.c_int() for _ in range(4))
     m.check(m.lib().mscclppAmdSelfReduceLL16DefaultShape(nbytes, ctypes.byref(w), ctypes.byref(u), ctypes.byref(nb),
                                                          ctypes.byref(sk)), "default shape")
-    assert (w.value, u.value, nb.value, sk.value) == (4, 1, nblocks, skew)
+    assert (w.value, u.value, nb.value, sk.value) == (waves, 1, nblocks, skew)
 
 
 

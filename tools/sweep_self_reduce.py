@@ -91,7 +91,7 @@ def candidates(S):
                 continue
             rounds = -(-tiles // nb)
             c.append((w, u, 1 if rounds >= 3 else 0, nb))
-            if rounds == 1 and w == 4:  # the one-round form with default-policy payload accesses
+            if rounds == 1 and w in (4, 8):  # the one-round form with default-policy payload accesses
                 c.append((w, u, 0, nb, 2))
             if rounds >= 4 and w == 4:  # partner tiles consumed two rounds late
                 c.append((w, u, 2, nb))
