@@ -11,9 +11,10 @@
 //
 // The built-in table restates algorithm_selector.cc:91-139 (AMD branch) as data: <= 16 KiB one-hop
 // LL8, <= 1 MiB two-hop LL16, larger the bulk all-pairs path.  At 2 ranks (its own profile) one-hop
-// LL8 holds up to 256 KiB: there both LL forms put the same bytes on the one link, and the one hop
-// measured 4.0 against 5.2-5.4 us at 1-128 KiB, equal at 256 KiB, slower from 512 KiB
-// (profiles/r3k_inprocess_ll_probe_n2_ll8.json, 2 ranks in one launch, fabric-free).  MSCCLPP_AMD_TUNED_CONFIG names a file
+// LL8 takes the whole LL range: there both LL forms put the same bytes on the one link, and the one
+// hop measured 4.0-4.2 against 5.2-5.6 us at 1-256 KiB, 4.4 / 6.2 against 7.3 / 9.5 us at 512 KiB /
+// 1 MiB (profiles/r3k_inprocess_ll_probe_n2_ll8.json, r3n_inprocess_ll8_probe_n2_shapes.json,
+// 2 ranks in one launch, fabric-free).  MSCCLPP_AMD_TUNED_CONFIG names a file
 // whose profiles are consulted first (e.g. the `tuned_config` that bench.py prints after tuning on
 // the node); mscclppAmdTunedConfigLoad does the same at run time.
 #include <fstream>
@@ -41,7 +42,6 @@ struct Profile {
 const char* kBuiltin = R"({"version": 1, "profiles": [
   {"scale": 2, "collectives": {"allreduce": [
       {"message_size": 1, "algorithm": "default_allreduce_allpair_packet"},
-      {"message_size": 262145, "algorithm": "default_allreduce_packet"},
       {"message_size": 1048577, "algorithm": "default_allreduce_fullmesh"}]}},
   {"collectives": {
     "allreduce": [

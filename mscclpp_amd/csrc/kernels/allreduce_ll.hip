@@ -588,13 +588,17 @@ static void ll16Defaults(int nranks, size_t bytes, int& nblocks, int& nthreads) 
   if (nblocks < nPeers) nblocks = nPeers;
 }
 
+// LL8: one lane per 16-byte unit, up to 128 workgroups; 256 lanes up to 128 KiB, 512 above (round 3:
+// at 2 ranks, where the selector keeps the one-hop form up to 1 MiB, the round-2 cap of 64 x 256 lanes
+// left 512 KiB - 1 MiB to 2-4 passes: 8.7 / 15.1 us against 4.4 / 6.2 us on 128 x 512,
+// profiles/r3n_inprocess_ll8_probe_n2_shapes.json).
 static void ll8Defaults(int nranks, size_t bytes, int& nblocks, int& nthreads) {
   const LL8Geom g = ll8Geometry(bytes, kF16);
-  if (nthreads <= 0) nthreads = 256;
+  if (nthreads <= 0) nthreads = g.units <= 16384 ? 256 : 512;
   if (nblocks <= 0) {
     uint64_t want = (g.units + nthreads - 1) / nthreads;
     if (want < 1) want = 1;
-    if (want > 64) want = 64;
+    if (want > 128) want = 128;
     nblocks = (int)want;
   }
   (void)nranks;

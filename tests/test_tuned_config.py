@@ -48,9 +48,10 @@ def test_builtin_table_restates_the_amd_thresholds(built):
     assert q["sel/8/1024"] == 2 and q["sel/8/16385"] == 1 and q["sel/8/50331648"] == 3
     assert q["ag"][0] == "default_allgather_fullmesh2"
     assert q["bcast"] is None
-    # 2 ranks: one-hop LL8 up to 256 KiB (the same bytes on the one link as LL16, one hop fewer)
+    # 2 ranks: one-hop LL8 over the whole LL range (the same bytes on the one link as LL16, one hop fewer)
     assert q["ar/2/262144"][0] == "default_allreduce_allpair_packet" and q["sel/2/262144"] == 2
-    assert q["ar/2/262145"][0] == "default_allreduce_packet" and q["ar/2/1048576"][0] == "default_allreduce_packet"
+    assert q["ar/2/262145"][0] == "default_allreduce_allpair_packet"
+    assert q["ar/2/1048576"][0] == "default_allreduce_allpair_packet"
     assert q["ar/2/50331648"][0] == "default_allreduce_fullmesh"
     assert q["ar/4/65536"][0] == "default_allreduce_packet"  # other scales: the reference's thresholds
 
