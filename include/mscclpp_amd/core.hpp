@@ -103,6 +103,12 @@ class RegisteredMemory {
   size_t size() const;
   TransportFlags transports() const;
   int rank() const;  // owner
+  // The owner's buffer is coherent with copies made by another agent while a kernel runs: a block
+  // of the uncached pool (GpuBuffer, mscclppAmdMallocUncached) or host memory.  A PortChannel
+  // destination must be coherent for a running kernel to read what the proxy delivered after
+  // wait(); cached device memory (hipMalloc) is guaranteed only to the host and to kernels launched
+  // after the receiving one.
+  bool coherent() const;
   std::vector<char> serialize() const;
   static RegisteredMemory deserialize(const std::vector<char>& data);
   struct Impl;

@@ -97,6 +97,13 @@ int mscclppAmdMallocUncached(void** ptr, size_t bytes);
 int mscclppAmdMalloc(void** ptr, size_t bytes);
 int mscclppAmdFree(void* ptr);
 int mscclppAmdUncachedPoolStats(size_t* held, size_t* inUse, size_t* freeBytes);
+/* Imports of peers' memory in this process: IPC mappings open now, and how many of them are kept
+ * imports of peers' pooled uncached blocks (scratch, tokens, GpuBuffer), which stay mapped until
+ * the process exits -- the import-side twin of the pool.  mscclppAmdIpcKeptRanges
+ * writes up to `cap` (mapped address, bytes) pairs of the kept imports and their count to *n.  Any
+ * pointer may be NULL. */
+int mscclppAmdIpcStats(size_t* openMappings, size_t* keptImports);
+int mscclppAmdIpcKeptRanges(uint64_t* addrs, uint64_t* bytes, size_t cap, size_t* n);
 int mscclppAmdFlagsInit(uint32_t* flags, void* stream);
 
 /* ---- 1-GPU microbench (BASELINE config 2) ------------------------------------------------- */

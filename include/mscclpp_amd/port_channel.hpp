@@ -52,6 +52,7 @@ class ProxyService : public BaseProxyService {
   struct ConnState;
   std::vector<std::shared_ptr<Host2DeviceSemaphore>> semaphores_;
   std::vector<RegisteredMemory> memories_;
+  bool warnedDst_ = false;  // a non-coherent PortChannel destination was reported (channels.cpp)
   std::unordered_map<const void*, std::shared_ptr<ConnState>> conns_;  // per connection: flushDonePos
   std::vector<std::shared_ptr<ConnState>> semConn_;                    // per semaphore id
   std::shared_ptr<Proxy> proxy_;

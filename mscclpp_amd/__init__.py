@@ -96,6 +96,9 @@ def lib():
         "mscclppAmdMallocUncached": [ctypes.POINTER(vp), sz],
         "mscclppAmdMalloc": [ctypes.POINTER(vp), sz],
         "mscclppAmdFree": [vp],
+        "mscclppAmdUncachedPoolStats": [ctypes.POINTER(sz), ctypes.POINTER(sz), ctypes.POINTER(sz)],
+        "mscclppAmdIpcStats": [ctypes.POINTER(sz), ctypes.POINTER(sz)],
+        "mscclppAmdIpcKeptRanges": [ctypes.POINTER(u64), ctypes.POINTER(u64), sz, ctypes.POINTER(sz)],
         "mscclppAmdTraceSet": [vp, sz],
         "mscclppAmdFlagsInit": [vp, vp],
         "mscclppAmdSelfReduceLL16": [vp, vp, vp, vp, sz, i32, i32, vp, i32, u64, vp, vp],
@@ -204,6 +207,30 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+def pool_stats():
+    """(held, in use, free) bytes of the process-lifetime uncached pool (mscclppAmdUncachedPoolStats)."""
+    a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    check(lib().mscclppAmdUncachedPoolStats(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "pool stats")
+    return a.value, b.value, c.value
+
+
+def ipc_stats():
+    """(IPC mappings open in this process, of which kept imports of peers' pooled blocks)."""
+    a, b = ctypes.c_size_t(), ctypes.c_size_t()
+    check(lib().mscclppAmdIpcStats(ctypes.byref(a), ctypes.byref(b)), "ipc stats")
+    return a.value, b.value
+
+
+def ipc_kept_ranges():
+    """[(mapped address, bytes)] of the kept imports of peers' pooled uncached blocks."""
+    n = ctypes.c_size_t()
+    check(lib().mscclppAmdIpcKeptRanges(None, None, 0, ctypes.byref(n)), "ipc kept ranges")
+    cap = n.value
+    addrs, sizes = (ctypes.c_uint64 * max(cap, 1))(), (ctypes.c_uint64 * max(cap, 1))()
+    check(lib().mscclppAmdIpcKeptRanges(addrs, sizes, cap, ctypes.byref(n)), "ipc kept ranges")
+    return [(addrs[i], sizes[i]) for i in range(min(cap, n.value))]
 
 
 def flags_init(flags_tensor, stream=None):

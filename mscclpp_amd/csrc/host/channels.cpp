@@ -208,9 +208,38 @@ BasePortChannel ProxyService::basePortChannel(SemaphoreId id) {
   return BasePortChannel(id, semaphores_.at(id), proxy_, semConn_.at(id)->dFlushDone);
 }
 
+// The destination contract of a PortChannel.  The proxy's copy
+// engine writes the destination behind the receiving GPU's L2, so a kernel that is running when the
+// data lands reads it reliably only from coherent memory: the uncached pool (GpuBuffer,
+// mscclppAmdMallocUncached -- what the reference's PortChannel tests allocate on AMD,
+// port_channel_tests.cu:209, :241) or host memory.  Data put into cached device memory (hipMalloc,
+// torch) is complete for the host and for kernels launched after the receiving one, as the
+// reference's customized AllGather example uses it.  MSCCLPP_AMD_PORT_CHANNEL_DST chooses what a
+// non-coherent destination gets: "warn" (default: one warning per ProxyService), "strict"
+// (InvalidUsage) or "off".
+static int portChannelDstPolicy() {
+  const char* e = std::getenv("MSCCLPP_AMD_PORT_CHANNEL_DST");
+  if (!e) return 1;
+  const std::string s(e);
+  return s == "off" ? 0 : s == "strict" ? 2 : 1;
+}
+
 PortChannel ProxyService::portChannel(SemaphoreId id, MemoryId dst, MemoryId src) {
   if (dst >= memories_.size() || src >= memories_.size())
     throw Error("ProxyService::portChannel: unknown memory id", ErrorCode::InvalidUsage);
+  if (!memories_[dst].coherent()) {
+    const int policy = portChannelDstPolicy();
+    const std::string what = "PortChannel destination (memory id " + std::to_string(dst) + ", rank " +
+                             std::to_string(memories_[dst].rank()) +
+                             ") is cached device memory: what the proxy puts there is visible to the host and to "
+                             "kernels launched after the receiving one, not to reads of a running kernel after "
+                             "wait(); allocate it with GpuBuffer / mscclppAmdMallocUncached for that";
+    if (policy == 2) throw Error(what + " (MSCCLPP_AMD_PORT_CHANNEL_DST=strict)", ErrorCode::InvalidUsage);
+    if (policy == 1 && !warnedDst_) {
+      warnedDst_ = true;
+      host::warn(what);
+    }
+  }
   return PortChannel(id, semaphores_.at(id), proxy_, semConn_.at(id)->dFlushDone, dst, src);
 }
 

@@ -32,7 +32,32 @@ int mscclppAmdMalloc(void** ptr, size_t bytes) {
 
 int mscclppAmdFree(void* ptr) {
   return guarded([&] {
-    if (ptr && !releaseUncached(ptr)) HIPCHECK(hipFree(ptr));
+    hipError_t syncErr = hipSuccess;
+    if (ptr && !releaseUncached(ptr, &syncErr)) HIPCHECK(hipFree(ptr));
+    HIPCHECK(syncErr);
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdIpcStats(size_t* openMappings, size_t* keptImports) {
+  return guarded([&] {
+    std::vector<std::pair<uint64_t, uint64_t>> kept;
+    keptIpcImports(&kept);
+    if (openMappings) *openMappings = liveIpcMappings();
+    if (keptImports) *keptImports = kept.size();
+    return (int)ncclSuccess;
+  });
+}
+
+int mscclppAmdIpcKeptRanges(uint64_t* addrs, uint64_t* bytes, size_t cap, size_t* n) {
+  return guarded([&] {
+    std::vector<std::pair<uint64_t, uint64_t>> kept;
+    keptIpcImports(&kept);
+    for (size_t i = 0; i < kept.size() && i < cap; ++i) {
+      if (addrs) addrs[i] = kept[i].first;
+      if (bytes) bytes[i] = kept[i].second;
+    }
+    if (n) *n = kept.size();
     return (int)ncclSuccess;
   });
 }
@@ -254,24 +279,34 @@ ncclResult_t ncclCommFinalize(ncclComm_t comm) {
   return ncclSuccess;
 }
 
+// The communicator is deleted whatever the teardown reports: a failed step is returned as the
+// result, never left behind as a half-destroyed handle.
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (!comm) return ncclInvalidArgument;
-  return (ncclResult_t)guarded([&] {
+  const int a = guarded([&] {
     destroyFallbackComm(comm, false);
-    comm->destroy();
-    delete comm;
     return (int)ncclSuccess;
   });
+  const int b = guarded([&] {
+    comm->destroy();
+    return (int)ncclSuccess;
+  });
+  delete comm;
+  return (ncclResult_t)(a != ncclSuccess ? a : b);
 }
 
 ncclResult_t ncclCommAbort(ncclComm_t comm) {
   if (!comm) return ncclSuccess;
-  return (ncclResult_t)guarded([&] {
+  const int a = guarded([&] {
     destroyFallbackComm(comm, true);
-    comm->destroy();
-    delete comm;
     return (int)ncclSuccess;
   });
+  const int b = guarded([&] {
+    comm->destroy();
+    return (int)ncclSuccess;
+  });
+  delete comm;
+  return (ncclResult_t)(a != ncclSuccess ? a : b);
 }
 
 const char* ncclGetErrorString(ncclResult_t result) {

@@ -124,12 +124,14 @@ inline size_t bulkScratchInitBytes() {
 
 // Uncached device memory (hipDeviceMallocUncached, zeroed) from the process-lifetime pool
 // (uncached_pool.cpp: never returned to HIP while the process runs).  freeDevice
-// returns a pooled block to the pool and hipFree's anything else; releaseUncached is false for a
-// pointer the pool does not own.
+// returns a pooled block to the pool and hipFree's anything else, and never throws (destructors
+// call it); releaseUncached is false for a pointer the pool does not own, and reports in
+// *syncError a failed synchronize of the owning device (the block is then leaked, not reused).
 void* allocUncached(size_t bytes);
-bool releaseUncached(void* p);
-void freeDevice(void* p);
+bool releaseUncached(void* p, hipError_t* syncError) noexcept;
+void freeDevice(void* p) noexcept;
 void uncachedPoolStats(size_t* held, size_t* inUse, size_t* freeBytes);
+bool isPooledUncached(const void* base);  // `base` is a live block of the pool (an allocation base)
 
 inline int dtypeFromNccl(ncclDataType_t t) {
   switch (t) {
@@ -206,6 +208,14 @@ namespace host {
 // is opened once per process however many owners hold it, and closed when the last owner drops
 // its reference.  Implemented in core.cpp.
 std::shared_ptr<void> openIpcHandle(const hipIpcMemHandle_t& handle);
+// An import of a peer's allocation (base, bytes) exported by process `owner` (its processNonce).
+// pooled: the owner's uncached pool holds the block for its whole life, so the mapping is kept open
+// for the life of this process and reused by later exports of the same block (core.cpp); otherwise
+// openIpcHandle.
+std::shared_ptr<void> openIpcImport(const hipIpcMemHandle_t& handle, uint64_t owner, uint64_t base, uint64_t bytes,
+                                    bool pooled);
+uint64_t processNonce();  // random, fixed per process: tells exporters' pools apart
+void keptIpcImports(std::vector<std::pair<uint64_t, uint64_t>>* ranges);  // (mapped address, bytes)
 size_t liveIpcMappings();
 uint64_t allocationId(const void* ptr);  // HIP_POINTER_ATTRIBUTE_BUFFER_ID (0 if unknown)
 // Tuned configuration (tuning.cpp) for a collective of `bytes` on `nranks` ranks of this device's
@@ -230,7 +240,29 @@ struct IpcBlob {
   uint64_t base;    // allocation base in the owner's address space (cache key)
   uint64_t offset;  // pointer - base
   uint64_t bytes;
+  uint64_t owner;   // the exporting process's processNonce()
+  uint32_t pooled;  // the allocation is a block of the owner's uncached pool (kept-open import)
+  uint32_t pad;
 };
+
+// This process's export record of the allocation holding `ptr`.
+inline IpcBlob exportBlob(const void* ptr) {
+  IpcBlob b{};
+  void* base = nullptr;
+  size_t sz = 0;
+  HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)ptr));
+  HIPCHECK(hipIpcGetMemHandle(&b.handle, base));
+  b.base = (uint64_t)base;
+  b.offset = (uint64_t)((const char*)ptr - (char*)base);
+  b.bytes = sz;
+  b.owner = processNonce();
+  b.pooled = isPooledUncached(base) ? 1u : 0u;
+  return b;
+}
+
+inline std::shared_ptr<void> importBlob(const IpcBlob& b) {
+  return openIpcImport(b.handle, b.owner, b.base, b.bytes, b.pooled != 0);
+}
 
 struct ncclComm {
   std::unique_ptr<TcpBootstrap> boot;
@@ -273,18 +305,12 @@ struct ncclComm {
   // mapped by several owners is opened once; a peer that freed an allocation and got a new one at
   // the same address sends a new handle, which maps afresh.
   PeerBufs exchange(void* ptr) {
-    IpcBlob mine{};
-    void* base = nullptr;
-    size_t sz = 0;
-    HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)ptr));
+    const IpcBlob mine = exportBlob(ptr);
     if (std::getenv("MSCCLPP_AMD_DEBUG_IPC"))
-      std::fprintf(stderr, "ipc rank %d export ptr %p base %p bytes %zu id %llu\n", rank, ptr, base, sz,
-                   (unsigned long long)allocationId(base));
-    HIPCHECK(hipIpcGetMemHandle(&mine.handle, base));
+      std::fprintf(stderr, "ipc rank %d export ptr %p base %llx bytes %llu id %llu pooled %u\n", rank, ptr,
+                   (unsigned long long)mine.base, (unsigned long long)mine.bytes,
+                   (unsigned long long)allocationId((void*)mine.base), mine.pooled);
     info("rank " + std::to_string(rank) + ": got ipc handle, all-gather");
-    mine.base = (uint64_t)base;
-    mine.offset = (uint64_t)((char*)ptr - (char*)base);
-    mine.bytes = sz;
     std::vector<IpcBlob> all(nranks);
     boot->allGather(&mine, all.data(), sizeof(IpcBlob));
     PeerBufs res;
@@ -293,7 +319,7 @@ struct ncclComm {
         res[r] = ptr;
         continue;
       }
-      res.maps[(size_t)r] = openIpcHandle(all[r].handle);
+      res.maps[(size_t)r] = importBlob(all[r]);
       res[r] = (char*)res.maps[(size_t)r].get() + all[r].offset;
     }
     if (std::getenv("MSCCLPP_AMD_DEBUG_IPC")) {  // one line per peer: what was imported and where
@@ -330,8 +356,19 @@ struct ncclComm {
   // bulk scratch grew 64 -> 128 MiB, two ranks' peers wrote the pipeline's stages into the old
   // buffer, tools/multi_rank_check.py).  Growth is geometric, so what is kept is at most the final size.
   std::vector<void*> outgrown;
-  void ensure(void*& buf, size_t& have, PeerBufs& peers, size_t need) {
+  //
+  // Growth synchronizes the device and allocates, so it cannot happen inside a HIP graph capture:
+  // a call that would grow while `stream` captures fails with ncclInvalidUsage instead (run the
+  // same call once eagerly before capturing, and the scratch is already large enough).
+  void ensure(void*& buf, size_t& have, PeerBufs& peers, size_t need, hipStream_t stream = nullptr) {
     if (need <= have) return;
+    if (stream) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        throw std::logic_error("scratch must grow to " + std::to_string(need) +
+                               " bytes, which cannot happen while the stream is capturing a graph: run this call "
+                               "once before capture");
+    }
     size_t want = have ? have : (size_t)64 << 20;
     while (want < need) want *= 2;
     HIPCHECK(hipDeviceSynchronize());
@@ -448,15 +485,8 @@ struct ncclComm {
   // consistent across ranks.
   int broadcast(const void* send, void* recv, size_t bytes, int root, int nblocks, int nthreads, hipStream_t stream) {
     std::lock_guard<std::mutex> lk(mu);
-    void* mine = rank == root ? const_cast<void*>(send) : recv;
-    IpcBlob blob{};
-    void* base = nullptr;
-    size_t sz = 0;
-    HIPCHECK(hipMemGetAddressRange((hipDeviceptr_t*)&base, &sz, (hipDeviceptr_t)mine));
-    HIPCHECK(hipIpcGetMemHandle(&blob.handle, base));
-    blob.base = (uint64_t)base;
-    blob.offset = (uint64_t)((char*)mine - (char*)base);
-    blob.bytes = sz;
+    const void* mine = rank == root ? send : recv;
+    const IpcBlob blob = exportBlob(mine);
     std::vector<IpcBlob> all(nranks);
     boot->allGather(&blob, all.data(), sizeof(IpcBlob));
     mscclppAmdRankView v = baseView(rank == root ? send : recv, recv);
@@ -464,7 +494,7 @@ struct ncclComm {
       // the mapping stays referenced until a later broadcast from the same root replaces it (and
       // is then retired: the kernel below may still be queued).  A mapping used under stream
       // capture is kept until dropUserRegistrations instead: the graph's replays read through it.
-      auto m = openIpcHandle(all[root].handle);
+      auto m = importBlob(all[root]);
       auto& slot = bcastMaps[(size_t)root];
       bool& captured = bcastCaptured[(size_t)root];  // sticky while the same mapping stays in the slot
       if (slot && slot != m) {
@@ -543,7 +573,7 @@ struct ncclComm {
                           : algo == MSCCLPP_AMD_ALGO_ALLPAIR ? ll8ScratchRequired(nranks, bytes, dtype)
                                                              : testLLScratchRequired(nranks, bytes);
       if (need == 0) return ncclInvalidUsage;
-      ensure(llScratch, llBytes, peerLL, need);
+      ensure(llScratch, llBytes, peerLL, need, stream);
       v.scratch = llScratch;
       v.scratchBytes = llBytes;
       for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerLL[r];
@@ -554,7 +584,7 @@ struct ncclComm {
       size_t need = bytes + 16 * (size_t)nranks * 64;
       const size_t cap = bulkBytes;
       if (need > cap) need = cap;
-      ensure(bulkScratch, bulkBytes, peerBulk, need);
+      ensure(bulkScratch, bulkBytes, peerBulk, need, stream);
       v.scratch = bulkScratch;
       v.scratchBytes = bulkBytes;
       for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
@@ -575,7 +605,7 @@ struct ncclComm {
       // every remote store lands in the bulk scratch: no user-buffer registration at all
       size_t need = 2 * bytes + 16 * (size_t)nranks * 64;
       if (need > bulkBytes) need = bulkBytes;  // fewer stages, never a re-allocation
-      ensure(bulkScratch, bulkBytes, peerBulk, need);
+      ensure(bulkScratch, bulkBytes, peerBulk, need, stream);
       v.scratch = bulkScratch;
       v.scratchBytes = bulkBytes;
       for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];
@@ -614,7 +644,7 @@ struct ncclComm {
     size_t need = total + 16 * (size_t)nranks * 64;
     const size_t cap = bulkBytes;
     if (need > cap) need = cap;
-    ensure(bulkScratch, bulkBytes, peerBulk, need);
+    ensure(bulkScratch, bulkBytes, peerBulk, need, stream);
     v.scratch = bulkScratch;
     v.scratchBytes = bulkBytes;
     for (int r = 0; r < nranks; ++r) v.peerScratch[r] = peerBulk[r];

@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <random>
 #include <unordered_map>
 
 #include "comm_internal.hpp"
@@ -69,6 +70,57 @@ size_t liveIpcMappings() {
   size_t n = 0;
   for (auto& kv : gIpcOpen) n += kv.second.expired() ? 0 : 1;
   return n;
+}
+
+uint64_t processNonce() {
+  static const uint64_t nonce = [] {
+    std::random_device rd;
+    uint64_t v = ((uint64_t)rd() << 32) ^ rd();
+    v ^= (uint64_t)getpid() * 0x9e3779b97f4a7c15ull;
+    v ^= (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    return v ? v : 1;
+  }();
+  return nonce;
+}
+
+namespace {
+// Imports of peers' pooled uncached blocks, kept mapped for the life of this process: the import-side
+// twin of the pool (uncached_pool.cpp).  The owner never returns such a block to HIP
+// while it runs, so (owner process, base, bytes) names the same memory for as long as the owner
+// lives, and a later export of the same block -- a re-created communicator getting the same scratch
+// back from the owner's pool -- finds its mapping here instead of opening a new one.  A mapping of
+// uncached memory is therefore never closed, so its virtual range is never handed to another
+// allocation of this process.  Bounded by the peers' pools (what their blocks peaked at).
+struct Kept {
+  std::shared_ptr<void> map;
+  uint64_t bytes;
+};
+std::mutex gKeptMu;
+std::map<std::pair<uint64_t, uint64_t>, Kept> gKept;  // (owner, base) -> mapping
+}  // namespace
+
+std::shared_ptr<void> openIpcImport(const hipIpcMemHandle_t& handle, uint64_t owner, uint64_t base, uint64_t bytes,
+                                    bool pooled) {
+  if (!pooled || !owner) return openIpcHandle(handle);
+  std::lock_guard<std::mutex> lk(gKeptMu);
+  const auto key = std::make_pair(owner, base);
+  auto it = gKept.find(key);
+  if (it != gKept.end()) return it->second.map;
+  auto p = openIpcHandle(handle);
+  if (!bytes) {  // the caller knows only the registered range: ask HIP for the mapping's extent
+    void* b = nullptr;
+    size_t sz = 0;
+    if (hipMemGetAddressRange((hipDeviceptr_t*)&b, &sz, (hipDeviceptr_t)p.get()) == hipSuccess) bytes = sz;
+    else (void)hipGetLastError();
+  }
+  gKept.emplace(key, Kept{p, bytes});  // never erased: the mapping stays open until the process exits
+  return p;
+}
+
+void keptIpcImports(std::vector<std::pair<uint64_t, uint64_t>>* ranges) {
+  std::lock_guard<std::mutex> lk(gKeptMu);
+  ranges->clear();
+  for (const auto& kv : gKept) ranges->emplace_back((uint64_t)kv.second.map.get(), kv.second.bytes);
 }
 
 uint64_t allocationId(const void* ptr) {
@@ -137,6 +189,9 @@ struct RegisteredMemory::Impl {
   int32_t pid = 0;
   hipIpcMemHandle_t handle{};
   uint64_t offset = 0;       // original - allocation base
+  uint64_t owner = 0;        // the owner process's processNonce()
+  bool pooled = false;       // the allocation is a block of the owner's uncached pool
+  bool coherent = false;     // pooled, or host memory (RegisteredMemory::coherent)
   std::shared_ptr<void> map;  // the IPC mapping (received from another process)
 };
 
@@ -149,6 +204,9 @@ struct MemWire {
   uint64_t original;
   uint64_t size;
   uint64_t offset;
+  uint64_t owner;
+  uint32_t flags;  // bit 0: pooled, bit 1: coherent
+  uint32_t pad;
   hipIpcMemHandle_t handle;
 };
 }  // namespace
@@ -158,6 +216,7 @@ void* RegisteredMemory::originalDataPtr() const { return pimpl_ ? (void*)pimpl_-
 size_t RegisteredMemory::size() const { return pimpl_ ? (size_t)pimpl_->size : 0; }
 TransportFlags RegisteredMemory::transports() const { return pimpl_ ? pimpl_->transports : TransportFlags(); }
 int RegisteredMemory::rank() const { return pimpl_ ? pimpl_->rank : -1; }
+bool RegisteredMemory::coherent() const { return pimpl_ && pimpl_->coherent; }
 
 std::vector<char> RegisteredMemory::serialize() const {
   if (!pimpl_) throw Error("serialize: empty RegisteredMemory", ErrorCode::InvalidUsage);
@@ -169,6 +228,8 @@ std::vector<char> RegisteredMemory::serialize() const {
   w.original = pimpl_->original;
   w.size = pimpl_->size;
   w.offset = pimpl_->offset;
+  w.owner = pimpl_->owner;
+  w.flags = (pimpl_->pooled ? 1u : 0u) | (pimpl_->coherent ? 2u : 0u);
   w.handle = pimpl_->handle;
   return std::vector<char>((char*)&w, (char*)&w + sizeof(w));
 }
@@ -186,11 +247,14 @@ RegisteredMemory RegisteredMemory::deserialize(const std::vector<char>& data) {
   impl->pid = w.pid;
   impl->handle = w.handle;
   impl->offset = w.offset;
+  impl->owner = w.owner;
+  impl->pooled = (w.flags & 1u) != 0;
+  impl->coherent = (w.flags & 2u) != 0;
   if (w.pid == (int32_t)getpid()) {
     impl->data = (void*)w.original;  // same process (in-process ranks): the pointer is usable as is
   } else {
     try {
-      impl->map = host::openIpcHandle(w.handle);
+      impl->map = host::openIpcImport(w.handle, w.owner, w.original - w.offset, 0, impl->pooled);
     } catch (const host::HipError& e) {
       throw Error(std::string("RegisteredMemory::deserialize: ") + e.what(), ErrorCode::SystemError);
     }
@@ -341,6 +405,16 @@ RegisteredMemory Communicator::registerMemory(void* ptr, size_t size, TransportF
   impl->transports = transports;
   impl->rank = comm_->rank;
   impl->pid = (int32_t)getpid();
+  impl->owner = host::processNonce();
+  {
+    hipPointerAttribute_t attr{};
+    if (hipPointerGetAttributes(&attr, ptr) == hipSuccess) {
+      impl->coherent = attr.type == hipMemoryTypeHost;
+    } else {
+      (void)hipGetLastError();
+      impl->coherent = true;  // pageable host memory, unknown to HIP
+    }
+  }
   if (transports.has(Transport::CudaIpc)) {
     void* base = nullptr;
     size_t range = 0;
@@ -351,6 +425,8 @@ RegisteredMemory Communicator::registerMemory(void* ptr, size_t size, TransportF
       throw Error(std::string("registerMemory: not a device allocation (") + hipGetErrorString(e) + ")",
                   ErrorCode::InvalidUsage);
     impl->offset = (uint64_t)((char*)ptr - (char*)base);
+    impl->pooled = host::isPooledUncached(base);
+    if (impl->pooled) impl->coherent = true;
   }
   return RegisteredMemory(impl);
 }

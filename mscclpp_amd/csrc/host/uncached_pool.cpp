@@ -8,8 +8,14 @@
 // result came back wrong through .cpu() (k5 in the full `-m gpu` session, 6 of 6 sessions; the
 // buffer sat exactly where 1-2 MiB uncached buffers had been allocated and freed).  Uncached memory
 // is therefore never returned to HIP while the process runs: a freed block goes to a free list
-// (after a device synchronize, as hipFree does) and is handed out again, zeroed, for a later request
-// of its size class.  MSCCLPP_AMD_UC_POOL=0 restores hipFree (diagnosis only).
+// (after a synchronize of the device that owns it, as hipFree does) and is handed out again, its
+// requested bytes zeroed, for a later request of its size class on the same device.
+//
+// Size classes: powers of two from 64 KiB up to 64 MiB; above that, multiples of 2 MiB (a 129 MiB
+// scratch holds 130 MiB, not 256).  A large request is served best-fit by a free block of at most
+// 5/4 of its class.  The held bytes are bounded by the peak of what was live at once, per class
+// (INTEGRATION.md §5); mscclppAmdUncachedPoolStats reports them.
+// MSCCLPP_AMD_UC_POOL=0 restores hipFree (diagnosis only).
 #include "comm_internal.hpp"
 
 #include <unordered_map>
@@ -18,11 +24,18 @@ namespace mscclpp_amd {
 namespace host {
 namespace {
 
+struct Block {
+  int device;
+  size_t cls;
+};
+
 struct UncachedPool {
   std::mutex mu;
-  std::multimap<size_t, void*> freeBlocks;   // class bytes -> block
-  std::unordered_map<void*, size_t> live;    // block -> class bytes
-  size_t held = 0;                           // bytes allocated from HIP and never freed
+  std::map<std::pair<int, size_t>, std::vector<void*>> freeBlocks;  // (device, class bytes) -> blocks
+  std::unordered_map<void*, Block> live;                            // block -> owner device, class
+  std::map<int, hipStream_t> zeroStreams;  // per device: the stream the zero fill runs on
+  size_t held = 0;                         // bytes allocated from HIP and never freed
+  size_t leaked = 0;                       // bytes dropped because their device could not synchronize
   bool enabled = [] {
     const char* e = std::getenv("MSCCLPP_AMD_UC_POOL");
     return !(e && std::string(e) == "0");
@@ -34,28 +47,70 @@ UncachedPool& pool() {
   return *p;
 }
 
-// Size classes: powers of two from 64 KiB, so a block serves requests down to half its size.
+constexpr size_t kPow2Max = (size_t)64 << 20;
+constexpr size_t kLargeStep = (size_t)2 << 20;
+
 size_t classOf(size_t bytes) {
+  if (bytes > kPow2Max) return (bytes + kLargeStep - 1) / kLargeStep * kLargeStep;
   size_t c = (size_t)64 << 10;
   while (c < bytes) c <<= 1;
   return c;
+}
+
+// A free block of `cls` on `dev` (caller holds the lock): the exact class, or for a large class the
+// smallest free one up to 5/4 of it.
+void* takeFree(UncachedPool& P, int dev, size_t cls, size_t* got) {
+  auto it = P.freeBlocks.lower_bound({dev, cls});
+  const size_t limit = cls > kPow2Max ? cls + cls / 4 : cls;
+  for (; it != P.freeBlocks.end() && it->first.first == dev && it->first.second <= limit; ++it) {
+    if (it->second.empty()) continue;
+    void* p = it->second.back();
+    it->second.pop_back();
+    *got = it->first.second;
+    return p;
+  }
+  return nullptr;
+}
+
+// Zero the first `bytes` of a block on the pool's own stream of `dev` (never the null stream: a
+// legacy-stream memset would join, or break, another thread's graph capture).
+void zeroFill(UncachedPool& P, int dev, void* p, size_t bytes) {
+  hipStream_t s = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto it = P.zeroStreams.find(dev);
+    if (it != P.zeroStreams.end()) s = it->second;
+  }
+  if (!s) {
+    HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto ins = P.zeroStreams.emplace(dev, s);
+    if (!ins.second) {  // another thread created one first
+      (void)hipStreamDestroy(s);
+      s = ins.first->second;
+    }
+  }
+  HIPCHECK(hipMemsetAsync(p, 0, bytes, s));
+  HIPCHECK(hipStreamSynchronize(s));
 }
 
 }  // namespace
 
 void* allocUncached(size_t bytes) {
   UncachedPool& P = pool();
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
   void* p = nullptr;
   size_t cls = bytes;
   {
     std::lock_guard<std::mutex> lk(P.mu);
     if (P.enabled) {
       cls = classOf(bytes);
-      auto it = P.freeBlocks.find(cls);
-      if (it != P.freeBlocks.end()) {
-        p = it->second;
-        P.freeBlocks.erase(it);
-        P.live[p] = cls;
+      size_t got = 0;
+      p = takeFree(P, dev, cls, &got);
+      if (p) {
+        cls = got;
+        P.live[p] = Block{dev, cls};
       }
     }
   }
@@ -63,42 +118,64 @@ void* allocUncached(size_t bytes) {
     HIPCHECK(hipExtMallocWithFlags(&p, cls, hipDeviceMallocUncached));
     std::lock_guard<std::mutex> lk(P.mu);
     if (P.enabled) {
-      P.live[p] = cls;
+      P.live[p] = Block{dev, cls};
       P.held += cls;
     }
   }
-  HIPCHECK(hipMemset(p, 0, cls));
+  zeroFill(P, dev, p, bytes);
   return p;
 }
 
-bool releaseUncached(void* p) {
+bool releaseUncached(void* p, hipError_t* syncError) noexcept {
+  if (syncError) *syncError = hipSuccess;
   if (!p) return true;
   UncachedPool& P = pool();
+  Block b{};
   {
     std::lock_guard<std::mutex> lk(P.mu);
-    if (P.live.find(p) == P.live.end()) return false;  // not a pooled block
+    auto it = P.live.find(p);
+    if (it == P.live.end()) return false;  // not a pooled block
+    b = it->second;
   }
-  // as hipFree: no queued kernel may still use the block when it is handed out again
-  HIPCHECK(hipDeviceSynchronize());
+  // as hipFree: no queued kernel of the owning device may still use the block when it is handed
+  // out again.  If that device cannot be synchronized (a sticky error), the block is leaked -- it
+  // leaves the live set but never reaches the free list.
+  int cur = -1;
+  hipError_t e = hipGetDevice(&cur);
+  if (e == hipSuccess && cur != b.device) e = hipSetDevice(b.device);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (cur >= 0 && cur != b.device) (void)hipSetDevice(cur);
+  if (e != hipSuccess) (void)hipGetLastError();
   std::lock_guard<std::mutex> lk(P.mu);
   auto it = P.live.find(p);
   if (it == P.live.end()) return true;
-  P.freeBlocks.emplace(it->second, p);
   P.live.erase(it);
+  if (e == hipSuccess) {
+    P.freeBlocks[{b.device, b.cls}].push_back(p);
+  } else {
+    P.leaked += b.cls;
+    if (syncError) *syncError = e;
+  }
   return true;
 }
 
-void freeDevice(void* p) {
+void freeDevice(void* p) noexcept {
   if (!p) return;
-  if (!releaseUncached(p)) (void)hipFree(p);
+  if (!releaseUncached(p, nullptr)) (void)hipFree(p);
+}
+
+bool isPooledUncached(const void* base) {
+  UncachedPool& P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  return P.live.count(const_cast<void*>(base)) != 0;
 }
 
 void uncachedPoolStats(size_t* held, size_t* inUse, size_t* freeBytes) {
   UncachedPool& P = pool();
   std::lock_guard<std::mutex> lk(P.mu);
   size_t used = 0, fr = 0;
-  for (const auto& e : P.live) used += e.second;
-  for (const auto& e : P.freeBlocks) fr += e.first;
+  for (const auto& e : P.live) used += e.second.cls;
+  for (const auto& e : P.freeBlocks) fr += e.first.second * e.second.size();
   if (held) *held = P.held;
   if (inUse) *inUse = used;
   if (freeBytes) *freeBytes = fr;

@@ -90,6 +90,35 @@ def test_ll_allreduce_bit_exact(built, algo, n, dt, count, special):
                 assert np.array_equal(got, scr[r]), f"scratch image of rank {r}"
 
 
+@pytest.mark.parametrize("count", [262144, 524288, 262146, 262147, 1023])
+def test_ll8_two_ranks_default_shape_bit_exact(built, count):
+    """at 2 ranks the selector sends the whole LL range (to 1 MiB) to one-hop LL8 with its
+    default grid (nblocks = nthreads = 0: up to 128 x 512 lanes, poll_units / waveSingle).  Outputs
+    and the flag-1 scratch image bit-exact at 512 KiB, 1 MiB, an odd LL8 word count (a trailing
+    single packet), a ragged tail below one word, and a small bucket, over three flags."""
+    import mscclpp_amd as m
+
+    n, dt = 2, O.F16
+    nbytes = count * 2
+    assert m.lib().mscclppAmdSelectAlgo(n, nbytes, dt) == m.ALGO_ALLPAIR
+    sb = max(m.scratch_required(m.ALGO_ALLPAIR, n, nbytes, dt), 1 << 16)
+    ranks = m.InProcessRanks(n, sb)
+    for call, flag in enumerate((1, 2, 3)):
+        ins = _inputs(dt, n, count, seq=call, special=(call == 1))
+        dins = [_dev(a, dt) for a in ins]
+        douts = [torch.full_like(d, 0) for d in dins]
+        ranks.all_reduce(dins, douts, m.ALGO_ALLPAIR, nblocks=0, nthreads=0)
+        torch.cuda.synchronize()
+        assert ranks.errors() == [0] * n
+        exp, scr = O.allreduce_allpairs(dt, O.SUM, ins, count, flag, sb // 2)
+        for r in range(n):
+            _cmp(_bytes(douts[r]), exp[r].view(np.uint8)[:nbytes], dt)
+        if call == 0:
+            for r in range(n):
+                got = ranks.scratch_tensor(r, sb).cpu().numpy().view(np.uint32)
+                assert np.array_equal(got, scr[r]), f"scratch image of rank {r}"
+
+
 @pytest.mark.parametrize("algo,order", [("fullmesh", 0), ("rsag", 1), ("rsag_zc", 1)])
 @pytest.mark.parametrize("n,dt,count", [(2, O.F16, 1 << 16), (8, O.F16, 1 << 18), (8, O.F32, 100000),
                                         (4, O.BF16, 65536 + 8), (8, O.I32, 4096), (7, O.F32, 12345),

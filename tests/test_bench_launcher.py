@@ -125,27 +125,97 @@ def _probe(put, getput):
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
-def test_multi_line_roofline_prices_the_kernels_pattern(n):
-    """the N>1 line's roofline carries bound / achieved / peak / frac, zero-copy
-    is priced against gets + puts driven together, the scratch kernels against puts, and a frac
-    above 1 (a probe that under-drove the links) is flagged, with no slack."""
+def test_multi_line_roofline_grades_the_spec_xgmi_ceiling(n):
+    """the N>1 line's roofline peak is the all-pairs algbw ceiling of BASELINE.md §2,
+    n * 153.6 / 2 GB/s (614.4 at n = 8), whatever the probe measured, and frac = the kernel's algbw /
+    that peak (= wire bytes per rank / ((n-1) * 153.6)).  The probe of the kernel's own pattern moves
+    to measured_ceiling / frac_of_measured; a frac_of_measured above 1 is flagged, with no slack."""
     import bench
 
     S, kern_ms = 48 << 20, 0.2
+    algbw = S / (kern_ms * 1e-3) / 1e9
     wire_gbs = 2 * (n - 1) * S / n / (kern_ms * 1e-3) / 1e9
+    peak = n * 153.6 / 2
     for algo, key in (("rsag_zc", "allpairs_getput_GBs"), ("fullmesh", "allpairs_put_out_GBs")):
         probe = _probe(2 * wire_gbs, 3 * wire_gbs)
         roof, xg = bench.multi_roofline(n, S, algo, kern_ms * 1.05e-3, kern_ms, probe, False)
         for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
             assert k in roof
-        assert roof["peak"] == probe[key] and roof["frac"] == pytest.approx(wire_gbs / probe[key], rel=1e-3)
-        assert roof["frac"] <= 1 and xg["probe_consistent"] is True
-        # the same kernel time against a probe slower than the kernel itself: inconsistent
+        assert roof["peak"] == pytest.approx(peak, abs=0.05)
+        assert roof["achieved"] == pytest.approx(algbw, rel=1e-3)
+        assert roof["frac"] == pytest.approx(algbw / peak, rel=1e-3)
+        assert roof["frac"] == pytest.approx(wire_gbs / ((n - 1) * 153.6), rel=1e-3)
+        mc = probe[key] * n / (2 * (n - 1))
+        assert roof["measured_ceiling"] == pytest.approx(mc, rel=1e-3)
+        assert roof["frac_of_measured"] == pytest.approx(algbw / mc, rel=1e-3)
+        assert xg["probe_consistent"] is True
+        # a probe slower than the kernel itself: inconsistent, and the peak does not move
         roof, xg = bench.multi_roofline(n, S, algo, kern_ms * 1.05e-3, kern_ms, _probe(0.99 * wire_gbs, 0.99 * wire_gbs),
                                         False)
-        assert roof["frac"] > 1 and xg["probe_consistent"] is False
-    _, xg = bench.multi_roofline(n, S, "fullmesh", 1e-4, 0.1, {"error": "no probe"}, True)
-    assert xg["probe_consistent"] is False
+        assert roof["frac_of_measured"] > 1 and xg["probe_consistent"] is False
+        assert roof["peak"] == pytest.approx(peak, abs=0.05)
+    roof, xg = bench.multi_roofline(n, S, "fullmesh", 1e-4, 0.1, {"error": "no probe"}, True)
+    assert xg["probe_consistent"] is False and "measured_ceiling" not in roof
+    assert roof["frac"] == pytest.approx(S / 1e-4 / 1e9 / peak, rel=1e-3)
+    assert bench.multi_roofline(8, S, "fullmesh", 1e-3, 1.0, {}, False)[0]["peak"] == pytest.approx(614.4)
+
+
+class _FakeLib:
+    """mscclppAmdSelectAlgo of the built-in table (host/tuning.cpp) for the winner_profile test."""
+
+    def mscclppAmdSelectAlgo(self, n, size, dt):
+        return 2 if size <= 16 << 10 or (n == 2 and size <= 1 << 20) else 1 if size <= 1 << 20 else 3
+
+
+class _FakeM:
+    def lib(self):
+        return _FakeLib()
+
+    def tuned_config(self, coll, n, size):
+        return None
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_winner_profile_keeps_the_ll_range(n):
+    """The profile bench.py loads before timing ncclAllReduce names the winner from the bucket size
+    up and keeps the selector's choices below it, so only the headline size changes algorithm."""
+    import bench
+
+    S = 48 << 20
+    prof = bench.winner_profile(_FakeM(), n, S, "AMD Instinct MI355X", "rsag_zc", 128, 512)
+    (p,) = prof["profiles"]
+    assert p["scale"] == n and prof["version"] == 1
+    es = p["collectives"]["allreduce"]
+    assert es[-1] == {"message_size": S, "algorithm": "default_allreduce_rsag_zero_copy", "nblocks": 128, "nthreads": 512}
+    want = ["default_allreduce_allpair_packet"] + ([] if n == 2 else ["default_allreduce_packet"]) + \
+        ["default_allreduce_fullmesh", "default_allreduce_rsag_zero_copy"]
+    assert [e["algorithm"] for e in es] == want
+    assert es[0]["message_size"] == 1
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "mscclpp_amd", "lib", "libmscclpp_amd.so")),
+                    reason="library not built")
+def test_loaded_winner_drives_the_library_selector(tmp_path):
+    """Host only (no GPU call): after mscclppAmdTunedConfigLoad of winner_profile, the library's own
+    selector -- what ncclAllReduce consults -- returns the winner and its launch shape at the bucket,
+    and the built-in choices below it."""
+    import bench
+    import mscclpp_amd as m
+
+    n, S = 8, 48 << 20
+    before = {sz: m.lib().mscclppAmdSelectAlgo(n, sz, 0) for sz in (1024, 64 << 10, 4 << 20)}
+    try:
+        # no SKU: this container has no GPU to name one (bench.py passes the device's name)
+        loaded = bench.load_winner(m, n, S, None, "rsag_zc", 128, 512)
+        assert loaded[-1]["algorithm"] == "default_allreduce_rsag_zero_copy"
+        assert m.tuned_config("allreduce", n, S) == ("default_allreduce_rsag_zero_copy", 128, 512)
+        assert bench.SELECT_NAMES[m.lib().mscclppAmdSelectAlgo(n, S, 0)] == "rsag_zc"
+        for sz, a in before.items():
+            assert m.lib().mscclppAmdSelectAlgo(n, sz, 0) == a, sz
+    finally:
+        empty = tmp_path / "empty.json"
+        empty.write_text('{"version": 1, "profiles": []}')
+        m.load_tuned_config(str(empty))
 
 
 def test_cpu_baselines_state_their_cores():

@@ -16,20 +16,21 @@ CASES = [  # (algo, dtype code, count)
     ("allpair", 0, 4096), ("packet", 0, 1 << 18), ("fullmesh", 0, 1 << 20), ("rsag", 2, 100000),
     ("packet", 1, 30000), ("auto", 0, 48 << 19), ("auto", 2, 1000), ("fullmesh", 1, 12345),
     ("rsag_zc", 0, 1 << 20), ("rsag_zc", 2, 12345), ("rsag_pipeline", 2, 100000), ("rsag_pipeline", 2, 3 << 20),
+    # 2 ranks: the selector's one-hop LL8 at the top of its range, default shape
+    ("auto", 0, 1 << 19), ("auto", 0, (1 << 18) + 3),
 ]
 
 
 def _worker(rank, n, uid, q, cases=None, rsag=True):
     try:
         os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "5000")
-        if n > 2:  # many ranks on one device: one hardware queue each keeps every rank's queue mapped
-            os.environ["GPU_MAX_HW_QUEUES"] = "1"
         import torch
 
+        import mp_util
         import mscclpp_amd as m
         import oracle_lib as O
 
-        torch.cuda.set_device(0)
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         tdt = {0: torch.float16, 1: torch.bfloat16, 2: torch.float32}
         results = []
@@ -150,7 +151,9 @@ def _ring_worker(rank, n, uid, q, nelems, nblocks):
 
         import mscclpp_amd as m
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         us, ok, _ = comm.proxy_ring_all_reduce(nelems, iters=1, graph_launches=1, nblocks=nblocks)
         errc = comm.device_error()
@@ -197,7 +200,9 @@ def _bcast_split_worker(rank, n, uid, q):
 
         import mscclpp_amd as m
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         out = []
         # ncclBroadcast out of place from the last rank, then ncclBcast in place from rank 0
@@ -263,7 +268,9 @@ def _stream_order_worker(rank, n, uid, q):
 
         import mscclpp_amd as m
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         res = []
         blk = 1 << 18
@@ -328,7 +335,9 @@ def _pipeline_then_worker(rank, n, uid, q):
 
         import mscclpp_amd as m
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         res = []
         cnt = 3 << 20  # 12 MiB of int32: several pipeline iterations at every shape below
@@ -394,7 +403,9 @@ def _churn_worker(rank, n, uid, q):
 
         import mscclpp_amd as m
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         L = m.lib()
         import ctypes
@@ -469,7 +480,9 @@ def _symmetric_worker(rank, n, uid, symmetric, q):
 
         import mscclpp_amd as m
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         L = m.lib()
         nslots, slot = 16, 1 << 19  # 16 sub-buffers of 512 KiB in one 8 MiB allocation
@@ -541,7 +554,9 @@ def _reimport_worker(rank, n, uid, q):
 
         import mscclpp_amd as m
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         L = m.lib()
         bad, addrs = 0, set()

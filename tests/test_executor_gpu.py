@@ -58,7 +58,9 @@ def _worker(rank, n, uid, cases, q):
         import mscclpp_amd as m
         import oracle_lib as O
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         ex = m.Executor(comm)
         tdt = {"f16": torch.float16, "bf16": torch.bfloat16, "f32": torch.float32, "e4m3": torch.float8_e4m3fn,

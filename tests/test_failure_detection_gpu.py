@@ -71,7 +71,9 @@ def _worker(rank, uid, q):
 
         import mscclpp_amd as m
 
-        th.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, 2)
         comm = m.Communicator(rank, 2, uid)
         x = th.ones(512, dtype=th.float16, device="cuda")
         y = th.zeros_like(x)

@@ -52,7 +52,9 @@ def _worker(rank, n, uid, q):
         import mscclpp_amd as m
         import oracle_lib as O
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         tdt = {0: torch.float16, 2: torch.float32}
         out = []
@@ -161,7 +163,9 @@ def _churn_worker(rank, n, uid, q):
         import mscclpp_amd as m
         import oracle_lib as O
 
-        torch.cuda.set_device(0)
+        import mp_util
+
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         count = 6 << 20  # 12 MiB: above the caching allocator's 10 MiB packing, so its own segment
         # a buffer registered for the caller (an algorithm plugin keeps these raw peer pointers)

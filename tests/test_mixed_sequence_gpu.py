@@ -53,14 +53,13 @@ def _worker(rank, n, uid, q):
         import time
 
         os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "8000")
-        if n > 2:  # many ranks on one device: one hardware queue each keeps every rank's queue mapped
-            os.environ["GPU_MAX_HW_QUEUES"] = "1"
         import torch
 
+        import mp_util
         import mscclpp_amd as m
         import oracle_lib as O
 
-        torch.cuda.set_device(0)
+        mp_util.place_rank(rank, n)
         comm = m.Communicator(rank, n, uid)
         seq = _sequence()
         data = []
