@@ -93,10 +93,10 @@ void enqueue(RelayConn& c, const MsgHeader& h, const char* body) {
 
 void rootLoop(int lfd, uint64_t nonce) {
   std::vector<RelayConn> cs;
+  std::vector<int> fds;  // accepted ranks' sockets until the relay (cs) owns them
   int nranks = -1;
   try {
     int have = 0;
-    std::vector<int> fds;
     while (nranks < 0 || have < nranks) {
       pollfd pf{lfd, POLLIN, 0};
       int r = ::poll(&pf, 1, 600 * 1000);
@@ -131,8 +131,9 @@ void rootLoop(int lfd, uint64_t nonce) {
     cs.resize(nranks);
     for (int r = 0; r < nranks; ++r) {
       cs[r].fd = fds[r];
-      setTimeouts(fds[r], 0);  // relay phase: ranks may stay idle indefinitely
-      ::fcntl(fds[r], F_SETFL, ::fcntl(fds[r], F_GETFL, 0) | O_NONBLOCK);
+      fds[r] = -1;
+      setTimeouts(cs[r].fd, 0);  // relay phase: ranks may stay idle indefinitely
+      ::fcntl(cs[r].fd, F_SETFL, ::fcntl(cs[r].fd, F_GETFL, 0) | O_NONBLOCK);
     }
     std::vector<std::deque<std::vector<char>>> pending(nranks);  // all-gather contributions per rank
     std::vector<pollfd> pfs(nranks);
@@ -200,7 +201,11 @@ void rootLoop(int lfd, uint64_t nonce) {
     }
   } catch (...) {
   }
+  // every socket still open gets closed, so waiting ranks see EOF instead of an open, silent socket
+  // (also when the accept phase failed before the relay took the sockets over)
   if (lfd >= 0) ::close(lfd);
+  for (int fd : fds)
+    if (fd >= 0) ::close(fd);
   for (auto& c : cs)
     if (c.fd >= 0) ::close(c.fd);
 }

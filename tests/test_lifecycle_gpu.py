@@ -30,7 +30,14 @@ def _check_packet(O, got, ins, rank, count):
     return int(np.count_nonzero(got != exp[rank].view(np.uint8)[: count * 2]))
 
 
-def _worker(rank, uid, q):
+def _log(rank, msg):
+    import sys
+    import time
+
+    print(f"[lifecycle rank {rank} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _worker(rank, uids, q):
     try:
         os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "10000")
         import torch
@@ -48,7 +55,8 @@ def _worker(rank, uid, q):
             big *= 2
         res["big_bytes"] = big * 2
         for cycle in range(3):
-            comm = m.Communicator(rank, N, uid)
+            _log(rank, f"cycle {cycle}: init")
+            comm = m.Communicator(rank, N, uids[cycle])  # a unique id serves one rendezvous
             for algo, count in (("packet", 1 << 16), ("fullmesh", 1 << 20), ("rsag_zc", 12345), ("packet", big)):
                 ins = [O.lcg(O.F16, count, r, cycle) for r in range(N)]
                 x = torch.from_numpy(ins[rank].view(np.int16).copy()).view(torch.float16).cuda()
@@ -66,6 +74,7 @@ def _worker(rank, uid, q):
             comm.destroy()
             torch.cuda.empty_cache()
             res["cycles"].append({"pool": m.pool_stats(), "ipc": m.ipc_stats()})
+        _log(rank, "cycles done; torch buffers")
         # torch buffers allocated now: none may sit where an import of the peer's uncached memory
         # was, and each must receive every store of a fill kernel
         kept = m.ipc_kept_ranges()
@@ -86,7 +95,8 @@ def _worker(rank, uid, q):
         res["overlaps"], res["lost"] = overlaps, lost[:4]
         del bufs
         # growth under capture: refused; eagerly: done; then the capture works and replays exactly
-        comm = m.Communicator(rank, N, uid)
+        _log(rank, "capture")
+        comm = m.Communicator(rank, N, uids[3])
         count = big
         ins = [O.lcg(O.F16, count, r, 7) for r in range(N)]
         x = torch.from_numpy(ins[rank].view(np.int16).copy()).view(torch.float16).cuda()
@@ -143,16 +153,16 @@ def _sum_bytes(O, ins, algo, rank, count):
 def test_create_destroy_cycles_pool_and_imports_bounded(built):
     import mscclpp_amd as m
 
-    uid = m.Communicator.unique_id()
+    uids = [m.Communicator.unique_id() for _ in range(4)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, uid, q)) for r in range(N)]
+    procs = [ctx.Process(target=_worker, args=(r, uids, q)) for r in range(N)]
     for p in procs:
         p.start()
     got = {}
     try:
         for _ in range(N):
-            rank, res, err = q.get(timeout=240)
+            rank, res, err = q.get(timeout=150)
             assert err is None, err
             got[rank] = res
     except queue.Empty:
