@@ -19,3 +19,34 @@ def place_rank(rank, n):
     dev = rank % max(1, ndev)
     torch.cuda.set_device(dev)
     return dev, shared
+
+
+def collect(procs, q, n, timeout):
+    """The (rank -> result) of n rank processes that put (rank, result, error) on q.  Fails at once
+    when a rank reported an error or died without reporting (a crash, a segfault), instead of
+    waiting out the timeout; kills what is left at the end."""
+    import queue
+    import time
+
+    import pytest
+
+    got, deadline = {}, time.time() + timeout
+    try:
+        while len(got) < n:
+            try:
+                rank, res, err = q.get(timeout=2)
+            except queue.Empty:
+                dead = [(i, p.exitcode) for i, p in enumerate(procs) if p.exitcode not in (None, 0) and i not in got]
+                if dead:
+                    pytest.fail(f"rank process(es) died without a result: {dead}")
+                if time.time() > deadline:
+                    pytest.fail(f"timed out after {timeout} s; results from ranks {sorted(got)}")
+                continue
+            assert err is None, f"rank {rank}: {err}"
+            got[rank] = res
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return got

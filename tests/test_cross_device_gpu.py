@@ -7,7 +7,6 @@ communicator, bit-exactly against the CPU oracle.  Every byte between ranks cros
 stores into a peer's output that the owner's next kernel and its copy engine must both see."""
 import multiprocessing as mp
 import os
-import queue
 import traceback
 
 import numpy as np
@@ -47,9 +46,9 @@ def _worker(rank, n, uid, q):
                 {1: "packet", 2: "allpair", 3: "fullmesh", 5: "rsag_zc", 6: "rsag_pipeline"}[
                     m.lib().mscclppAmdSelectAlgo(n, nbytes, dt)]
             if sel == "packet":
-                e = O.allreduce_packet(dt, O.SUM, ins, count, 1, 1 << 22)[0][rank].view(np.uint8)[:nbytes]
+                e = O.allreduce_packet(dt, O.SUM, ins, count, 1, max(1 << 22, m.scratch_required(m.ALGO_PACKET, n, nbytes, dt) // 2))[0][rank].view(np.uint8)[:nbytes]
             elif sel == "allpair":
-                e = O.allreduce_allpairs(dt, O.SUM, ins, count, 1, 1 << 22)[0][rank].view(np.uint8)[:nbytes]
+                e = O.allreduce_allpairs(dt, O.SUM, ins, count, 1, max(1 << 22, m.scratch_required(m.ALGO_ALLPAIR, n, nbytes, dt) // 2))[0][rank].view(np.uint8)[:nbytes]
             else:
                 sl = ((nbytes + n - 1) // n + 15) // 16 * 16
                 nw = (nbytes + 3) // 4
@@ -83,19 +82,9 @@ def test_ranks_on_distinct_devices_bit_exact(built):
     procs = [ctx.Process(target=_worker, args=(r, n, uid, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=300)
-            assert err is None, err
-            got[rank] = res
-    except queue.Empty:
-        pytest.fail(f"{n}-GPU AllReduce timed out")
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    import mp_util
+
+    got = mp_util.collect(procs, q, n, 300)
     assert len({got[r]["dev"] for r in got}) == n, got
     assert len({got[r]["bus"] for r in got}) == n, got
     for rank, res in got.items():

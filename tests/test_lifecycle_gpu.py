@@ -14,7 +14,6 @@ by tests/mp_util.py (one per GPU where there are two):
 Every AllReduce result is compared bit-exactly with the CPU oracle."""
 import multiprocessing as mp
 import os
-import queue
 import traceback
 
 import numpy as np
@@ -26,7 +25,10 @@ N = 2
 
 
 def _check_packet(O, got, ins, rank, count):
-    exp, _ = O.allreduce_packet(O.F16, O.SUM, ins, count, 1, 1 << 22)
+    import mscclpp_amd as m
+
+    half = m.scratch_required(m.ALGO_PACKET, N, count * 2, m.F16) // 2  # the oracle's scratch must hold the call
+    exp, _ = O.allreduce_packet(O.F16, O.SUM, ins, count, 1, half)
     return int(np.count_nonzero(got != exp[rank].view(np.uint8)[: count * 2]))
 
 
@@ -39,6 +41,9 @@ def _log(rank, msg):
 
 def _worker(rank, uids, q):
     try:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(120, exit=True)  # a stuck rank says where, then ends
         os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "10000")
         import torch
 
@@ -61,6 +66,7 @@ def _worker(rank, uids, q):
                 ins = [O.lcg(O.F16, count, r, cycle) for r in range(N)]
                 x = torch.from_numpy(ins[rank].view(np.int16).copy()).view(torch.float16).cuda()
                 y = torch.zeros_like(x)
+                _log(rank, f"cycle {cycle}: {algo} {count}")
                 comm.all_reduce(x, y, algo=algo)
                 torch.cuda.synchronize()
                 got = y.cpu().view(torch.uint8).numpy()
@@ -70,6 +76,7 @@ def _worker(rank, uids, q):
                     res["bad"] += int(np.count_nonzero(got != _sum_bytes(O, ins, algo, rank, count)))
                 del x, y
             res["bad"] += comm.device_error()
+            _log(rank, f"cycle {cycle}: destroy")
             comm.barrier()
             comm.destroy()
             torch.cuda.empty_cache()
@@ -159,19 +166,9 @@ def test_create_destroy_cycles_pool_and_imports_bounded(built):
     procs = [ctx.Process(target=_worker, args=(r, uids, q)) for r in range(N)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(N):
-            rank, res, err = q.get(timeout=150)
-            assert err is None, err
-            got[rank] = res
-    except queue.Empty:
-        pytest.fail("lifecycle test timed out")
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    import mp_util
+
+    got = mp_util.collect(procs, q, N, 150)
     for rank, res in got.items():
         assert res["bad"] == 0, (rank, res)
         cyc = res["cycles"]
