@@ -577,7 +577,8 @@ def bench_multi(args):
     # tuning (algo None -> ncclAllReduce -> mscclppAmdSelectAlgo + its launch shape), timed like the
     # headline: the `default_selector` figure beside it
     progress("default selector")
-    default_sel = {"algo": SELECT_NAMES[m.lib().mscclppAmdSelectAlgo(n, S, 0)]}
+    default_sel = {"algo": SELECT_NAMES[m.lib().mscclppAmdSelectAlgo(n, S, 0)],
+                   "source": m.tuned_config_source("allreduce", n, S)}
     try:
         for j in range(3):
             comm.all_reduce(xs[j % 2], out)
@@ -717,7 +718,8 @@ def bench_multi(args):
         "config": {"workload": f"allreduce_fp16_{S >> 20}MiB (BASELINE configs[2]: 2048x12288 fp16 bucket per rank)",
                    "bytes": S, "parallelism": f"allreduce{world}", "call": "ncclAllReduce (algorithm and shape "
                    "from the library's selector after mscclppAmdTunedConfigLoad of this node's winner)",
-                   "algo": sel_algo, "nblocks": nb, "nthreads": nt, "tuned_config_loaded": loaded},
+                   "algo": sel_algo, "nblocks": nb, "nthreads": nt, "tuned_config_loaded": loaded,
+                   "selector_source": m.tuned_config_source("allreduce", n, S)},
         "default_selector": default_sel,
         # ranks sharing fewer GPUs than ranks (a 1-GPU box): every number below is HBM, not xGMI
         "rehearsal": ndev < world,

@@ -164,6 +164,10 @@ int mscclppAmdSelectAlgo(int nranks, size_t bytes, int dtype);
 int mscclppAmdTunedConfigLoad(const char* path);
 int mscclppAmdTunedConfig(const char* collective, int nranks, size_t bytes, char* algorithm, size_t algorithmLen,
                           int* nblocks, int* nthreads);
+/* Where the entry that applies came from: "reference" (the reference's selector restated),
+ * "fabric-free" (measured with every rank on one GPU: no link bytes priced), "reference; grid
+ * fabric-free", "tuned" (a loaded file's entry without its own "source" tag) or that tag. */
+int mscclppAmdTunedConfigSource(const char* collective, int nranks, size_t bytes, char* source, size_t sourceLen);
 
 /* ---- communicator extensions -------------------------------------------------------------- */
 // Phase trace of the collective kernels (the reference's NPKit events, npkit.hpp): while a buffer of

@@ -105,6 +105,7 @@ def lib():
         "mscclppAmdAllReduceLaunch": [i32, ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, i32, u64, vp],
         "mscclppAmdSelectAlgo": [i32, sz, i32],
         "mscclppAmdTunedConfigLoad": [ctypes.c_char_p],
+        "mscclppAmdTunedConfigSource": [ctypes.c_char_p, i32, sz, ctypes.c_char_p, sz],
         "mscclppAmdTunedConfig": [ctypes.c_char_p, i32, sz, ctypes.c_char_p, sz, ctypes.POINTER(i32),
                                   ctypes.POINTER(i32)],
         "mscclppAmdCollectiveLaunch": [i32, i32, ctypes.POINTER(RankView), i32, i32, sz, i32, i32, i32, i32, u64, vp],
@@ -257,6 +258,16 @@ def tuned_config(collective, nranks, nbytes):
         return None
     check(rc, "tuned config")
     return name.value.decode(), nb.value, nt.value
+
+
+def tuned_config_source(collective, nranks, nbytes):
+    """Where the tuned-config entry that applies came from ("reference", "fabric-free", "tuned", ...)."""
+    buf = ctypes.create_string_buffer(128)
+    rc = lib().mscclppAmdTunedConfigSource(collective.encode(), nranks, nbytes, buf, 128)
+    if rc == 5:
+        return None
+    check(rc, "tuned config source")
+    return buf.value.decode()
 
 
 def load_tuned_config(path):

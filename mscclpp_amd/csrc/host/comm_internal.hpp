@@ -221,7 +221,7 @@ uint64_t allocationId(const void* ptr);  // HIP_POINTER_ATTRIBUTE_BUFFER_ID (0 i
 // Tuned configuration (tuning.cpp) for a collective of `bytes` on `nranks` ranks of this device's
 // SKU: the algorithm name and launch shape (0 = the algorithm's default); false if none.
 bool tunedConfig(const std::string& collective, int nranks, uint64_t bytes, std::string& algorithm, int& nblocks,
-                 int& nthreads);
+                 int& nthreads, std::string* source = nullptr);
 int algoCodeOf(const std::string& name);  // MSCCLPP_AMD_ALGO_* of a default_allreduce_* name, or -1
 }  // namespace host
 }  // namespace mscclpp_amd

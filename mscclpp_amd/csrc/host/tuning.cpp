@@ -32,6 +32,7 @@ struct Entry {
   uint64_t size;
   std::string algorithm;
   int nblocks = 0, nthreads = 0;
+  std::string source;  // "reference", "fabric-free", "tuned" (loaded files), or the file's own tag
 };
 struct Profile {
   std::string sku;  // empty: any
@@ -39,17 +40,26 @@ struct Profile {
   std::map<std::string, std::vector<Entry>> byCollective;  // sorted by size
 };
 
+// Every entry says where it came from ("source"): "reference" restates the reference's selector;
+// "fabric-free" was measured with all ranks on one GPU (in-process or shared-device sweeps), which
+// prices the hand-off but no link bytes -- a guess for the node until a node-measured table (bench.py
+// prints one as `tuned_config_table`) overrides it.  Entries of a loaded file without a source are
+// "tuned".  "reference; grid fabric-free": the reference's choice of algorithm, run on the kernel's
+// default grid, whose few-rank cap (max(16, 48 / (n-1)) workgroups per peer, allreduce_ll.hip) came
+// from fabric-free sweeps -- an entry with nblocks / nthreads replaces it.
+// mscclppAmdTunedConfigSource reports which entry applied.
 const char* kBuiltin = R"({"version": 1, "profiles": [
   {"scale": 2, "collectives": {"allreduce": [
-      {"message_size": 1, "algorithm": "default_allreduce_allpair_packet"},
-      {"message_size": 1048577, "algorithm": "default_allreduce_fullmesh"}]}},
+      {"message_size": 1, "algorithm": "default_allreduce_allpair_packet", "source": "fabric-free"},
+      {"message_size": 1048577, "algorithm": "default_allreduce_fullmesh", "source": "reference"}]}},
   {"collectives": {
     "allreduce": [
-      {"message_size": 1, "algorithm": "default_allreduce_allpair_packet"},
-      {"message_size": 16385, "algorithm": "default_allreduce_packet"},
-      {"message_size": 1048577, "algorithm": "default_allreduce_fullmesh"}],
-    "allgather": [{"message_size": 1, "algorithm": "default_allgather_fullmesh2"}],
-    "reducescatter": [{"message_size": 1, "algorithm": "default_reducescatter_fullmesh"}]}}
+      {"message_size": 1, "algorithm": "default_allreduce_allpair_packet", "source": "reference"},
+      {"message_size": 16385, "algorithm": "default_allreduce_packet",
+       "source": "reference; grid fabric-free"},
+      {"message_size": 1048577, "algorithm": "default_allreduce_fullmesh", "source": "reference"}],
+    "allgather": [{"message_size": 1, "algorithm": "default_allgather_fullmesh2", "source": "reference"}],
+    "reducescatter": [{"message_size": 1, "algorithm": "default_reducescatter_fullmesh", "source": "reference"}]}}
 ]})";
 
 std::string normalizeSku(const std::string& raw) {
@@ -62,7 +72,7 @@ std::string normalizeSku(const std::string& raw) {
   return out.empty() ? "UNKNOWN" : out;
 }
 
-std::vector<Profile> parseStore(const std::string& text) {
+std::vector<Profile> parseStore(const std::string& text, const char* defaultSource) {
   const json::Value doc = json::parse(text);
   if (!doc.isObject() || !doc.contains("profiles") || !doc["profiles"].isArray())
     throw std::invalid_argument("tuned config: expected an object with a 'profiles' list");
@@ -83,6 +93,7 @@ std::vector<Profile> parseStore(const std::string& text) {
           en.algorithm = e["algorithm"].str();
           if (e.contains("nblocks") && e["nblocks"].kind != json::Value::Null) en.nblocks = (int)e["nblocks"].asI64();
           if (e.contains("nthreads") && e["nthreads"].kind != json::Value::Null) en.nthreads = (int)e["nthreads"].asI64();
+          en.source = e.contains("source") && e["source"].kind != json::Value::Null ? e["source"].str() : defaultSource;
           es.push_back(en);
         }
         std::sort(es.begin(), es.end(), [](const Entry& a, const Entry& b) { return a.size < b.size; });
@@ -115,7 +126,7 @@ Store& store() {
   std::lock_guard<std::mutex> lk(s.mu);
   if (!s.init) {
     s.init = true;
-    s.builtin = parseStore(kBuiltin);
+    s.builtin = parseStore(kBuiltin, "builtin");
     int dev = 0;
     hipDeviceProp_t prop{};
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) {
@@ -128,7 +139,7 @@ Store& store() {
         std::ifstream f(path);
         std::stringstream ss;
         ss << f.rdbuf();
-        s.user = parseStore(ss.str());
+        s.user = parseStore(ss.str(), "tuned");
       } catch (const std::exception& e) {
         warn(std::string("MSCCLPP_AMD_TUNED_CONFIG ignored: ") + e.what());
       }
@@ -165,7 +176,7 @@ const Entry* selectProfiles(const std::vector<Profile>& ps, const std::string& s
 }  // namespace
 
 bool tunedConfig(const std::string& collective, int nranks, uint64_t bytes, std::string& algorithm, int& nblocks,
-                 int& nthreads) {
+                 int& nthreads, std::string* source) {
   Store& s = store();
   std::lock_guard<std::mutex> lk(s.mu);
   const Entry* e = selectProfiles(s.user, s.sku, nranks, collective, bytes);
@@ -174,6 +185,7 @@ bool tunedConfig(const std::string& collective, int nranks, uint64_t bytes, std:
   algorithm = e->algorithm;
   nblocks = e->nblocks;
   nthreads = e->nthreads;
+  if (source) *source = e->source;
   return true;
 }
 
@@ -197,7 +209,7 @@ extern "C" int mscclppAmdTunedConfigLoad(const char* path) {
     if (!f) return (int)ncclInvalidArgument;
     std::stringstream ss;
     ss << f.rdbuf();
-    auto parsed = parseStore(ss.str());  // throws std::invalid_argument on a malformed file
+    auto parsed = parseStore(ss.str(), "tuned");  // throws std::invalid_argument on a malformed file
     Store& s = store();
     std::lock_guard<std::mutex> lk(s.mu);
     s.user = std::move(parsed);
@@ -217,6 +229,18 @@ extern "C" int mscclppAmdTunedConfig(const char* collective, int nranks, size_t 
     }
     if (nblocks) *nblocks = nb;
     if (nthreads) *nthreads = nt;
+    return (int)ncclSuccess;
+  });
+}
+
+extern "C" int mscclppAmdTunedConfigSource(const char* collective, int nranks, size_t bytes, char* source,
+                                           size_t sourceLen) {
+  return guarded([&] {
+    if (!collective) return (int)ncclInvalidArgument;
+    std::string name, src;
+    int nb = 0, nt = 0;
+    if (!tunedConfig(collective, nranks, bytes, name, nb, nt, &src)) return (int)ncclInvalidUsage;
+    if (source && sourceLen) std::snprintf(source, sourceLen, "%s", src.c_str());
     return (int)ncclSuccess;
   });
 }

@@ -21,6 +21,7 @@ for n, size in ((8, 1024), (8, 16384), (8, 16385), (8, 1 << 20), (8, (1 << 20) +
                 (2, 4096), (2, 262144), (2, 262145), (2, 1 << 20), (2, 48 << 20), (4, 65536)):
     out[f"ar/{{n}}/{{size}}"] = m.tuned_config("allreduce", n, size)
     out[f"sel/{{n}}/{{size}}"] = m.lib().mscclppAmdSelectAlgo(n, size, 0)
+    out[f"src/{{n}}/{{size}}"] = m.tuned_config_source("allreduce", n, size)
 out["ag"] = m.tuned_config("allgather", 8, 1 << 20)
 out["bcast"] = m.tuned_config("broadcast", 8, 1 << 20)
 print(json.dumps(out))
@@ -54,6 +55,11 @@ def test_builtin_table_restates_the_amd_thresholds(built):
     assert q["ar/2/1048576"][0] == "default_allreduce_allpair_packet"
     assert q["ar/2/50331648"][0] == "default_allreduce_fullmesh"
     assert q["ar/4/65536"][0] == "default_allreduce_packet"  # other scales: the reference's thresholds
+    # the defaults that came from fabric-free sweeps say so
+    assert q["src/2/262144"] == "fabric-free" and q["src/2/1048576"] == "fabric-free"
+    assert q["src/2/50331648"] == "reference"
+    assert q["src/8/1024"] == "reference" and q["src/8/50331648"] == "reference"
+    assert q["src/8/16385"] == "reference; grid fabric-free" and q["src/4/65536"] == "reference; grid fabric-free"
 
 
 def test_user_profile_overrides_by_scale(built, tmp_path):
@@ -72,6 +78,7 @@ def test_user_profile_overrides_by_scale(built, tmp_path):
     assert q["ar/8/1048576"] == ["default_allreduce_packet", 56, 512]
     assert q["ar/8/50331648"] == ["default_allreduce_rsag_zero_copy", 128, 512]
     assert q["sel/8/50331648"] == 5
+    assert q["src/8/50331648"] == "tuned" and q["src/2/4096"] == "fabric-free"  # a node table overrides
     # other scales: the built-in table
     assert q["ar/4/50331648"][0] == "default_allreduce_fullmesh" and q["sel/4/50331648"] == 3
     assert q["ar/2/4096"][0] == "default_allreduce_allpair_packet"
