@@ -3,15 +3,18 @@
 //   P = LL16(Y, flag)                 pack   (copyToPackets<LL16>, copy_device.hpp:160-171)
 //   O = X (op) unpack(P, flag)        reduce (LL16Packet::read + calVectorAccum, allreduce_packet.cu:93-108)
 //
-// One launch, two roles per workgroup.  Workgroup b packs tile t = i*G + b in round i and consumes
-// a tile packed by its partner b^1, so every packet is handed from one CU to a CU on a different
-// XCD (blocks are dealt round-robin over the 8 XCDs) purely through the LL flags, exactly as a peer
-// GPU's packets arrive in the AllReduce.  With SKEW (the default) the tile consumed in round i is
-// the one the partner packed in round i-1: it has had a whole round to land, so the first poll
-// finds its flags and no uncached 1 KiB packet line is re-read (the unskewed form consumed the
-// partner's tile of the same round and re-polled ~10 % of the packet bytes, profiles/r1f_*).  The
-// only residency requirement is that both workgroups of a pair are resident: the host keeps the
-// grid at or below 4 workgroups per CU (256 CUs).  Every spin is time-bounded.
+// One launch, two roles per wave.  Wave w of workgroup b packs its 1 KiB chunks of tile t = i*G + b
+// in round i and consumes the chunks its partner packed -- purely through the LL flags in the
+// packet buffer in memory, as a peer GPU's packets arrive in the AllReduce.  The partner is the
+// neighbouring wave w ^ 1 of the same workgroup (round 4, PMASK 0).  Rounds 1-3 paired workgroup b
+// with b ^ 1 on another XCD (blocks are dealt round-robin over the 8 XCDs); the packets crossed no
+// more memory that way, but every consumer then also waited for a workgroup the dispatcher had
+// started up to ~0.6 us later: 0.6-2 us of a 3-8 us one-round bucket and 2.5 us at 8 MiB
+// (profiles/r4a_small_bucket_probe*.json, r4a_multi_round_probe.json; the b ^ 1 and b ^ 8 forms
+// stay in the diagnostics library).  With SKEW the chunk consumed in round i is the one the partner
+// packed in round i - SKEW: it has had a round to land, so the first poll finds its flags and no
+// uncached 1 KiB packet line is re-read (profiles/r1f_*).  Every spin is time-bounded; a partner
+// lives in the same workgroup, so no residency requirement is left.
 //
 // Algorithmic HBM bytes per launch: 7*S (Y read S, P written 2S, P read 2S, X read S, O written S).
 #include "common.hpp"
@@ -40,12 +43,25 @@ namespace mscclpp_amd {
 // LP: cache policy of the X / Y payload loads and the output stores (nt for streaming buckets; the
 // one-round small form reads with the default policy, so a bucket written or read just before --
 // an AllReduce's input straight from its producer kernel -- is served from the caches).
-template <int DT, int OP, int W, int U, int SKEW, bool COUNT, int LP = kNonTemporal>
+//
+// PMASK: workgroup b's partner is b ^ PMASK (1: the neighbour, on another XCD; 8: the same XCD).
+// TR: diagnostic build that stamps lane 0 of wave 0's wall clock into trace[b * 8 + event] (pollMiss
+// is then a uint64_t trace buffer): 0 start, 1 payload loads landed, 2 packet stores acknowledged,
+// 3 partner's packets ready, 4 output stores acknowledged, 5 flags bumped.  Each stamp waits for the
+// wave's outstanding memory operations first, so the phases are serialised (diagnosis only).
+template <int DT, int OP, int W, int U, int SKEW, bool COUNT, int LP = kNonTemporal, int PMASK = 1, bool TR = false>
 __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t* __restrict__ x,
                                                                   const uint8_t* __restrict__ y, uint8_t* pkts,
                                                                   uint8_t* __restrict__ out, uint64_t bytes,
                                                                   uint32_t* flags, uint64_t budget, uint32_t* err,
                                                                   uint32_t* pollMiss) {
+  auto stamp = [&](int ev) {
+    if constexpr (TR) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0) ((uint64_t*)pollMiss)[blockIdx.x * 8 + ev] = wall_ticks();
+    }
+  };
+  stamp(0);
   constexpr uint32_t kWaves = W;
   constexpr uint64_t kTileBytes = (uint64_t)kWaves * U * 1024;  // payload bytes per workgroup and round
   __shared__ __attribute__((aligned(16))) uint8_t ldsP[kWaves][U][1024];
@@ -54,9 +70,13 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
   const uint32_t wave = wave_uniform(threadIdx.x / 64), lane = threadIdx.x % 64;  // wave-uniform: scalar rsrc
   const uint64_t ntiles = (bytes + kTileBytes - 1) / kTileBytes;
   const uint64_t rounds = (ntiles + G - 1) / G;
-  const uint32_t partner = b ^ 1u;
+  // PMASK 0: the partner is this workgroup itself and wave w consumes the chunks wave w ^ 1 packed
+  // (same CU); otherwise workgroup b ^ PMASK, wave for wave
+  const uint32_t partner = b ^ (uint32_t)PMASK;
+  const uint32_t cwave = PMASK == 0 ? (wave ^ 1u) : wave;
   // payload byte offset of (tile, sub-tile k) for this wave: 1 KiB chunks dealt k-major over waves
   auto chunk = [&](uint64_t t, int k) { return t * kTileBytes + (uint64_t)(k * kWaves + wave) * 1024; };
+  auto cchunk = [&](uint64_t t, int k) { return t * kTileBytes + (uint64_t)(k * kWaves + cwave) * 1024; };
   u32x4 yw[U];
   auto load_y = [&](uint64_t t) {
 #pragma unroll
@@ -69,7 +89,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
   auto load_x = [&](uint64_t tp) {
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-      const uint64_t c = chunk(tp, k);
+      const uint64_t c = cchunk(tp, k);
       if (c + lane * 16 < bytes) a[k] = load16<LP>(make_rsrc(x + c), lane * 16);
     }
   };
@@ -77,6 +97,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
   if (b < ntiles) load_y(b);
   if (SKEW == 0 && partner < G && partner < ntiles) load_x(partner);  // round 0's consumed tile
   const uint32_t flag = wave_uniform(flagv);
+  stamp(1);
   for (uint64_t i = 0; i < rounds + SKEW; ++i) {
     const uint64_t t = i * G + b;                           // packed this round (i < rounds)
     const uint64_t tp = (i - (uint64_t)SKEW) * G + partner;  // consumed this round (i >= SKEW)
@@ -97,6 +118,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
         if (c + lane * 8 < bytes) store16<kSystem>(rp, lane * 16, LL16Packet::make(lo.x, lo.y, flag));
         if (c + 512 + lane * 8 < bytes) store16<kSystem>(rp, 1024 + lane * 16, LL16Packet::make(hi.x, hi.y, flag));
       }
+      stamp(2);
       if (t + G < ntiles) load_y(t + G);
     }
     // ---- consume a partner tile: packet-major polls -> LDS -> payload-major sum and store
@@ -108,7 +130,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
       u32x4 v[2 * U];
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        const uint64_t c = chunk(tp, k);
+        const uint64_t c = cchunk(tp, k);
         const auto rp = __builtin_amdgcn_make_buffer_rsrc(pkts + 2 * c, 0, c < bytes ? 0xFFFFFFFFu : 0u, 0x00020000);
         v[2 * k] = load16<kSystem>(rp, c + lane * 8 < bytes ? lane * 16 : 0u);
         v[2 * k + 1] = load16<kSystem>(rp, c + 512 + lane * 8 < bytes ? 1024 + lane * 16 : 0u);
@@ -116,7 +138,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
       bool ok = true;
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        const uint64_t c = chunk(tp, k);
+        const uint64_t c = cchunk(tp, k);
         if (c + lane * 8 < bytes) ok &= LL16Packet::ready(v[2 * k], flag);
         if (c + 512 + lane * 8 < bytes) ok &= LL16Packet::ready(v[2 * k + 1], flag);
       }
@@ -124,7 +146,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
         uint32_t miss = 0;
 #pragma unroll
         for (int i2 = 0; i2 < 2 * U; ++i2) {
-          const uint64_t c = chunk(tp, i2 / 2);
+          const uint64_t c = cchunk(tp, i2 / 2);
           if (c + (i2 & 1) * 512 + lane * 8 < bytes && !LL16Packet::ready(v[i2], flag)) ++miss;
         }
         // wave-wide sum of the misses, one atomic per wave
@@ -134,7 +156,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
       if (!ok) {
 #pragma unroll
         for (int i2 = 0; i2 < 2 * U; ++i2) {
-          const uint64_t c = chunk(tp, i2 / 2);
+          const uint64_t c = cchunk(tp, i2 / 2);
           const uint32_t off = (i2 & 1) * 1024 + lane * 16;
           if (c + (i2 & 1) * 512 + lane * 8 < bytes && !LL16Packet::ready(v[i2], flag)) {
             const auto rp = make_rsrc(pkts + 2 * c);
@@ -149,6 +171,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
           }
         }
       }
+      stamp(3);
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         *(u32x2*)&ldsC[wave][k][lane * 8] = u32x2{v[2 * k].x, v[2 * k].z};
@@ -157,18 +180,27 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int k = 0; k < U; ++k) {
-        const uint64_t c = chunk(tp, k);
+        const uint64_t c = cchunk(tp, k);
         const u32x4 p = *(const u32x4*)&ldsC[wave][k][lane * 16];
         if (c + lane * 16 < bytes) store16<LP>(make_rsrc(out + c), lane * 16, reduce4<DT, OP>(a[k], p));
       }
+      stamp(4);
     }
     __builtin_amdgcn_wave_barrier();
   }
   bump_flags(flags, flag);
+  stamp(5);
 }
 
 // Launch shape of the product kernel for `bytes` (nblocks > 0: the caller's grid), from the
-// same-process shape sweeps (tools/sweep_self_reduce.py, profiles/r3_sweep_self_reduce.json):
+// same-process shape sweeps (tools/sweep_self_reduce.py, profiles/r3_sweep_self_reduce.json), and
+// since round 4 the one-round forms' hand-off partner from tools/small_bucket_probe.py
+// (profiles/r4_small_bucket_probe*.json): in one round a workgroup's waves hand their packets to
+// each other (wave w consumes wave w ^ 1's, same CU) instead of to workgroup b ^ 1 on another XCD.
+// The packets still go through the packet buffer in memory with their flags polled; what goes away
+// is the wait for a partner workgroup that the dispatcher started up to ~0.6 us later on another
+// XCD: 64-256 KiB 3.44-3.46 against 4.04-4.12 us, 1 MiB 3.40 / 4.57, 2 MiB 4.11 / 5.93, 4 MiB
+// 6.2 / 8.1 (graph-captured, one box).  Earlier notes:
 // 4 waves x 1 KiB per workgroup and round, one workgroup per 4 KiB tile up to 1024 workgroups (4 per
 // CU, all resident, so every partner pair is co-resident); 8 waves per workgroup for 1-4 MiB.
 //  * one round (up to 4 MiB): payload read and written with the default cache policy (a bucket just
@@ -204,15 +236,20 @@ static SelfReduceShape selfReduceShape(uint64_t bytes, int nblocks) {
   sh.nblocks = nblocks > 0 ? nblocks : (int)(tiles < 1024 ? tiles : 1024);
   if (sh.nblocks % 2) sh.nblocks += 1;
   const uint64_t rounds = (tiles + sh.nblocks - 1) / sh.nblocks;
-  sh.skew = rounds >= 8 ? 2 : rounds >= 3 ? 1 : 0;
+  // the partner is the neighbouring wave of the same workgroup in every form; with two or more rounds
+  // its tile is consumed a round late (two from 8 rounds): 8 MiB 10.6 against 13.1 us (the cross-XCD
+  // partner workgroup, unskewed), 16 MiB 19.4-19.5 / 21.9, 32-48 MiB even
+  // (profiles/r4a_multi_round_probe.json)
+  sh.skew = rounds >= 8 ? 2 : rounds >= 2 ? 1 : 0;
   sh.plain = rounds == 1;
   return sh;
 }
 
-template <int DT, int OP, int W, int U, int SKEW, bool COUNT, int LP = kNonTemporal>
+template <int DT, int OP, int W, int U, int SKEW, bool COUNT, int LP = kNonTemporal, int PMASK = 1, bool TR = false>
 static void launchSelfReduceShape(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                                   int nblocks, uint64_t budget, uint32_t* err, uint32_t* pollMiss, hipStream_t stream) {
-  hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, W, U, SKEW, COUNT, LP>), dim3(nblocks), dim3(64 * W), 0, stream,
+  hipLaunchKernelGGL((selfReduceLL16LdsKernel<DT, OP, W, U, SKEW, COUNT, LP, PMASK, TR>), dim3(nblocks), dim3(64 * W), 0,
+                     stream,
                      (const uint8_t*)x, (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, bytes, flags, budget, err,
                      pollMiss);
 }
@@ -221,21 +258,22 @@ template <int DT, int OP>
 static void launchSelfReduce(const void* x, const void* y, void* pkts, void* out, uint64_t bytes, uint32_t* flags,
                              int nblocks, uint64_t budget, uint32_t* err, hipStream_t stream) {
   const SelfReduceShape sh = selfReduceShape(bytes, nblocks);
+  // wave w of a workgroup consumes what wave w ^ 1 of the same workgroup packed (PMASK 0)
   if (sh.waves == 8)
-    launchSelfReduceShape<DT, OP, 8, 1, 0, false, kPlain>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err,
-                                                              nullptr, stream);
+    launchSelfReduceShape<DT, OP, 8, 1, 0, false, kPlain, 0>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err,
+                                                                 nullptr, stream);
   else if (sh.plain)
-    launchSelfReduceShape<DT, OP, 4, 1, 0, false, kPlain>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err,
-                                                              nullptr, stream);
+    launchSelfReduceShape<DT, OP, 4, 1, 0, false, kPlain, 0>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err,
+                                                                 nullptr, stream);
   else if (sh.skew == 2)
-    launchSelfReduceShape<DT, OP, 4, 1, 2, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
-                                                  stream);
+    launchSelfReduceShape<DT, OP, 4, 1, 2, false, kNonTemporal, 0>(x, y, pkts, out, bytes, flags, sh.nblocks, budget,
+                                                                   err, nullptr, stream);
   else if (sh.skew == 1)
-    launchSelfReduceShape<DT, OP, 4, 1, 1, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
-                                                     stream);
-  else
-    launchSelfReduceShape<DT, OP, 4, 1, 0, false>(x, y, pkts, out, bytes, flags, sh.nblocks, budget, err, nullptr,
-                                                      stream);
+    launchSelfReduceShape<DT, OP, 4, 1, 1, false, kNonTemporal, 0>(x, y, pkts, out, bytes, flags, sh.nblocks, budget,
+                                                                   err, nullptr, stream);
+  else  // a caller's grid with more workgroups than tiles
+    launchSelfReduceShape<DT, OP, 4, 1, 0, false, kNonTemporal, 0>(x, y, pkts, out, bytes, flags, sh.nblocks, budget,
+                                                                   err, nullptr, stream);
 }
 
 // Streaming copy (read S, write S) used by the benchmark to measure the achievable HBM ceiling on
@@ -337,7 +375,20 @@ extern "C" int mscclppAmdSelfReduceLL16Shape(const void* x, const void* y, void*
   // count: bit 0 = count first-poll misses, bit 1 = default-policy payload loads / stores (the small
   // form's choice)
   const bool plain = (count & 2) != 0;
+  const int pmask = (count & 4) ? 0 : (count & 8) ? 8 : 1;  // bit 2: partner wave w ^ 1 of the workgroup; bit 3: b ^ 8
   count &= 1;
+  if (pmask != 1) {  // 4 x 1 KiB waves, nt payload, skew 0 / 1 / 2 (multi-round forms)
+    if (waves != 4 || units != 1 || count || plain || (pmask == 8 && nblocks % 16)) return 4;
+#define SRPM(SK, PM)                                                                                              \
+    if (skew == SK && pmask == PM) {                                                                              \
+      launchSelfReduceShape<kF16, kSum, 4, 1, SK, false, kNonTemporal, PM>(x, y, pkts, out, bytes, flags, nblocks, \
+                                                                          budgetTicks, err, pollMiss, s);          \
+      return hipGetLastError() == hipSuccess ? 0 : 1;                                                             \
+    }
+    SRPM(0, 0) SRPM(1, 0) SRPM(2, 0) SRPM(0, 8) SRPM(1, 8) SRPM(2, 8)
+#undef SRPM
+    return 4;
+  }
 #define SRS(W, U, SK, C)                                                                                      \
   if (waves == W && units == U && skew == SK && (count != 0) == C) {                                          \
     if (plain)                                                                                                \
@@ -353,6 +404,31 @@ extern "C" int mscclppAmdSelfReduceLL16Shape(const void* x, const void* y, void*
   SRS(4, 1, 2, false) SRS(4, 1, 2, true) SRS(4, 2, 2, false) SRS(4, 2, 2, true)
 #undef SRS_SK
 #undef SRS
+  return 4;
+}
+
+// Small-bucket probe (fp16 SUM, one round, default-policy payload): `waves` per workgroup on
+// `nblocks` workgroups of one 1 KiB tile per wave, partners b ^ pmask (1 or 8; with 8 the grid must be
+// a multiple of 16; 0: wave w ^ 1 of the same workgroup), trace != 0: phase stamps into `trace` (nblocks * 8 uint64).
+extern "C" int mscclppAmdSelfReduceSmallProbe(const void* x, const void* y, void* pkts, void* out, size_t bytes,
+                                              uint32_t* flags, int nblocks, int waves, int pmask, uint64_t* trace,
+                                              uint64_t budgetTicks, uint32_t* err, void* streamPtr) {
+  hipStream_t s = (hipStream_t)streamPtr;
+  if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0 || nblocks <= 0 || nblocks > 1024) return 4;
+  if ((uint64_t)nblocks * waves * 1024 < bytes) return 4;  // one round only
+  if (pmask == 8 ? (nblocks % 16) != 0 : pmask == 0 ? waves < 2 : (pmask != 1 || nblocks % 2)) return 4;
+  uint32_t* tr = (uint32_t*)trace;
+#define SRP(W, PM, T)                                                                                          \
+  if (waves == W && pmask == PM && (trace != nullptr) == T) {                                                 \
+    launchSelfReduceShape<kF16, kSum, W, 1, 0, false, kPlain, PM, T>(x, y, pkts, out, bytes, flags, nblocks,   \
+                                                                      budgetTicks, err, tr, s);                \
+    return hipGetLastError() == hipSuccess ? 0 : 1;                                                           \
+  }
+#define SRP_W(W) SRP(W, 1, false) SRP(W, 1, true) SRP(W, 8, false) SRP(W, 8, true) SRP(W, 0, false) SRP(W, 0, true)
+  SRP(1, 1, false) SRP(1, 1, true) SRP(1, 8, false) SRP(1, 8, true)
+  SRP_W(2) SRP_W(4) SRP_W(8) SRP_W(16)
+#undef SRP_W
+#undef SRP
   return 4;
 }
 #endif
