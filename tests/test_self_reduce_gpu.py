@@ -94,7 +94,7 @@ def test_self_reduce_rejects_unaligned(built):
 
 @pytest.mark.parametrize("nbytes,waves,nblocks,skew", [
     (16, 4, 2, 0), (1 << 20, 4, 256, 0), ((1 << 20) + 48, 8, 130, 0), (4 << 20, 8, 512, 0),
-    ((4 << 20) + 16, 4, 1024, 0), ((8 << 20) + 16, 4, 1024, 1), ((24 << 20) + 16, 4, 1024, 1),
+    ((4 << 20) + 16, 4, 1024, 1), ((8 << 20) + 16, 4, 1024, 1), ((24 << 20) + 16, 4, 1024, 1),
     ((32 << 20) + 16, 4, 1024, 2), (48 << 20, 4, 1024, 2)])
 def test_self_reduce_default_shape(built, nbytes, waves, nblocks, skew):
     """The launch shape the product entry picks (4 waves x 1 KiB, one workgroup per 4 KiB up to 1024,
