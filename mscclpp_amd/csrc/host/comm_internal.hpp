@@ -87,6 +87,15 @@ int guarded(F&& f) {
   } catch (const HipError& e) {
     warn(e.what());
     return ncclUnhandledCudaError;
+  } catch (const mscclpp_amd::Error& e) {  // the host channel API's errors (core.hpp)
+    warn(e.what());
+    switch (e.getErrorCode()) {
+      case mscclpp_amd::ErrorCode::InvalidUsage: return ncclInvalidUsage;
+      case mscclpp_amd::ErrorCode::RemoteError:
+      case mscclpp_amd::ErrorCode::Timeout: return ncclRemoteError;
+      case mscclpp_amd::ErrorCode::SystemError: return ncclSystemError;
+      default: return ncclInternalError;
+    }
   } catch (const std::invalid_argument& e) {
     warn(e.what());
     return ncclInvalidArgument;

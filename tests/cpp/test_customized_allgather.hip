@@ -6,7 +6,14 @@
 // HIP graph of calls.  Every rank's output is checked exactly.  The kernel and the host-side API calls
 // keep the example's spellings (namespace alias; HIP instead of CUDA runtime names).
 //
-//   test_customized_allgather gpu <nranks> [floats per rank]
+//   test_customized_allgather gpu <nranks> [floats per rank] [cached | uncached | refuse]
+//
+// The PortChannel destination contract: `cached` (default, the example's
+// cudaMalloc -> hipMalloc) is exact -- the receiving kernel only signals, the data is read after it
+// -- and ProxyService warns once that the destination is cached device memory; `uncached` allocates
+// the receive buffer from the uncached pool (no warning); `refuse` runs with
+// MSCCLPP_AMD_PORT_CHANNEL_DST=strict and expects the first ncclAllGather to return
+// ncclInvalidUsage (2 ranks: every rank refuses at its first and only peer).
 #include <hip/hip_runtime.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -170,7 +177,7 @@ class AllgatherAlgoBuilder : public mscclpp::AlgorithmBuilder {
   }
 };
 
-static int worker(int rank, int worldSize, ncclUniqueId id, size_t size) {
+static int worker(int rank, int worldSize, ncclUniqueId id, size_t size, const std::string& mode) {
   const int iter = 10;
   int ndev = 0;
   HIP_OK(hipGetDeviceCount(&ndev));
@@ -191,7 +198,11 @@ static int worker(int rank, int worldSize, ncclUniqueId id, size_t size) {
   float *sendbuff, *recvbuff;
   hipStream_t stream;
   HIP_OK(hipMalloc(&sendbuff, size * sizeof(float)));
-  HIP_OK(hipMalloc(&recvbuff, size * sizeof(float) * worldSize));
+  if (mode == "uncached")
+    CHECK(mscclppAmdMallocUncached((void**)&recvbuff, size * sizeof(float) * worldSize) == 0);
+  else
+    HIP_OK(hipMalloc(&recvbuff, size * sizeof(float) * worldSize));
+  if (mode == "refuse") setenv("MSCCLPP_AMD_PORT_CHANNEL_DST", "strict", 1);
   std::vector<float> h(size);
   for (size_t i = 0; i < size; ++i) h[i] = (float)(rank * 1000003 + (int)(i % 999983));
   HIP_OK(hipMemcpy(sendbuff, h.data(), size * sizeof(float), hipMemcpyHostToDevice));
@@ -210,6 +221,18 @@ static int worker(int rank, int worldSize, ncclUniqueId id, size_t size) {
           std::exit(1);
         }
   };
+  if (mode == "refuse") {  // the context's portChannel() refuses the cached destination
+    const ncclResult_t r = ncclAllGather(sendbuff, recvbuff, size, ncclFloat, comm, stream);
+    CHECK(r == ncclInvalidUsage);
+    CHECK(std::string(ncclGetLastError(comm)).find("cached device memory") != std::string::npos);
+    CHECK(ncclCommDestroy(comm) == ncclSuccess);
+    HIP_OK(hipFree(sendbuff));
+    HIP_OK(hipFree(recvbuff));
+    algoCollectionBuilder->reset();
+    std::printf("rank %d refused OK\n", rank);
+    std::fflush(stdout);
+    return 0;
+  }
   // direct calls (the first one builds the context)
   CHECK(ncclAllGather(sendbuff, recvbuff, size, ncclFloat, comm, stream) == ncclSuccess);
   HIP_OK(hipStreamSynchronize(stream));
@@ -245,7 +268,10 @@ static int worker(int rank, int worldSize, ncclUniqueId id, size_t size) {
   HIP_OK(hipGraphDestroy(graph));
   CHECK(ncclCommDestroy(comm) == ncclSuccess);
   HIP_OK(hipFree(sendbuff));
-  HIP_OK(hipFree(recvbuff));
+  if (mode == "uncached")
+    CHECK(mscclppAmdFree(recvbuff) == 0);
+  else
+    HIP_OK(hipFree(recvbuff));
   algoCollectionBuilder->reset();
   std::printf("rank %d OK\n", rank);
   std::fflush(stdout);
@@ -256,13 +282,15 @@ int main(int argc, char** argv) {
   if (argc >= 3 && std::string(argv[1]) == "gpu") {
     const int n = std::atoi(argv[2]);
     const size_t size = argc >= 4 ? (size_t)std::atoll(argv[3]) : (size_t)1 << 20;
+    const std::string mode = argc >= 5 ? argv[4] : "cached";
+    if (mode != "cached" && mode != "uncached" && mode != "refuse") return 2;
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) return 1;
     std::vector<pid_t> pids;
     for (int r = 0; r < n; ++r) {
       pid_t pid = fork();
       if (pid < 0) return 1;
-      if (pid == 0) std::_Exit(worker(r, n, id, size));
+      if (pid == 0) std::_Exit(worker(r, n, id, size, mode));
       pids.push_back(pid);
     }
     int bad = 0;

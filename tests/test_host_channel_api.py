@@ -47,6 +47,18 @@ def test_memory_and_port_channels_reference_spellings(built):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [2, 4])
-def test_customized_allgather_port_channels(built, n):
-    out = _run("test_customized_allgather", ["gpu", str(n), str(1 << 18)], 200)
+@pytest.mark.parametrize("mode", ["cached", "uncached"])
+def test_customized_allgather_port_channels(built, n, mode):
+    """PortChannel destinations: the example's hipMalloc receive
+    buffer is exact and gets the one-time warning; a pool (uncached) receive buffer gets none."""
+    out = _run("test_customized_allgather", ["gpu", str(n), str(1 << 18), mode], 200)
     assert "gpu OK" in out and all(f"rank {r} OK" in out for r in range(n)), out
+    assert ("is cached device memory" in out) == (mode == "cached"), out
+
+
+@pytest.mark.gpu
+def test_port_channel_strict_refuses_cached_destination(built):
+    """MSCCLPP_AMD_PORT_CHANNEL_DST=strict: a PortChannel into cached device memory is refused with
+    ncclInvalidUsage and the reason in ncclGetLastError."""
+    out = _run("test_customized_allgather", ["gpu", "2", str(1 << 12), "refuse"], 120)
+    assert "gpu OK" in out and "rank 0 refused OK" in out and "rank 1 refused OK" in out, out
