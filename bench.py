@@ -364,6 +364,24 @@ def same_run_ceilings(m, S, x, y, pk, out, flags, err, kern_ms, reps=20):
     torch.cuda.synchronize()
     mix_us = a.elapsed_time(b) * 1e3 / reps
     mix_gbs = 7 * S / (mix_us * 1e-6) / 1e9
+    # an independent ceiling of the same 4:3 read:write mix: a generic grid-stride kernel with none
+    # of the self-reduce's layout, grid or rounds (mscclppAmdMixStream), separate write buffers
+    pout = torch.empty(2 * S, dtype=torch.uint8, device=x.device)
+
+    def generic():
+        m.check(L.mscclppAmdMixStream(vp(x.data_ptr()), vp(y.data_ptr()), vp(pk.ptr), vp(pout.data_ptr()),
+                                      vp(dst.data_ptr()), S, 0, m.stream_ptr()), "generic mix")
+
+    generic()
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(reps):
+        generic()
+    b.record()
+    torch.cuda.synchronize()
+    gen_us = a.elapsed_time(b) * 1e3 / reps
+    gen_gbs = 7 * S / (gen_us * 1e-6) / 1e9
+    del pout
     scrub = torch.empty(512 << 20, dtype=torch.uint8, device=x.device)
 
     def one_pair(cold):
@@ -389,6 +407,10 @@ def same_run_ceilings(m, S, x, y, pk, out, flags, err, kern_ms, reps=20):
             "mix_us": round(mix_us, 2), "frac_of_mix_ceiling": round(seven / (kern_ms * 1e-3) / 1e9 / mix_gbs, 4),
             "mix_note": "mix: the kernel's own 7*S accesses on the same buffers, grid and rounds with no flags, "
                         "polls or LDS (mscclppAmdSelfReduceStream)",
+            "generic_mix_ceiling_GBs": round(gen_gbs, 1), "generic_mix_us": round(gen_us, 2),
+            "frac_of_generic_mix_ceiling": round(seven / (kern_ms * 1e-3) / 1e9 / gen_gbs, 4),
+            "generic_mix_note": "an independent ceiling of the 4:3 read:write mix: a grid-stride kernel over 16-byte "
+                                "units, 2048 x 256 lanes, nt accesses, separate write buffers (mscclppAmdMixStream)",
             "cold": {"kernel_us": round(res["cold"], 2),
                      "achieved": round(seven / (res["cold"] * 1e-6) / 1e9, 1),
                      "frac": round(seven / (res["cold"] * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),

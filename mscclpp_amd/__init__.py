@@ -116,6 +116,7 @@ def lib():
         "mscclppAmdCommDeregisterAll": [vp],
         "mscclppAmdCopy": [vp, vp, sz, i32, vp],
         "mscclppAmdSelfReduceStream": [vp, vp, vp, vp, sz, vp],
+        "mscclppAmdMixStream": [vp, vp, vp, vp, vp, sz, i32, vp],
         "mscclppAmdCopyJobs": [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz), i32, i32, vp],
         "mscclppAmdCopyJobsPolicy": [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(sz), i32, i32, i32, i32, vp],
         "mscclppAmdSelfReduceLL16DefaultShape": [sz, vp, vp, vp, vp],

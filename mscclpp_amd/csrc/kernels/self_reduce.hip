@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(256) copyKernel(const uint8_t* __restrict__ sr
 
 // Same-traffic streaming ceiling of the self-reduce (benchmark only): the large form's exact memory
 // accesses -- per wave and round, 1 KiB of Y read, 2 KiB of packets stored packet-major (two 1 KiB
-// instructions, system scope), the partner's 2 KiB of packets from two rounds earlier read (system
+// instructions, system scope), the partner wave's 2 KiB of packets from two rounds earlier read (system
 // scope), 1 KiB of X read and 1 KiB of O written, all on the same buffers, grid and rounds -- with no
 // flags, readiness tests, re-polls or LDS.  Its time is what the memory system gives this 7*S access
 // mix; the product kernel's time against it is the cost of the hand-off itself.  (The packets read
@@ -312,8 +312,9 @@ __global__ void __launch_bounds__(256) selfReduceStreamKernel(const uint8_t* __r
   for (uint64_t i = 0; i < rounds; ++i) {
     const uint64_t t = i * G + b;
     if (t >= ntiles) break;
-    const uint64_t tp = ((i >= 2 ? i - 2 : i + rounds - 2) * G + (b ^ 1u)) % ntiles;  // partner, two rounds late
-    const uint64_t c = t * kTile + wave * 1024, cp = tp * kTile + wave * 1024;
+    // the product's partner (round 4): wave ^ 1 of the same workgroup, its tile two rounds late
+    const uint64_t tp = ((i >= 2 ? i - 2 : i + rounds - 2) * G + b) % ntiles;
+    const uint64_t c = t * kTile + wave * 1024, cp = tp * kTile + (wave ^ 1u) * 1024;
     const u32x4 yv = load16<kNonTemporal>(make_rsrc(y + c), lane * 16);
     const u32x4 xv = load16<kNonTemporal>(make_rsrc(x + cp), lane * 16);
     const auto rpp = make_rsrc(pkts + 2 * cp);
@@ -323,6 +324,41 @@ __global__ void __launch_bounds__(256) selfReduceStreamKernel(const uint8_t* __r
     store16<kSystem>(rp, lane * 16, u32x4{yv.x, 0u, yv.y, 0u});  // flag 0: no call ever waits for it
     store16<kSystem>(rp, 1024 + lane * 16, u32x4{yv.z, 0u, yv.w, 0u});
     store16<kNonTemporal>(make_rsrc(out + cp), lane * 16, u32x4{xv.x ^ p0.x, xv.y ^ p0.z, xv.z ^ p1.x, xv.w ^ p1.z});
+  }
+}
+
+// An independent ceiling for the same 4:3 read:write mix (benchmark only): none of the self-reduce's
+// choices -- a grid-stride loop over 16-byte units, 2048 workgroups of 256 lanes, U units per lane in
+// flight, every access non-temporal; per unit X, Y and two packet units read from `pin`, two units
+// written to a separate `pout` and one to `out` (4 * bytes read, 3 * bytes written, no buffer read
+// and written in the same launch).
+template <int U>
+__global__ void __launch_bounds__(256) mixStreamKernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
+                                                       const uint8_t* __restrict__ pin, uint8_t* __restrict__ pout,
+                                                       uint8_t* __restrict__ out, uint64_t nunits) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t u0 = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; u0 < nunits; u0 += stride) {
+    u32x4 a[U], b[U], p0[U], p1[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t u = u0 + (uint64_t)k * 256;
+      if (u < nunits) {
+        a[k] = load16<kNonTemporal>(make_rsrc(x), (uint32_t)(u * 16));
+        b[k] = load16<kNonTemporal>(make_rsrc(y), (uint32_t)(u * 16));
+        p0[k] = load16<kNonTemporal>(make_rsrc(pin), (uint32_t)(u * 32));
+        p1[k] = load16<kNonTemporal>(make_rsrc(pin), (uint32_t)(u * 32 + 16));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const uint64_t u = u0 + (uint64_t)k * 256;
+      if (u < nunits) {
+        store16<kNonTemporal>(make_rsrc(pout), (uint32_t)(u * 32), u32x4{b[k].x, 0u, b[k].y, 0u});
+        store16<kNonTemporal>(make_rsrc(pout), (uint32_t)(u * 32 + 16), u32x4{b[k].z, 0u, b[k].w, 0u});
+        store16<kNonTemporal>(make_rsrc(out), (uint32_t)(u * 16),
+                              u32x4{a[k].x ^ p0[k].x, a[k].y ^ p0[k].z, a[k].z ^ p1[k].x, a[k].w ^ p1[k].z});
+      }
+    }
   }
 }
 
@@ -463,6 +499,16 @@ extern "C" int mscclppAmdSelfReduceStream(const void* x, const void* y, void* pk
   const int nblocks = (int)(tiles < 1024 ? tiles : 1024);
   hipLaunchKernelGGL(selfReduceStreamKernel, dim3(nblocks), dim3(256), 0, (hipStream_t)streamPtr, (const uint8_t*)x,
                      (const uint8_t*)y, (uint8_t*)pkts, (uint8_t*)out, (uint64_t)bytes);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+extern "C" int mscclppAmdMixStream(const void* x, const void* y, const void* pin, void* pout, void* out, size_t bytes,
+                                   int nblocks, void* streamPtr) {
+  // buffer offsets are 32-bit (buffer resources): pin / pout hold 2 * bytes
+  if (!x || !y || !pin || !pout || !out || bytes == 0 || bytes % 16 || 2 * (uint64_t)bytes > 0xFFFFFFF0ull) return 4;
+  if (nblocks <= 0) nblocks = 2048;
+  hipLaunchKernelGGL((mixStreamKernel<4>), dim3(nblocks), dim3(256), 0, (hipStream_t)streamPtr, (const uint8_t*)x,
+                     (const uint8_t*)y, (const uint8_t*)pin, (uint8_t*)pout, (uint8_t*)out, (uint64_t)(bytes / 16));
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
