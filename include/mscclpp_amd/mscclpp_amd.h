@@ -104,6 +104,13 @@ int mscclppAmdUncachedPoolStats(size_t* held, size_t* inUse, size_t* freeBytes);
  * pointer may be NULL. */
 int mscclppAmdIpcStats(size_t* openMappings, size_t* keptImports);
 int mscclppAmdIpcKeptRanges(uint64_t* addrs, uint64_t* bytes, size_t cap, size_t* n);
+/* Forget the kept imports (after a device synchronize): each closes unless a live communicator still
+ * holds it.  For a long-lived process whose peers come and go (an elastic job re-creating its peer
+ * processes): a kept import keeps the exited peer's memory alive.  Call it only with no communicator
+ * of the departed peers left, and expect this process's next allocations to be placed where the
+ * closed mappings were -- the hazard DESIGN.md §21 describes, which the kept imports otherwise rule
+ * out. */
+int mscclppAmdIpcReleaseKept(size_t* released);
 int mscclppAmdFlagsInit(uint32_t* flags, void* stream);
 
 /* ---- 1-GPU microbench (BASELINE config 2) ------------------------------------------------- */

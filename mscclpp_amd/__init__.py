@@ -99,6 +99,7 @@ def lib():
         "mscclppAmdUncachedPoolStats": [ctypes.POINTER(sz), ctypes.POINTER(sz), ctypes.POINTER(sz)],
         "mscclppAmdIpcStats": [ctypes.POINTER(sz), ctypes.POINTER(sz)],
         "mscclppAmdIpcKeptRanges": [ctypes.POINTER(u64), ctypes.POINTER(u64), sz, ctypes.POINTER(sz)],
+        "mscclppAmdIpcReleaseKept": [ctypes.POINTER(sz)],
         "mscclppAmdTraceSet": [vp, sz],
         "mscclppAmdFlagsInit": [vp, vp],
         "mscclppAmdSelfReduceLL16": [vp, vp, vp, vp, sz, i32, i32, vp, i32, u64, vp, vp],
@@ -233,6 +234,13 @@ def ipc_kept_ranges():
     addrs, sizes = (ctypes.c_uint64 * max(cap, 1))(), (ctypes.c_uint64 * max(cap, 1))()
     check(lib().mscclppAmdIpcKeptRanges(addrs, sizes, cap, ctypes.byref(n)), "ipc kept ranges")
     return [(addrs[i], sizes[i]) for i in range(min(cap, n.value))]
+
+
+def ipc_release_kept():
+    """Forget the kept imports of peers' pooled blocks (mscclppAmdIpcReleaseKept); returns how many."""
+    n = ctypes.c_size_t()
+    check(lib().mscclppAmdIpcReleaseKept(ctypes.byref(n)), "ipc release kept")
+    return n.value
 
 
 def flags_init(flags_tensor, stream=None):

@@ -49,6 +49,15 @@ int mscclppAmdIpcStats(size_t* openMappings, size_t* keptImports) {
   });
 }
 
+int mscclppAmdIpcReleaseKept(size_t* released) {
+  return guarded([&] {
+    HIPCHECK(hipDeviceSynchronize());  // no queued kernel may still read through a mapping closed here
+    const size_t n = releaseKeptIpcImports();
+    if (released) *released = n;
+    return (int)ncclSuccess;
+  });
+}
+
 int mscclppAmdIpcKeptRanges(uint64_t* addrs, uint64_t* bytes, size_t cap, size_t* n) {
   return guarded([&] {
     std::vector<std::pair<uint64_t, uint64_t>> kept;

@@ -225,6 +225,7 @@ std::shared_ptr<void> openIpcImport(const hipIpcMemHandle_t& handle, uint64_t ow
                                     bool pooled);
 uint64_t processNonce();  // random, fixed per process: tells exporters' pools apart
 void keptIpcImports(std::vector<std::pair<uint64_t, uint64_t>>* ranges);  // (mapped address, bytes)
+size_t releaseKeptIpcImports();  // forget every kept import (mscclppAmdIpcReleaseKept)
 size_t liveIpcMappings();
 uint64_t allocationId(const void* ptr);  // HIP_POINTER_ATTRIBUTE_BUFFER_ID (0 if unknown)
 // Tuned configuration (tuning.cpp) for a collective of `bytes` on `nranks` ranks of this device's

@@ -117,6 +117,15 @@ std::shared_ptr<void> openIpcImport(const hipIpcMemHandle_t& handle, uint64_t ow
   return p;
 }
 
+size_t releaseKeptIpcImports() {
+  std::map<std::pair<uint64_t, uint64_t>, Kept> drop;
+  {
+    std::lock_guard<std::mutex> lk(gKeptMu);
+    drop.swap(gKept);
+  }
+  return drop.size();  // each mapping closes here unless a live owner (a communicator) still holds it
+}
+
 void keptIpcImports(std::vector<std::pair<uint64_t, uint64_t>>* ranges) {
   std::lock_guard<std::mutex> lk(gKeptMu);
   ranges->clear();

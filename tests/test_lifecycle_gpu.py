@@ -140,6 +140,9 @@ def _worker(rank, uids, q):
         comm.barrier()
         del g
         comm.destroy()
+        # with no communicator left, the kept imports can be forgotten explicitly (elastic jobs)
+        res["released"] = m.ipc_release_kept()
+        res["kept_after_release"] = m.ipc_stats()[1]
         q.put((rank, res, None))
     except Exception:
         q.put((rank, None, traceback.format_exc()))
@@ -181,3 +184,4 @@ def test_create_destroy_cycles_pool_and_imports_bounded(built):
         assert res["overlaps"] == 0 and res["lost"] == [], (rank, res)
         assert res["capture_code"] == 5, (rank, res)  # ncclInvalidUsage
         assert res["bad_graph"] == 0, (rank, res)
+        assert res["released"] >= kept[0] and res["kept_after_release"] == 0, (rank, res)
