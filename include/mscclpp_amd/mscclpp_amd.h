@@ -143,7 +143,7 @@ int mscclppAmdCopyJobsPolicy(const void* const* srcs, void* const* dsts, const s
 int mscclppAmdSelfReduceStream(const void* x, const void* y, void* pkts, void* out, size_t bytes, void* stream);
 /* An independent streaming ceiling of the same 4:3 read:write mix, with none of the self-reduce's
  * layout or grid: X, Y (bytes each) and pin (2 * bytes) read, pout (2 * bytes) and out written, one
- * grid-stride loop, 2048 workgroups by default, non-temporal accesses.  bytes % 16 == 0. */
+ * grid-stride loop, 2048 workgroups by default, non-temporal accesses.  bytes % 4096 == 0. */
 int mscclppAmdMixStream(const void* x, const void* y, const void* pin, void* pout, void* out, size_t bytes, int nblocks,
                         void* stream);
 

@@ -336,25 +336,27 @@ template <int U>
 __global__ void __launch_bounds__(256) mixStreamKernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ y,
                                                        const uint8_t* __restrict__ pin, uint8_t* __restrict__ pout,
                                                        uint8_t* __restrict__ out, uint64_t nunits) {
-  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
-  for (uint64_t u0 = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; u0 < nunits; u0 += stride) {
+  // a workgroup's pass covers 256 * U units of X / Y / out and the 512 * U units of pin / pout at twice
+  // their offset; every wave instruction touches 1 KiB of contiguous, whole lines
+  const uint64_t step = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 * U; base < nunits; base += step) {
     u32x4 a[U], b[U], p0[U], p1[U];
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-      const uint64_t u = u0 + (uint64_t)k * 256;
+      const uint64_t u = base + (uint64_t)k * 256 + threadIdx.x, q = 2 * (base + (uint64_t)k * 256) + threadIdx.x;
       if (u < nunits) {
         a[k] = load16<kNonTemporal>(make_rsrc(x), (uint32_t)(u * 16));
         b[k] = load16<kNonTemporal>(make_rsrc(y), (uint32_t)(u * 16));
-        p0[k] = load16<kNonTemporal>(make_rsrc(pin), (uint32_t)(u * 32));
-        p1[k] = load16<kNonTemporal>(make_rsrc(pin), (uint32_t)(u * 32 + 16));
+        p0[k] = load16<kNonTemporal>(make_rsrc(pin), (uint32_t)(q * 16));
+        p1[k] = load16<kNonTemporal>(make_rsrc(pin), (uint32_t)((q + 256) * 16));
       }
     }
 #pragma unroll
     for (int k = 0; k < U; ++k) {
-      const uint64_t u = u0 + (uint64_t)k * 256;
+      const uint64_t u = base + (uint64_t)k * 256 + threadIdx.x, q = 2 * (base + (uint64_t)k * 256) + threadIdx.x;
       if (u < nunits) {
-        store16<kNonTemporal>(make_rsrc(pout), (uint32_t)(u * 32), u32x4{b[k].x, 0u, b[k].y, 0u});
-        store16<kNonTemporal>(make_rsrc(pout), (uint32_t)(u * 32 + 16), u32x4{b[k].z, 0u, b[k].w, 0u});
+        store16<kNonTemporal>(make_rsrc(pout), (uint32_t)(q * 16), u32x4{b[k].x, 0u, b[k].y, 0u});
+        store16<kNonTemporal>(make_rsrc(pout), (uint32_t)((q + 256) * 16), u32x4{b[k].z, 0u, b[k].w, 0u});
         store16<kNonTemporal>(make_rsrc(out), (uint32_t)(u * 16),
                               u32x4{a[k].x ^ p0[k].x, a[k].y ^ p0[k].z, a[k].z ^ p1[k].x, a[k].w ^ p1[k].z});
       }
@@ -505,7 +507,8 @@ extern "C" int mscclppAmdSelfReduceStream(const void* x, const void* y, void* pk
 extern "C" int mscclppAmdMixStream(const void* x, const void* y, const void* pin, void* pout, void* out, size_t bytes,
                                    int nblocks, void* streamPtr) {
   // buffer offsets are 32-bit (buffer resources): pin / pout hold 2 * bytes
-  if (!x || !y || !pin || !pout || !out || bytes == 0 || bytes % 16 || 2 * (uint64_t)bytes > 0xFFFFFFF0ull) return 4;
+  // whole 4 KiB passes only: a pass's pin / pout units lie inside 2 * bytes exactly when it is whole
+  if (!x || !y || !pin || !pout || !out || bytes == 0 || bytes % 4096 || 2 * (uint64_t)bytes > 0xFFFFFFF0ull) return 4;
   if (nblocks <= 0) nblocks = 2048;
   hipLaunchKernelGGL((mixStreamKernel<4>), dim3(nblocks), dim3(256), 0, (hipStream_t)streamPtr, (const uint8_t*)x,
                      (const uint8_t*)y, (const uint8_t*)pin, (uint8_t*)pout, (uint8_t*)out, (uint64_t)(bytes / 16));
