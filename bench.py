@@ -642,6 +642,8 @@ def bench_multi(args):
         try:
             for j in range(2):
                 comm.all_reduce(xs[j], out, algo=a, nblocks=nb, nthreads=nt)
+            torch.cuda.synchronize()
+            dist.barrier()  # the ranks start each candidate's timed calls together
             tune[(a, nb, nt)] = tmax(_time_calls(lambda: comm.all_reduce(xs[0], out, algo=a, nblocks=nb, nthreads=nt), 5))
         except Exception as e:  # a rejected shape is simply skipped
             tune[(a, nb, nt)] = float("inf")
@@ -1117,6 +1119,8 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
                 try:
                     for _ in range(2):
                         comm.all_reduce(xs, os_, algo=a, nblocks=nb_, nthreads=nt_)
+                    torch.cuda.synchronize()
+                    barrier()
                     row[f"{a}:{nb_}x{nt_}"] = round(tmax(_time_calls(
                         lambda: comm.all_reduce(xs, os_, algo=a, nblocks=nb_, nthreads=nt_), 5)) * 1e6, 1)
                 except Exception as e:  # noqa: BLE001
@@ -1182,7 +1186,13 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         mine = full[comm.rank * bw:(comm.rank + 1) * bw]
         ok_rs = bool(np.array_equal(rs.view(torch.uint8).cpu().numpy().view(np.uint32), mine))
         ok_ag = bool(np.array_equal(ag.view(torch.uint8).cpu().numpy().view(np.uint32), full))
+        # every rank computed the oracle above at its own pace: line the ranks up before each timed
+        # loop, or the first call of a fast rank waits in its handshake for a slow one (round 3's
+        # rehearsal lines timed 1.2-10 ms of reduce-scatter that way; the kernel takes ~120 us)
+        torch.cuda.synchronize()
+        barrier()
         t_rs = tmax(_time_calls(lambda: comm.reduce_scatter(x, rs), 5))
+        barrier()
         t_ag = tmax(_time_calls(lambda: comm.all_gather(rs, ag), 5))
         extras["reduce_scatter_allgather"] = {
             "bytes_in_per_rank_rs": blk * n, "bytes_out_per_rank_ag": blk * n,
@@ -1206,6 +1216,8 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         for a in ("rsag", "rsag_zc"):
             for _ in range(2):
                 comm.all_reduce(xs, os_, algo=a)
+            torch.cuda.synchronize()
+            barrier()
             t = tmax(_time_calls(lambda: comm.all_reduce(xs, os_, algo=a), 5))
             extras[f"fp32_1GiB_{a}"] = {"ms": round(t * 1e3, 3), "algbw_GBs": round(S / t / 1e9, 2),
                                         "busbw_GBs": round(S / t / 1e9 * 2 * (n - 1) / n, 2)}
