@@ -530,14 +530,9 @@ def bench_multi(args):
         hp = host_proxy_baseline(n_hp, timeout=120)
         progress("CPU baselines: oracle n-way sum")
         cpu = {"host_proxy": hp, "sum": cpu_baseline_sum(world, args.bytes, args.cpu_seconds)}
-    ndev = torch.cuda.device_count()  # (counting devices does not start HIP)
+    ndev = torch.cuda.device_count()
     if ndev < world:  # rehearsal on a smaller box: ranks share devices (never the case on the 8-GPU node)
         local = local % ndev
-        if world > 2:
-            # one hardware queue per rank process (set before HIP starts), as the multi-process tests
-            # do: with four per process the ranks' queues outnumber what the device keeps mapped, and a
-            # kernel spinning for a peer whose queue is not mapped waits a scheduler time slice
-            os.environ["GPU_MAX_HW_QUEUES"] = "1"
     torch.cuda.set_device(local)
     # a rank that stalls must turn into an error (caught per extras section) well before the driver's
     # limit, so the JSON line is still printed: bounded bootstrap and gloo timeouts
