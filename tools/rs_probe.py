@@ -60,7 +60,7 @@ def worker(rank, n, uid, q):
 if __name__ == "__main__":
     import mscclpp_amd as m
 
-    n = 2
+    n = int(os.environ.get("N", "2"))
     uid = m.Communicator.unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -75,4 +75,4 @@ if __name__ == "__main__":
         p.join(30)
     print(json.dumps(out, indent=1))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "rs_probe.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", f"rs_probe_n{n}.json"), "w"), indent=1)
