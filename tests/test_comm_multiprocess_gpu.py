@@ -4,10 +4,10 @@ scratch / semaphores / output buffers between processes, and every algorithm, ch
 against the CPU oracle (same LCG inputs as test/torch/correctness_test.py:44-56)."""
 import multiprocessing as mp
 import os
-import queue
 import traceback
 
 import numpy as np
+import mp_util
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -94,19 +94,7 @@ def _run(n, cases=None, rsag=True, timeout=240):
     procs = [ctx.Process(target=_worker, args=(r, n, uid, q, cases, rsag)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=timeout)
-            assert err is None, err
-            got[rank] = res
-    except queue.Empty:
-        pytest.fail(f"{n}-process AllReduce timed out")
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, timeout)
     for rank in range(n):
         for algo, dt, count, errc, bad in got[rank]:
             assert errc == 0, (rank, algo, dt, count, errc)
@@ -178,17 +166,7 @@ def test_proxy_ring_reduced_halves_are_complete_before_put(built, nblocks):
     procs = [ctx.Process(target=_ring_worker, args=(r, n, uid, q, 1 << 27, nblocks)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=200)
-            assert err is None, err
-            got[rank] = res
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 200)
     for rank in range(n):
         assert got[rank] == (True, 0), (rank, got[rank])
 
@@ -246,17 +224,7 @@ def test_broadcast_and_split_two_processes(built):
     procs = [ctx.Process(target=_bcast_split_worker, args=(r, n, uid, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=200)
-            assert err is None, err
-            got[rank] = res
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 200)
     for rank in range(n):
         assert got[rank] == [True, True, True, True, True, True, 0], (rank, got[rank])
 
@@ -313,17 +281,7 @@ def test_collectives_wait_for_the_peers_stream(built):
     procs = [ctx.Process(target=_stream_order_worker, args=(r, n, uid, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=200)
-            assert err is None, err
-            got[rank] = res
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 200)
     for rank in range(n):
         assert got[rank] == [True, True, True, 0], (rank, got[rank])
 
@@ -381,17 +339,7 @@ def test_pipeline_then_scratch_collectives(built):
     procs = [ctx.Process(target=_pipeline_then_worker, args=(r, n, uid, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=200)
-            assert err is None, err
-            got[rank] = res
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 200)
     for rank in range(n):
         assert got[rank] == [True] * 6 + [0], (rank, got[rank])
 
@@ -448,17 +396,7 @@ def test_registration_churn_stays_bounded_and_exact(built):
     procs = [ctx.Process(target=_churn_worker, args=(r, n, uid, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=240)
-            assert err is None, err
-            got[rank] = res
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 240)
     for rank in range(n):
         bad, peak, maps, err = got[rank]
         assert bad == 0 and err == 0, (rank, got[rank])
@@ -526,17 +464,7 @@ def test_symmetric_memory_registration(built, symmetric):
     procs = [ctx.Process(target=_symmetric_worker, args=(r, n, uid, symmetric, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=180)
-            assert err is None, err
-            got[rank] = res
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 180)
     for rank in range(n):
         bad, allocs, offs, sym, err = got[rank]
         assert bad == 0 and err == 0, (rank, got[rank])
@@ -595,17 +523,7 @@ def test_reimport_after_close_at_the_same_address(built, n):
     procs = [ctx.Process(target=_reimport_worker, args=(r, n, uid, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=180)
-            assert err is None, err
-            got[rank] = res
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 180)
     for rank in range(n):
         bad, naddr, err = got[rank]
         assert bad == 0 and err == 0, (rank, got[rank])

@@ -7,11 +7,11 @@ here with LCG inputs and bit-exact checks instead of a tolerance."""
 import json
 import multiprocessing as mp
 import os
-import queue
 import sys
 import traceback
 
 import numpy as np
+import mp_util
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -99,19 +99,7 @@ def _run(n, cases):
     procs = [ctx.Process(target=_worker, args=(r, n, uid, cases, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=300)
-            assert err is None, err
-            got[rank] = res
-    except queue.Empty:
-        pytest.fail("executor processes timed out")
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 300)
     return got
 
 

@@ -11,10 +11,10 @@ In-process cases launch rank 0 of a 2-rank AllReduce alone (one view): its peer'
 and buffers exist but no kernel of the peer ever runs.  The two-process case runs the NCCL ABI with
 rank 1 never calling the collective."""
 import multiprocessing as mp
-import queue
 import time
 import traceback
 
+import mp_util
 import pytest
 import torch
 
@@ -101,19 +101,7 @@ def test_absent_peer_reported_by_ncclCommGetAsyncError(built):
     procs = [ctx.Process(target=_worker, args=(r, uid, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(2):
-            rank, res, err = q.get(timeout=180)
-            assert err is None, err
-            got[rank] = res
-    except queue.Empty:
-        pytest.fail("absent-peer case hung")
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, 2, 180)
     NCCL_SUCCESS, NCCL_REMOTE_ERROR = 0, 6
     assert got[0] == (NCCL_SUCCESS, NCCL_REMOTE_ERROR), got
     assert got[1] == (NCCL_SUCCESS, NCCL_SUCCESS), got

@@ -8,10 +8,10 @@ stale between replays.  Buffers are registered by one eager call before the capt
 costs a host exchange, which has no place inside a capture)."""
 import multiprocessing as mp
 import ctypes
-import queue
 import traceback
 
 import numpy as np
+import mp_util
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -134,19 +134,7 @@ def test_captured_allreduce_replays_with_new_data(built):
     procs = [ctx.Process(target=_worker, args=(r, n, uid, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=240)
-            assert err is None, err
-            got[rank] = res
-    except queue.Empty:
-        pytest.fail("graph-captured AllReduce timed out")
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 240)
     for rank in range(n):
         for algo, bad, errc in got[rank]:
             assert errc == 0, (rank, algo, errc)
@@ -259,19 +247,7 @@ def test_captured_buffers_survive_registration_churn(built):
     procs = [ctx.Process(target=_churn_worker, args=(r, n, uid, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=240)
-            assert err is None, err
-            got[rank] = res
-    except queue.Empty:
-        pytest.fail("registration churn case timed out")
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 240)
     for rank in range(n):
         assert got[rank]["pinned"] >= 1 and got[rank]["regs"] == 64 + got[rank]["pinned"], got
         assert got[rank]["bad"] == 0 and got[rank]["err"] == 0, got

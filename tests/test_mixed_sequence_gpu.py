@@ -7,11 +7,11 @@ call that reads scratch, flags or semaphores still in use by the previous call o
 algorithm -- or a peer's stale input -- shows up as a wrong word (ADVICE r1's pipeline exit race
 was of this kind)."""
 import multiprocessing as mp
-import queue
 import random
 import traceback
 
 import numpy as np
+import mp_util
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -106,19 +106,7 @@ def test_mixed_algorithm_sequence_back_to_back(built, n):
     procs = [ctx.Process(target=_worker, args=(r, n, uid, q)) for r in range(n)]
     for p in procs:
         p.start()
-    got = {}
-    try:
-        for _ in range(n):
-            rank, res, err = q.get(timeout=240)
-            assert err is None, err
-            got[rank] = res
-    except queue.Empty:
-        pytest.fail("mixed sequence timed out")
-    finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
+    got = mp_util.collect(procs, q, n, 240)
     for rank in range(n):
         bad, errc = got[rank]
         assert errc == 0, (rank, errc)
