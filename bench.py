@@ -981,6 +981,13 @@ def xgmi_probe(comm, n, dev, tmax, barrier, S=64 << 20):
         return tmax((time.perf_counter() - t0) / reps)
 
     base_s, base_d = src.data_ptr(), dst.data_ptr()
+    # one link at a time: every rank puts S/4 into the peer at distance d (d = 1 .. n-1) in the same
+    # launch, so each rank drives exactly one outgoing link and receives on one; a node whose links
+    # differ (topology, a degraded link) shows it here
+    per_peer = {}
+    for d in range(1, n):
+        q = (rank + d) % n
+        per_peer[f"+{d}"] = round((S // 4) / timed(jobs([(base_s, pdst[q], S // 4)], 512)) / 1e9, 1)
     t_put = timed(jobs([(base_s, pdst[nxt], S)], 512))
     t_get = timed(jobs([(psrc[prv], base_d, S)], 512))
     chunk = (S // (n - 1)) // 16 * 16
@@ -1009,7 +1016,8 @@ def xgmi_probe(comm, n, dev, tmax, barrier, S=64 << 20):
            "allpairs_put_out_GBs": round((n - 1) * chunk / t_ap / 1e9, 1),
            "allpairs_get_in_GBs": round((n - 1) * chunk / t_ag / 1e9, 1),
            "allpairs_getput_GBs": round(2 * (n - 1) * chunk / t_gp / 1e9, 1),
-           "allpairs_put_out_GBs_by_store_policy": by_store, "allpairs_get_in_GBs_by_load_policy": by_load}
+           "allpairs_put_out_GBs_by_store_policy": by_store, "allpairs_get_in_GBs_by_load_policy": by_load,
+           "single_link_put_GBs_by_distance": per_peer}
     # all-pairs AllReduce moves 2(n-1)/n * S per rank: its algbw ceilings at the measured rates
     out["allpairs_algbw_ceiling_put"] = round(out["allpairs_put_out_GBs"] * n / (2 * (n - 1)), 1)
     out["allpairs_algbw_ceiling_getput"] = round(out["allpairs_getput_GBs"] * n / (2 * (n - 1)), 1)
