@@ -825,11 +825,13 @@ def winner_profile(m, n, S, sku, algo, nb, nt):
             break
         a = SELECT_NAMES[m.lib().mscclppAmdSelectAlgo(n, size, 0)]
         nb_, nt_ = _builtin_shape(m, n, size)
-        e = {"message_size": size, "algorithm": FULL_NAMES[a], "nblocks": nb_, "nthreads": nt_}
+        e = {"message_size": size, "algorithm": FULL_NAMES[a], "nblocks": nb_, "nthreads": nt_,
+             "source": m.tuned_config_source("allreduce", n, size)}
         if not entries or {k: v for k, v in entries[-1].items() if k != "message_size"} != \
                 {k: v for k, v in e.items() if k != "message_size"}:
             entries.append(e)
-    entries.append({"message_size": S, "algorithm": FULL_NAMES[algo], "nblocks": nb, "nthreads": nt})
+    entries.append({"message_size": S, "algorithm": FULL_NAMES[algo], "nblocks": nb, "nthreads": nt,
+                    "source": "tuned (bench.py, this run)"})
     prof = {"scale": n, "collectives": {"allreduce": entries}}
     if sku:
         prof = {"sku": sku, **prof}
@@ -1076,7 +1078,8 @@ def node_tuned_table(n, sku, extras, headline):
     for size, key in pts:
         algo, shape = key.split(":")
         nb, nt = (int(v) for v in shape.split("x"))
-        e = {"message_size": size, "algorithm": FULL_NAMES[algo], "nblocks": nb, "nthreads": nt}
+        e = {"message_size": size, "algorithm": FULL_NAMES[algo], "nblocks": nb, "nthreads": nt,
+             "source": f"node ({sku}, {n} ranks, bench.py)"}
         if entries and {k: v for k, v in entries[-1].items() if k != "message_size"} == \
                 {k: v for k, v in e.items() if k != "message_size"}:
             continue

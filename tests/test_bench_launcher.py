@@ -174,6 +174,9 @@ class _FakeM:
     def tuned_config(self, coll, n, size):
         return None
 
+    def tuned_config_source(self, coll, n, size):
+        return "reference"
+
 
 @pytest.mark.parametrize("n", [2, 8])
 def test_winner_profile_keeps_the_ll_range(n):
@@ -186,7 +189,9 @@ def test_winner_profile_keeps_the_ll_range(n):
     (p,) = prof["profiles"]
     assert p["scale"] == n and prof["version"] == 1
     es = p["collectives"]["allreduce"]
-    assert es[-1] == {"message_size": S, "algorithm": "default_allreduce_rsag_zero_copy", "nblocks": 128, "nthreads": 512}
+    assert {k: v for k, v in es[-1].items() if k != "source"} == \
+        {"message_size": S, "algorithm": "default_allreduce_rsag_zero_copy", "nblocks": 128, "nthreads": 512}
+    assert es[-1]["source"].startswith("tuned") and es[0]["source"] == "reference"
     want = ["default_allreduce_allpair_packet"] + ([] if n == 2 else ["default_allreduce_packet"]) + \
         ["default_allreduce_fullmesh", "default_allreduce_rsag_zero_copy"]
     assert [e["algorithm"] for e in es] == want

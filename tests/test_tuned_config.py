@@ -121,3 +121,4 @@ def test_bench_node_table_loads_and_selects(built, tmp_path):
     assert q["ar/8/1048577"] == ["default_allreduce_packet", 0, 0]
     assert q["ar/8/50331648"] == ["default_allreduce_rsag_zero_copy", 128, 512]
     assert q["ar/4/50331648"][0] == "default_allreduce_fullmesh"  # other scales keep the built-in table
+    assert q["src/8/50331648"].startswith("node (") and q["src/4/50331648"] == "reference"
