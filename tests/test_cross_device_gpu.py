@@ -71,11 +71,16 @@ def _worker(rank, n, uid, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (ranks on distinct devices)")
+# MSCCLPP_AMD_TEST_SHARED_REHEARSAL=1 runs the same test with 2 ranks sharing the one device of a
+# one-GPU box (only the distinct-device assertions are skipped): a check of the test itself.
+REHEARSE = os.environ.get("MSCCLPP_AMD_TEST_SHARED_REHEARSAL") == "1"
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2 and not REHEARSE, reason="needs two GPUs (ranks on distinct devices)")
 def test_ranks_on_distinct_devices_bit_exact(built):
     import mscclpp_amd as m
 
-    n = min(torch.cuda.device_count(), 8)
+    n = min(torch.cuda.device_count(), 8) if torch.cuda.device_count() >= 2 else 2
     uid = m.Communicator.unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -85,9 +90,11 @@ def test_ranks_on_distinct_devices_bit_exact(built):
     import mp_util
 
     got = mp_util.collect(procs, q, n, 300)
-    assert len({got[r]["dev"] for r in got}) == n, got
-    assert len({got[r]["bus"] for r in got}) == n, got
+    shared = torch.cuda.device_count() < n
+    if not shared:
+        assert len({got[r]["dev"] for r in got}) == n, got
+        assert len({got[r]["bus"] for r in got}) == n, got
     for rank, res in got.items():
-        assert not res["shared"] and res["err"] == 0, (rank, res)
+        assert res["shared"] == shared and res["err"] == 0, (rank, res)
         for algo, dt, count, nbad, same_dev in res["bad"]:
             assert nbad == 0 and same_dev, (rank, algo, dt, count, nbad, same_dev)
