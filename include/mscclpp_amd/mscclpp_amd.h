@@ -76,7 +76,8 @@ typedef struct {
   uint64_t* tokens;                                /* own inbound tokens [MAX_RANKS][MAX_CHANNELS] */
   uint64_t* peerTokens[MSCCLPP_AMD_MAX_RANKS];     /* rank q's tokens as mapped here */
   uint64_t* expected;                              /* own expected counters [MAX_RANKS][MAX_CHANNELS] */
-  uint32_t* flags;                                 /* MSCCLPP_AMD_FLAG_SLOTS words, initialised to 1 */
+  uint32_t* flags;                                 /* MSCCLPP_AMD_FLAG_SLOTS words, initialised to 1,
+                                                      16-byte aligned */
   uint32_t* err;                                   /* device error word (0 = ok) */
   uint64_t scratchBytes;
   int32_t rank;
@@ -117,7 +118,8 @@ int mscclppAmdFlagsInit(uint32_t* flags, void* stream);
 /* out = x (op) unpack(pack(y, flag)); pkts: 2*bytes of (uncached) device memory; bytes % 16 == 0.
  * 256-lane workgroups with 4 KiB per round; nblocks <= 0 selects the default grid (one workgroup per
  * 4 KiB up to 1024 of them), nblocks > 0 that grid (<= 1024).  budgetTicks: spin budget in 10 ns
- * ticks. */
+ * ticks.  flags: MSCCLPP_AMD_FLAG_SLOTS words, 16-byte aligned.  The packet hand-off runs between the
+ * waves of each workgroup. */
 int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts, void* out, size_t bytes, int dtype, int op,
                              uint32_t* flags, int nblocks, uint64_t budgetTicks, uint32_t* err, void* stream);
 /* The default shape for `bytes`: waves per workgroup, KiB per wave and round, workgroups, skewed. */

@@ -113,6 +113,7 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
       if (v.rank < 0 || v.rank >= nranks || (seen >> v.rank) & 1u) return (int)ncclInvalidArgument;
       seen |= 1u << v.rank;
       if (!v.input || !v.output || !v.flags || !v.err) return (int)ncclInvalidArgument;
+      if (ll && ((uintptr_t)v.flags % 16)) return (int)ncclInvalidArgument;  // 16-byte flag refresh
       if (!zc && (!v.scratch || v.scratchBytes == 0)) return (int)ncclInvalidArgument;
       for (int q = 0; q < nranks; ++q) {
         if (!zc && !v.peerScratch[q]) return (int)ncclInvalidArgument;

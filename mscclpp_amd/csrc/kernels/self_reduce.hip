@@ -559,6 +559,7 @@ extern "C" int mscclppAmdSelfReduceLL16(const void* x, const void* y, void* pkts
                                         void* streamPtr) {
   hipStream_t stream = (hipStream_t)streamPtr;
   if (!x || !y || !pkts || !out || !flags || bytes == 0 || (bytes % 16) != 0) return 4;
+  if ((uintptr_t)flags % 16) return 4;  // the flag slots above the grid are refreshed 16 bytes at a time
   // nblocks <= 0: the default shape (selfReduceShape); otherwise the large form on that grid, at most
   // 1024 workgroups = 4 per CU (16 KiB LDS each), all resident, so every partner pair is co-resident
   if (nblocks > 1024) return 4;
