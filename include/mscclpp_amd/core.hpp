@@ -109,6 +109,8 @@ class RegisteredMemory {
   // wait(); cached device memory (hipMalloc) is guaranteed only to the host and to kernels launched
   // after the receiving one.
   bool coherent() const;
+  // Received from another process (data() is this process's mapping of the owner's buffer).
+  bool remote() const;
   std::vector<char> serialize() const;
   static RegisteredMemory deserialize(const std::vector<char>& data);
   struct Impl;

@@ -189,9 +189,18 @@ SemaphoreId ProxyService::addSemaphore(std::shared_ptr<Host2DeviceSemaphore> sem
   return (SemaphoreId)(semaphores_.size() - 1);
 }
 
+static int portChannelDstPolicy();
+
 MemoryId ProxyService::addMemory(RegisteredMemory memory) {
   if (memories_.size() >= (1u << TriggerBitsMemoryId))
     throw Error("ProxyService: too many memories for the trigger's 9-bit id", ErrorCode::InvalidUsage);
+  // strict: a peer's cached buffer is refused as soon as it is added -- before any semaphore is built
+  // with that peer, so every rank refuses before it could wait in the bootstrap for another
+  if (memory.remote() && !memory.coherent() && portChannelDstPolicy() == 2)
+    throw Error("ProxyService::addMemory: rank " + std::to_string(memory.rank()) +
+                    "'s buffer is cached device memory, refused as a PortChannel destination "
+                    "(MSCCLPP_AMD_PORT_CHANNEL_DST=strict; allocate it with GpuBuffer / mscclppAmdMallocUncached)",
+                ErrorCode::InvalidUsage);
   memories_.push_back(std::move(memory));
   return (MemoryId)(memories_.size() - 1);
 }

@@ -226,6 +226,7 @@ size_t RegisteredMemory::size() const { return pimpl_ ? (size_t)pimpl_->size : 0
 TransportFlags RegisteredMemory::transports() const { return pimpl_ ? pimpl_->transports : TransportFlags(); }
 int RegisteredMemory::rank() const { return pimpl_ ? pimpl_->rank : -1; }
 bool RegisteredMemory::coherent() const { return pimpl_ && pimpl_->coherent; }
+bool RegisteredMemory::remote() const { return pimpl_ && pimpl_->pid != (int32_t)getpid(); }
 
 std::vector<char> RegisteredMemory::serialize() const {
   if (!pimpl_) throw Error("serialize: empty RegisteredMemory", ErrorCode::InvalidUsage);

@@ -13,7 +13,8 @@
 // -- and ProxyService warns once that the destination is cached device memory; `uncached` allocates
 // the receive buffer from the uncached pool (no warning); `refuse` runs with
 // MSCCLPP_AMD_PORT_CHANNEL_DST=strict and expects the first ncclAllGather to return
-// ncclInvalidUsage (2 ranks: every rank refuses at its first and only peer).
+// ncclInvalidUsage on every rank (ProxyService::addMemory refuses the peer's buffer before any
+// semaphore is built, so no rank is left waiting for another).
 #include <hip/hip_runtime.h>
 #include <sys/wait.h>
 #include <unistd.h>

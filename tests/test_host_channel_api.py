@@ -57,8 +57,9 @@ def test_customized_allgather_port_channels(built, n, mode):
 
 
 @pytest.mark.gpu
-def test_port_channel_strict_refuses_cached_destination(built):
+@pytest.mark.parametrize("n", [2, 4])
+def test_port_channel_strict_refuses_cached_destination(built, n):
     """MSCCLPP_AMD_PORT_CHANNEL_DST=strict: a PortChannel into cached device memory is refused with
-    ncclInvalidUsage and the reason in ncclGetLastError."""
-    out = _run("test_customized_allgather", ["gpu", "2", str(1 << 12), "refuse"], 120)
-    assert "gpu OK" in out and "rank 0 refused OK" in out and "rank 1 refused OK" in out, out
+    ncclInvalidUsage and the reason in ncclGetLastError, on every rank and with no rank left waiting."""
+    out = _run("test_customized_allgather", ["gpu", str(n), str(1 << 12), "refuse"], 120)
+    assert "gpu OK" in out and all(f"rank {r} refused OK" in out for r in range(n)), out
