@@ -124,3 +124,26 @@ def test_exports_every_reference_nccl_entry_point(built):
     w = vp()
     assert L.ncclCommWindowRegister(None, None, 0, ctypes.byref(w), 0) == 4
     assert L.ncclCommWindowDeregister(None, None) == 4
+
+
+def test_flag_alignment_and_mix_sizes_rejected_without_gpu(built):
+    """Round 4: flag buffers are refreshed 16 bytes at a time, so a misaligned flag pointer is an
+    invalid argument (checked before any launch), and the generic mix ceiling takes whole 4 KiB passes."""
+    import mscclpp_amd as m
+
+    L = m.lib()
+    vp = ctypes.c_void_p
+    fake = vp(1 << 20)
+    assert L.mscclppAmdSelfReduceLL16(fake, fake, fake, fake, 4096, m.F16, m.SUM, vp((1 << 20) + 4), 0, 1000, fake,
+                                      None) == 4
+    arr = (m.RankView * 2)()
+    for r in range(2):
+        v = arr[r]
+        v.input = v.output = v.scratch = v.tokens = v.expected = v.err = 1 << 20
+        v.flags = (1 << 20) + 8  # not 16-byte aligned
+        v.scratchBytes = 1 << 20
+        v.rank = r
+        for q in range(2):
+            v.peerScratch[q] = v.peerOutput[q] = v.peerInput[q] = v.peerTokens[q] = 1 << 20
+    assert L.mscclppAmdAllReduceLaunch(m.ALGO_ALLPAIR, arr, 2, 2, 1024, m.F16, m.SUM, 0, 0, 1000, None) == 4
+    assert L.mscclppAmdMixStream(fake, fake, fake, fake, fake, 4096 + 16, 0, None) == 4
