@@ -415,15 +415,16 @@ extern "C" int mscclppAmdSelfReduceLL16Shape(const void* x, const void* y, void*
   const bool plain = (count & 2) != 0;
   const int pmask = (count & 4) ? 0 : (count & 8) ? 8 : 1;  // bit 2: partner wave w ^ 1 of the workgroup; bit 3: b ^ 8
   count &= 1;
-  if (pmask != 1) {  // 4 x 1 KiB waves, nt payload, skew 0 / 1 / 2 (multi-round forms)
-    if (waves != 4 || units != 1 || count || plain || (pmask == 8 && nblocks % 16)) return 4;
-#define SRPM(SK, PM)                                                                                              \
-    if (skew == SK && pmask == PM) {                                                                              \
-      launchSelfReduceShape<kF16, kSum, 4, 1, SK, false, kNonTemporal, PM>(x, y, pkts, out, bytes, flags, nblocks, \
+  if (pmask != 1) {  // 4 x 1 KiB, 4 x 2 KiB or 8 x 1 KiB waves, nt payload, skew 0 / 1 / 2 (multi-round forms)
+    if (count || plain || (pmask == 8 && nblocks % 16)) return 4;
+#define SRPM(W, U, SK, PM)                                                                                        \
+    if (waves == W && units == U && skew == SK && pmask == PM) {                                                  \
+      launchSelfReduceShape<kF16, kSum, W, U, SK, false, kNonTemporal, PM>(x, y, pkts, out, bytes, flags, nblocks, \
                                                                           budgetTicks, err, pollMiss, s);          \
       return hipGetLastError() == hipSuccess ? 0 : 1;                                                             \
     }
-    SRPM(0, 0) SRPM(1, 0) SRPM(2, 0) SRPM(0, 8) SRPM(1, 8) SRPM(2, 8)
+    SRPM(4, 1, 0, 0) SRPM(4, 1, 1, 0) SRPM(4, 1, 2, 0) SRPM(4, 1, 0, 8) SRPM(4, 1, 1, 8) SRPM(4, 1, 2, 8)
+    SRPM(4, 2, 1, 0) SRPM(4, 2, 2, 0) SRPM(8, 1, 1, 0) SRPM(8, 1, 2, 0)
 #undef SRPM
     return 4;
   }

@@ -36,10 +36,10 @@ pk = m.DeviceBuffer(2 * SMAX)
 ref = (x.float() + y.float()).clamp(-65504, 65504).half()
 
 
-def shape_fn(S, sk, bits, nb=1024):
+def shape_fn(S, sk, bits, nb=1024, w=4, u=1):
     def f():
         rc = D.mscclppAmdSelfReduceLL16Shape(vp(x.data_ptr()), vp(y.data_ptr()), vp(pk.ptr), vp(out.data_ptr()), S,
-                                             vp(flags.data_ptr()), nb, 4, 1, sk, bits, 500_000_000,
+                                             vp(flags.data_ptr()), nb, w, u, sk, bits, 500_000_000,
                                              vp(err.data_ptr()), vp(miss.data_ptr()), m.stream_ptr())
         assert rc == 0, (S, sk, bits, rc)
     return f
@@ -73,6 +73,11 @@ for S in [int(v) for v in os.environ.get("SIZES", "8388608,16777216,33554432,503
     for sk in (0, 1, 2):
         for pname, bits in (("p1", 0), ("p0", 4), ("p8", 8)):
             variants[f"skew{sk}_{pname}"] = shape_fn(S, sk, bits)
+    if os.environ.get("WIDE"):  # 2 KiB per wave, or 8 waves, with the in-workgroup partner
+        for sk in (1, 2):
+            for nb in (512, 1024):
+                variants[f"w4u2_x{nb}_skew{sk}_p0"] = shape_fn(S, sk, 4, nb, 4, 2)
+                variants[f"w8u1_x{nb}_skew{sk}_p0"] = shape_fn(S, sk, 4, nb, 8, 1)
     ok = {}
     for k, f in variants.items():
         out.zero_()
