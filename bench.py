@@ -455,6 +455,89 @@ def lcg_tensor(count, rank, seq, dtype, dev):
     return ((s % 4096).to(torch.float32) / 4096.0).to(dtype)
 
 
+RING_CHUNK = 1 << 25  # elements per generator call of the fp32 ring check (bounds its int64 temporaries)
+
+
+def ring_bits(i, rank, seq):
+    """Order-sensitive fp32 inputs of configs[4] (the 1 GiB ring-order RS+AG): a 32-bit hash of
+    (element i, rank, seq) laid out as IEEE bits -- random sign, exponent 2^0 .. 2^-7, full 23-bit
+    mantissa -- so that a sum of n ranks' values rounds differently in different orders (the LCG of
+    lcg_tensor makes multiples of 1/4096, whose fp32 sums are exact in ANY order and would let a
+    wrong order pass).  `i` is an int64 numpy array or torch tensor; every product stays below 2^63.
+    Returns the bits as signed int64 (view them as int32 -> float32)."""
+    M = 0xFFFFFFFF
+    s = (i + rank * 0x9E3779B1 + seq * 0x7F4A7C15) & M
+    s = (s * 1664525 + 1013904223) & M
+    s = s ^ (s >> 15)
+    s = (s * 0x2C1B3C6D) & M
+    s = s ^ (s >> 13)
+    sign = (s >> 31) & 1
+    bits = (sign << 31) | ((127 - ((s >> 23) & 7)) << 23) | (s & 0x7FFFFF)
+    return bits - (sign << 32)
+
+
+def ring_tensor(start, count, rank, seq, dev):
+    """ring_bits of elements [start, start + count) as a float32 tensor on `dev`."""
+    out = torch.empty(count, dtype=torch.float32, device=dev)
+    for a in range(0, count, RING_CHUNK):
+        b = min(count, a + RING_CHUNK)
+        i = torch.arange(start + a, start + b, dtype=torch.int64, device=dev)
+        out[a:b] = ring_bits(i, rank, seq).to(torch.int32).view(torch.float32)
+    return out
+
+
+def ring_slice_elems(n, count):
+    """Elements per owner slice of the bulk kernels' geometry (BulkGeom: ceil(S / n) rounded up to 16 B)."""
+    return ((count * 4 + n - 1) // n + 15) // 16 * 4
+
+
+def ring_order_mismatches(out, n, seq, order="ring"):
+    """Elements of a 4-byte-per-element AllReduce output `out` (fp32, ring_tensor inputs of every rank
+    for `seq`) that differ bit-wise from the order-stable sum of allreduce_rsag.cu:85-94 / allreduce_rsag_
+    zero_copy.cu:88-98: in owner o's slice, x_o + x_{o+1} + ... + x_{o-1}, computed here elementwise by
+    torch on out's device in the same order (IEEE fp32 adds, so 0 ulp is the bar).  order="ascending"
+    sums x_0 + x_1 + ... instead (tests: a wrong order must be caught)."""
+    count = out.numel()
+    se = ring_slice_elems(n, count)
+    bad = 0
+    ov = out.view(torch.int32)
+    for o in range(n):
+        lo, hi = o * se, min(count, (o + 1) * se)
+        for a in range(lo, hi, RING_CHUNK):
+            b = min(hi, a + RING_CHUNK)
+            ranks = [(o + k) % n for k in range(n)] if order == "ring" else list(range(n))
+            acc = ring_tensor(a, b - a, ranks[0], seq, out.device)
+            for r in ranks[1:]:
+                acc += ring_tensor(a, b - a, r, seq, out.device)
+            bad += int((acc.view(torch.int32) != ov[a:b]).sum().item())
+    return bad
+
+
+def ring_oracle_sample(out, n, seq, samples=1 << 16, rng_seed=5):
+    """`samples` random elements plus both ends of every owner slice of `out` against the CPU oracle's
+    fp32 sum (oracle_reduce_seq, oracle/ll_oracle.c) in ring order from the owner; True if all match."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    count = out.numel()
+    se = ring_slice_elems(n, count)
+    rng = np.random.default_rng(rng_seed)
+    idx = np.concatenate([rng.integers(0, count, samples),
+                          np.array([v for k in range(n) for v in (k * se, min(count, (k + 1) * se) - 1) if v < count])])
+    idx = np.unique(idx).astype(np.int64)
+    got = out.view(torch.int32)[torch.from_numpy(idx).to(out.device)].cpu().numpy().view(np.uint32)
+    vals = [ring_bits(idx, r, seq).astype(np.int32).view(np.uint32) for r in range(n)]
+    owner = idx // se
+    for o in range(n):
+        sel = owner == o
+        if not sel.any():
+            continue
+        exp = O.reduce_seq(O.F32, O.SUM, [vals[(o + k) % n][sel] for k in range(n)])
+        if not np.array_equal(exp, got[sel]):
+            return False
+    return True
+
+
 class BitExactChecker:
     """Expected AllReduce results from the CPU oracle (tests/oracle_lib.py -> oracle/liboracle.so) in the sum order
     of the algorithm that produced them; computed lazily, cached per (order, ownership, seq).  Runs outside every
@@ -504,6 +587,11 @@ class BitExactChecker:
         if key not in self.cache:
             self.cache[key] = O.allreduce_owned(self.dt, O.SUM, ins, nw, n * chunk, chunk, order)[: S // 4]
         return self.cache[key]
+
+    def forget(self):
+        """Drop the cached inputs and expectations (host memory: 8 ranks x 256 MiB per size otherwise)."""
+        self.inputs.clear()
+        self.cache.clear()
 
     @staticmethod
     def words(t):
@@ -572,28 +660,66 @@ def bench_multi(args):
         flat = o.detach().contiguous().view(torch.uint8)[: want.numel() * 4].view(torch.int32)
         return bool(torch.equal(flat, want))
 
-    def check_run(algo, nb, nt, nbytes=None):
-        """Untimed: run once on seq 0, poison the output, run on seq 1, compare every word with the oracle."""
-        if nbytes is None:
+    def expected_of(algo, nb, nt, nbytes):
+        """The oracle's seq-1 result for this rank; algo None = what ncclAllReduce with no algorithm
+        runs at this size (the library's selector and its tuned launch shape)."""
+        if algo is None:
+            algo = SELECT_NAMES[m.lib().mscclppAmdSelectAlgo(n, nbytes or S, 0)]
+            nb, nt = _builtin_shape(m, n, nbytes or S)
+        return checker.expected(algo, nb, nt, 1, nbytes, rank)
+
+    def verify(o, exp, what):
+        """Every word of `o` equals `exp` -- read by the copy engine and by a kernel on this rank --
+        and no device error; the verdict of all ranks (MIN), so every rank returns the same."""
+        got = BitExactChecker.words(o)
+        same = bool(np.array_equal(got, exp)) and device_matches(o, exp)
+        if not same:  # say where on stderr (the JSON line carries the verdict per case)
+            bad = np.nonzero(got != exp)[0]
+            sw = ((got.size * 4 + n - 1) // n + 15) // 16 * 4
+            first = int(bad[0]) if bad.size else -1
+            print(f"bench: rank {rank} {what}: {bad.size} of {got.size} words differ, first {first} "
+                  f"(slice {first // sw}), slices {sorted(set((bad // sw).tolist()))[:8]}, "
+                  f"{int((got[bad] == 0xFFFFFFFF).sum())} poisoned", file=sys.stderr)
+        return all_ok(same and comm.device_error() == 0)
+
+    def check_run(algo, nb, nt, nbytes=None, bufs=None):
+        """Untimed: run once on seq 0, poison the output, run on seq 1, compare every word with the
+        oracle.  algo None calls ncclAllReduce with no algorithm (the drop-in caller's path); bufs =
+        (seq-0 input, seq-1 input, output) of nbytes when the caller times the same buffers."""
+        if bufs is not None:
+            a0, a1, o = bufs
+        elif nbytes is None:
             a0, a1, o = xs[0], xs[1], out
         else:
             c = nbytes // 2
             a0, a1 = (lcg_tensor(c, rank, sq, torch.float16, dev) for sq in (0, 1))
             o = torch.empty_like(a0)
-        comm.all_reduce(a0, o, algo=algo, nblocks=nb, nthreads=nt)
+
+        def call(a):
+            if algo is None:
+                comm.all_reduce(a, o)
+            else:
+                comm.all_reduce(a, o, algo=algo, nblocks=nb, nthreads=nt)
+
+        call(a0)
         poison(o)
-        comm.all_reduce(a1, o, algo=algo, nblocks=nb, nthreads=nt)
+        call(a1)
         torch.cuda.synchronize()
-        exp = checker.expected(algo, nb, nt, 1, nbytes, rank)
-        got = BitExactChecker.words(o)
-        same = bool(np.array_equal(got, exp)) and device_matches(o, exp)
-        if not same:  # say where on stderr (the JSON line carries the verdict per candidate)
-            bad = np.nonzero(got != exp)[0]
-            sw = ((got.size * 4 + n - 1) // n + 15) // 16 * 4
-            print(f"bench: rank {rank} {algo} {nb}x{nt}: {bad.size} of {got.size} words differ, first {int(bad[0])} "
-                  f"(slice {int(bad[0]) // sw}), slices {sorted(set((bad // sw).tolist()))[:8]}, "
-                  f"{int((got[bad] == 0xFFFFFFFF).sum())} poisoned", file=sys.stderr)
-        return all_ok(same and comm.device_error() == 0)
+        return verify(o, expected_of(algo, nb, nt, nbytes), f"{algo or 'selector'} {nb}x{nt} {nbytes or S} B")
+
+    def check_replay(graph, inp, seq1, o, nbytes):
+        """A captured graph reads its input at replay time: load the seq-1 input, poison the output,
+        replay once, and compare with the oracle (ncclAllReduce with no algorithm was captured)."""
+        inp.copy_(seq1)
+        poison(o)
+        torch.cuda.synchronize()
+        dist.barrier()
+        graph.replay()
+        torch.cuda.synchronize()
+        return verify(o, expected_of(None, 0, 0, nbytes), f"graph replay {nbytes} B")
+
+    vf = None if checker is None else {"check_run": check_run, "check_replay": check_replay, "poison": poison,
+                                       "all_ok": all_ok, "forget": checker.forget}
 
     # ---- the built-in selector's choice, as a drop-in caller of ncclAllReduce gets it before any
     # tuning (algo None -> ncclAllReduce -> mscclppAmdSelectAlgo + its launch shape), timed like the
@@ -771,7 +897,11 @@ def bench_multi(args):
         res["cpu_baseline"] = dict(cpu["sum"])
         res["host_proxy_baseline"] = hp
     if not args.no_extras:
-        res["extras"] = bench_extras(args, comm, n, dev, tmax, dist.barrier)
+        res["extras"] = bench_extras(args, comm, n, dev, tmax, dist.barrier, vf)
+        # every size and kernel the extras time is checked first (mscclpp-test common.cc:346-360
+        # checks each size it times): all of those verdicts, and any section that failed, are part
+        # of `correct`
+        res["correct"] = bool(res["correct"] and extras_correct(res["extras"], vf is not None))
         # every measured winner as a ready-to-commit tuned-config profile for this node and scale --
         # only from a node where every rank has its own GPU; a rehearsal's table is tagged as such
         table = node_tuned_table(n, torch.cuda.get_device_name(dev), res["extras"], (S, algo, nb, nt))
@@ -1090,33 +1220,109 @@ def node_tuned_table(n, sku, extras, headline):
     return {"version": 1, "profiles": [{"sku": sku, "scale": n, "collectives": {"allreduce": entries}}]}
 
 
-def bench_extras(args, comm, n, dev, tmax, barrier):
-    """BASELINE configs[3] (LL latency sweep, fp16 1 KiB..1 MiB) and configs[4] (fp32 1 GiB
-    RS+AG in ring order), timed the same way; failures are recorded, not raised."""
+EXTRAS_CHECK_KEYS = (["ll_sweep:%dKiB" % kb for kb in LL_SWEEP_KIB] + ["ll_graph:%dKiB" % kb for kb in LL_SWEEP_KIB]
+                     + ["ll16_48MiB", "fp32_1GiB_rsag", "fp32_1GiB_rsag_zc"])
+
+
+def extras_correct(extras, checked):
+    """True when no extras section failed and (checked) every case of EXTRAS_CHECK_KEYS is present
+    in extras["correct_bitexact"] and True; a section's error, or a missing case, is False."""
+    if any(k.endswith("_error") and k != "device_error" for k in extras) or extras.get("device_error", 0):
+        return False
+    if not checked:
+        return True
+    cb = extras.get("correct_bitexact", {})
+    return all(cb.get(k) is True for k in EXTRAS_CHECK_KEYS) and all(v is True for v in cb.values())
+
+
+def ll16_ceiling(n):
+    """The LL16 AllReduce's algbw ceiling over xGMI: the all-pairs ceiling n * 153.6 / 2 GB/s halved,
+    since every 16-byte LL16 packet carries 8 bytes of data and two 4-byte flags (SURVEY §7 "LL
+    framing"; docs/tutorials/03-memory-channel.md:26-34)."""
+    return n * XGMI_LINK_GBS / 4
+
+
+def bench_extras(args, comm, n, dev, tmax, barrier, vf=None):
+    """BASELINE configs[3] (LL latency sweep, fp16 1 KiB..1 MiB, eager and graph-captured), LL16 at
+    the headline bucket, and configs[4] (fp32 1 GiB RS+AG in ring order), each size checked
+    bit-exactly before it is timed (vf: bench_multi's checkers; None under --no-check); failures are
+    recorded, not raised.  Verdicts go to extras["correct_bitexact"]."""
     import mscclpp_amd as m
 
     extras = {}
+    checks = extras["correct_bitexact"] = {}
+    rank = comm.rank
+
+    def lcg_pair(cnt):
+        return [lcg_tensor(cnt, rank, sq, torch.float16, dev) for sq in (0, 1)]
+
     progress("extras: LL latency sweep")
     try:
         lat = {}
         for kb in LL_SWEEP_KIB:
-            cnt = kb * 512
-            xs = torch.rand(cnt, device=dev).half()
-            os_ = torch.empty_like(xs)
+            a0, a1 = lcg_pair(kb * 512)
+            os_ = torch.empty_like(a0)
+            if vf:  # ncclAllReduce with no algorithm, exactly as timed below
+                checks[f"ll_sweep:{kb}KiB"] = vf["check_run"](None, 0, 0, kb << 10, bufs=(a0, a1, os_))
             for _ in range(5):
-                comm.all_reduce(xs, os_)
+                comm.all_reduce(a1, os_)
             torch.cuda.synchronize()
             barrier()
-            lat[f"{kb}KiB"] = round(tmax(_time_calls(lambda: comm.all_reduce(xs, os_), 50)) * 1e6, 2)
+            lat[f"{kb}KiB"] = round(tmax(_time_calls(lambda: comm.all_reduce(a1, os_), 50)) * 1e6, 2)
         extras["ll_latency_us"] = lat
+        extras["ll_latency_algo"] = {f"{kb}KiB": SELECT_NAMES[m.lib().mscclppAmdSelectAlgo(n, kb << 10, 0)]
+                                     for kb in LL_SWEEP_KIB}
     except Exception as e:
         extras["ll_latency_error"] = str(e)
+    progress("extras: LL16 at the headline bucket")
+    try:
+        # LL16 two-hop at the 48 MiB bucket, graded against its own halved ceiling;
+        # default shape and two wider grids, each checked bit-exactly (owner's sum of
+        # allreduce_packet.cu:93-106) before it is timed
+        nbytes = args.bytes
+        a0, a1 = lcg_pair(nbytes // 2)
+        o = torch.empty_like(a0)
+        peers = n - 1
+        shapes = [(0, 0), (peers * 16, 512), (peers * 32, 512)]
+        if ndev_shared(n):  # rehearsal: every rank's grid resident on the shared device
+            shapes = [s for s in shapes if s[0] * n <= 512]
+        row, ok = {}, True
+        for nb_, nt_ in shapes:
+            key = f"packet:{nb_}x{nt_}"
+            try:
+                if vf:
+                    good = vf["check_run"]("packet", nb_, nt_, nbytes, bufs=(a0, a1, o))
+                    ok = ok and good
+                    row[key + ":bitexact"] = good
+                for _ in range(2):
+                    comm.all_reduce(a1, o, algo="packet", nblocks=nb_, nthreads=nt_)
+                torch.cuda.synchronize()
+                barrier()
+                row[key] = round(tmax(_time_calls(
+                    lambda: comm.all_reduce(a1, o, algo="packet", nblocks=nb_, nthreads=nt_), 5)) * 1e6, 1)
+            except Exception as e:  # noqa: BLE001 -- a shape the library refuses is recorded
+                row[key] = str(e)[:80]
+                ok = False
+        times = [(v, k) for k, v in row.items() if isinstance(v, float)]
+        if times:
+            best_us, best = min(times)
+            ach = nbytes / (best_us * 1e-6) / 1e9
+            extras["ll16_48MiB"] = {"bytes": nbytes, "us": row, "best": best, "algbw_GBs": round(ach, 2),
+                                    "peak": round(ll16_ceiling(n), 1), "frac": round(ach / ll16_ceiling(n), 4),
+                                    "peak_source": "n * 153.6 / 4 GB/s: the all-pairs ceiling halved by LL16 framing "
+                                                   "(8 data bytes per 16-byte packet)"}
+        if vf:
+            checks["ll16_48MiB"] = bool(ok and times)
+            vf["forget"]()
+        del a0, a1, o
+    except Exception as e:
+        extras["ll16_48MiB_error"] = str(e)[-300:]
     progress("extras: bulk size sweep")
     try:
         # per message size, the best of the bulk algorithms at two shapes each (fp16): the data for
         # the tuned-config table (host/tuning.cpp) above the LL range
         sweep = {}
-        big = torch.rand((256 << 20) // 2, device=dev).half()
+        big0, big = lcg_pair((256 << 20) // 2)
         bout = torch.empty_like(big)
         for mb in (2, 4, 8, 16, 32, 64, 128, 256):
             xs, os_ = big[: (mb << 20) // 2], bout[: (mb << 20) // 2]
@@ -1138,8 +1344,14 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
                     row[f"{a}:{nb_}x{nt_}"] = str(e)[:80]
             best = min((v, k) for k, v in row.items() if isinstance(v, float))
             sweep[f"{mb}MiB"] = {"us": row, "best": best[1], "algbw_GBs": round((mb << 20) / best[0] / 1e3, 1)}
+            if vf:  # the winner (it goes into the node's tuned table) checked bit-exactly at this size
+                a, shp = best[1].split(":")
+                nb_, nt_ = (int(v) for v in shp.split("x"))
+                checks[f"bulk_sweep:{mb}MiB:{best[1]}"] = vf["check_run"](
+                    a, nb_, nt_, mb << 20, bufs=(big0[: (mb << 20) // 2], xs, os_))
+                vf["forget"]()
         extras["bulk_size_sweep"] = sweep
-        del big, bout
+        del big0, big, bout
     except Exception as e:
         extras["bulk_size_sweep_error"] = str(e)[-300:]
     progress("extras: selector crossover")
@@ -1151,13 +1363,15 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         if ndev_shared(n):
             bulk_c = tuple((a, max(8, 256 // n), 512) for a, _, _ in bulk_c)
         for kb in CROSSOVER_KIB:
-            cnt = kb * 512
-            xs = torch.rand(cnt, device=dev).half()
+            x0, xs = lcg_pair(kb * 512)
             os_ = torch.empty_like(xs)
             cands = (("allpair", 0, 0), ("packet", 0, 0)) if kb <= 64 else (("packet", 0, 0),) + bulk_c
             row = {}
             for a, nb_, nt_ in cands:
                 try:
+                    if vf:
+                        checks[f"crossover:{kb}KiB:{a}:{nb_}x{nt_}"] = vf["check_run"](a, nb_, nt_, kb << 10,
+                                                                                      bufs=(x0, xs, os_))
                     for _ in range(3):
                         comm.all_reduce(xs, os_, algo=a, nblocks=nb_, nthreads=nt_)
                     torch.cuda.synchronize()
@@ -1171,7 +1385,7 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
             sel = SELECT_NAMES[m.lib().mscclppAmdSelectAlgo(n, kb << 10, 0)]
             keep = [k for k, v in row.items() if k.startswith(sel + ":") and isinstance(v, float) and v <= 1.03 * best[0]]
             cross[f"{kb}KiB"] = {"us": row, "best": keep[0] if keep else best[1]}
-            del xs, os_
+            del x0, xs, os_
         extras["selector_crossover"] = cross
     except Exception as e:
         extras["selector_crossover_error"] = str(e)[-300:]
@@ -1214,6 +1428,7 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
             # every rank's check (a max over ranks of "differs")
             "correct_bitexact": {"reduce_scatter": tmax(0.0 if ok_rs else 1.0) == 0.0,
                                  "all_gather": tmax(0.0 if ok_ag else 1.0) == 0.0}}
+        checks.update(extras["reduce_scatter_allgather"]["correct_bitexact"])
         del x, rs, ag
     except Exception as e:
         extras["reduce_scatter_allgather_error"] = str(e)[-300:]
@@ -1221,20 +1436,40 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
     try:
         # BASELINE configs[4]: both ring-order kernels (the same order-stable sum, own then r+1, ...):
         # through the 128 MiB bulk scratch in several passes (rsag) and zero-copy (rsag_zc)
+        # Inputs: ring_tensor (random signs, 8 exponents, full mantissas), so that the 0-ulp check
+        # below tells the ring order from any other; every rank checks its whole output against the
+        # ring-order sum computed on its own device, and a sample against the CPU oracle
         S = 1 << 30
-        xs = torch.rand(S // 4, device=dev)
-        os_ = torch.empty_like(xs)
+        count = S // 4
+        x0, x1 = (ring_tensor(0, count, rank, sq, dev) for sq in (0, 1))
+        os_ = torch.empty_like(x0)
+        peak = n * XGMI_LINK_GBS / 2
         for a in ("rsag", "rsag_zc"):
+            row = {}
+            if vf:
+                comm.all_reduce(x0, os_, algo=a)
+                vf["poison"](os_)
+                comm.all_reduce(x1, os_, algo=a)
+                torch.cuda.synchronize()
+                bad = ring_order_mismatches(os_, n, 1)
+                sample = ring_oracle_sample(os_, n, 1)
+                row["mismatched_elements_max_over_ranks"] = int(tmax(float(bad)))
+                row["oracle_sample_ok"] = vf["all_ok"](sample)
+                checks[f"fp32_1GiB_{a}"] = vf["all_ok"](bad == 0 and sample and comm.device_error() == 0)
             for _ in range(2):
-                comm.all_reduce(xs, os_, algo=a)
+                comm.all_reduce(x1, os_, algo=a)
             torch.cuda.synchronize()
             barrier()
-            t = tmax(_time_calls(lambda: comm.all_reduce(xs, os_, algo=a), 5))
-            extras[f"fp32_1GiB_{a}"] = {"ms": round(t * 1e3, 3), "algbw_GBs": round(S / t / 1e9, 2),
-                                        "busbw_GBs": round(S / t / 1e9 * 2 * (n - 1) / n, 2)}
-        del xs, os_
+            t = tmax(_time_calls(lambda: comm.all_reduce(x1, os_, algo=a), 5))
+            ach = S / t / 1e9
+            row.update({"ms": round(t * 1e3, 3), "algbw_GBs": round(ach, 2),
+                        "busbw_GBs": round(ach * 2 * (n - 1) / n, 2), "peak": round(peak, 1),
+                        "frac": round(ach / peak, 4),
+                        "peak_source": "n * 153.6 / 2 GB/s, the all-pairs AllReduce algbw ceiling (BASELINE.md §2)"})
+            extras[f"fp32_1GiB_{a}"] = row
+        del x0, x1, os_
     except Exception as e:
-        extras["fp32_1GiB_error"] = str(e)
+        extras["fp32_1GiB_error"] = str(e)[-300:]
     progress("extras: graph-captured LL latency sweep")
     try:
         glat = {}
@@ -1243,13 +1478,16 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         xw = torch.rand(512, device=dev).half()
         graph_time_per_call(lambda: comm.all_reduce(xw, torch.empty_like(xw)), sync=barrier)
         for kb in LL_SWEEP_KIB:
-            cnt = kb * 512
-            xs = torch.rand(cnt, device=dev).half()
-            os_ = torch.empty_like(xs)
-            glat[f"{kb}KiB"] = round(tmax(graph_time_per_call(lambda: comm.all_reduce(xs, os_), sync=barrier)) * 1e6, 2)
+            a0, a1 = lcg_pair(kb * 512)
+            os_ = torch.empty_like(a0)
+            t, g = graph_time_per_call(lambda: comm.all_reduce(a0, os_), sync=barrier, keep=True)
+            glat[f"{kb}KiB"] = round(tmax(t) * 1e6, 2)
+            if vf:  # the captured calls on new data: the replay must produce the seq-1 result
+                checks[f"ll_graph:{kb}KiB"] = vf["check_replay"](g, a0, a1, os_, kb << 10)
+            del g
         extras["ll_latency_graph_us"] = glat
     except Exception as e:
-        extras["ll_latency_error"] = str(e)
+        extras["ll_latency_graph_error"] = str(e)[-300:]
     progress("extras: mscclpp-test kernels")
     try:
         # the mscclpp-test kernels on the sizes the reference publishes (BASELINE.md §1,
@@ -1267,6 +1505,11 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
             us = tmax(graph_time_per_call(lambda: comm.all_reduce(xs, os_, algo=k), calls=20, replays=15,
                                           sync=barrier)) * 1e6
             row = {"us": round(us, 2), "algbw_GBs": round((kb << 10) / us / 1e3, 2)}
+            if k != "k5":  # out of place: every element is 0 + 1 + ... + (n-1) after the replays
+                torch.cuda.synchronize()
+                good = bool(torch.all(os_ == n * (n - 1) // 2).item()) and comm.device_error() == 0
+                row["correct"] = vf["all_ok"](good) if vf else good
+                checks[f"{k}_{kb}KiB"] = row["correct"]
             if pub:
                 row["reference_published"] = pub
             mt[f"{k}_{kb}KiB" if kb < 1024 else f"{k}_{kb >> 10}MiB"] = row
@@ -1279,6 +1522,7 @@ def bench_extras(args, comm, n, dev, tmax, barrier):
         us = tmax(us)
         mt["k1_1GiB"] = {"us": round(us, 1), "algbw_GBs": round((1 << 30) / us / 1e3, 2), "correct": ok,
                          "reference_published": "A100 7701.98 us, 139.41 GB/s"}
+        checks["k1_1GiB"] = vf["all_ok"](ok) if vf else bool(ok)
         extras["mscclpp_test"] = mt
     except Exception as e:
         extras["mscclpp_test_error"] = str(e)

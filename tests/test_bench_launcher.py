@@ -243,3 +243,69 @@ def test_cpu_threaded_sum_matches_the_oracle():
     want = O.reduce_seq(O.F16, O.SUM, ins)
     got = bench._threaded_sum_for_test(n, nbytes, threads=5)
     assert np.array_equal(got, want)
+
+
+def _ring_output(bench, n, count, seq, order):
+    """An AllReduce output of ring_tensor inputs summed in `order` per owner slice (CPU)."""
+    out = torch.empty(count)
+    se = bench.ring_slice_elems(n, count)
+    for o in range(n):
+        lo, hi = o * se, min(count, (o + 1) * se)
+        if lo >= hi:
+            continue
+        ranks = [(o + k) % n for k in range(n)] if order == "ring" else list(range(n))
+        acc = bench.ring_tensor(lo, hi - lo, ranks[0], seq, "cpu")
+        for r in ranks[1:]:
+            acc += bench.ring_tensor(lo, hi - lo, r, seq, "cpu")
+        out[lo:hi] = acc
+    return out
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_fp32_ring_check_tells_the_order_apart(n, monkeypatch):
+    """the config-5 check (fp32 1 GiB rsag / rsag_zc) must catch a wrong sum order.
+    Its inputs (ring_bits: random sign, 8 exponents, full mantissa) make the ring-order sum differ from
+    the ascending-order sum on a large share of elements, the device-side check counts 0 mismatches
+    only for the ring order, and the CPU-oracle sample agrees.  A small chunk exercises the chunking."""
+    import bench
+
+    monkeypatch.setattr(bench, "RING_CHUNK", 1000)
+    count = n * 4096 + 36  # ragged last slice
+    i = np.arange(5000, dtype=np.int64)
+    assert np.array_equal(bench.ring_bits(i, 3, 1), bench.ring_bits(torch.from_numpy(i), 3, 1).numpy())
+    good = _ring_output(bench, n, count, 1, "ring")
+    wrong = _ring_output(bench, n, count, 1, "ascending")
+    assert bench.ring_order_mismatches(good, n, 1) == 0
+    bad = bench.ring_order_mismatches(wrong, n, 1)
+    assert bench.ring_order_mismatches(good, n, 0) > count // 2  # another seq's inputs
+    assert bench.ring_oracle_sample(good, n, 1, samples=3000)
+    if n == 2:  # a + b == b + a in IEEE arithmetic: two ranks have one sum whatever the order
+        assert bad == 0
+        return
+    assert bad > count // 8, bad  # slice 0's orders coincide; the others differ widely
+    assert not bench.ring_oracle_sample(wrong, n, 1, samples=3000)
+
+
+def test_extras_check_every_timed_size():
+    """the N>1 extras check every LL sweep size (eager and graph-captured), LL16 at
+    48 MiB and both fp32 1 GiB ring kernels before timing them, and all of it folds into `correct`."""
+    import bench
+
+    keys = set(bench.EXTRAS_CHECK_KEYS)
+    for kb in bench.LL_SWEEP_KIB:
+        assert f"ll_sweep:{kb}KiB" in keys and f"ll_graph:{kb}KiB" in keys
+    assert {"ll16_48MiB", "fp32_1GiB_rsag", "fp32_1GiB_rsag_zc"} <= keys
+    assert bench.LL_SWEEP_KIB[0] == 1 and bench.LL_SWEEP_KIB[-1] == 1024
+    ok = {"correct_bitexact": {k: True for k in keys}, "device_error": 0}
+    assert bench.extras_correct(ok, True)
+    assert bench.extras_correct({"device_error": 0}, False)
+    for k in ("ll_graph:64KiB", "fp32_1GiB_rsag_zc", "ll16_48MiB"):
+        missing = {"correct_bitexact": {q: True for q in keys if q != k}, "device_error": 0}
+        assert not bench.extras_correct(missing, True), k
+        wrong = {"correct_bitexact": dict(ok["correct_bitexact"], **{k: False}), "device_error": 0}
+        assert not bench.extras_correct(wrong, True), k
+    assert not bench.extras_correct(dict(ok, fp32_1GiB_error="boom"), True)
+    assert not bench.extras_correct(dict(ok, device_error=3), True)
+    extra_false = {"correct_bitexact": dict(ok["correct_bitexact"], **{"crossover:4KiB:packet:0x0": False})}
+    assert not bench.extras_correct(extra_false, True)
+    assert bench.ll16_ceiling(8) == pytest.approx(307.2)
