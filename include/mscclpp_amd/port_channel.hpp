@@ -46,6 +46,8 @@ class ProxyService : public BaseProxyService {
   void stopProxy() override;
   // Proxy thread's NUMA node (-1 before start or when unknown) and the number of triggers handled.
   int proxyNumaNode() const;
+  uint64_t proxyMaxPollGapNs() const;  // Proxy::maxPollGapNs of this service's proxy thread
+  void resetProxyPollGap();
   uint64_t triggersHandled() const { return handled_; }
 
  private:

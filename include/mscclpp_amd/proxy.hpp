@@ -27,6 +27,11 @@ class Proxy {
   void stop();
   Fifo& fifo() { return fifo_; }
   int numaNode() const { return numaNode_; }
+  // The longest time (ns) the proxy thread went between two polls of the FIFO since the last reset:
+  // a figure near the whole stall of an iteration means the thread was not running (host side).
+  // Measured only with MSCCLPP_AMD_PROXY_GAP_STATS=1 (a clock read per poll), else 0.
+  uint64_t maxPollGapNs() const { return maxGapNs_.load(std::memory_order_relaxed); }
+  void resetPollGap() { resetGap_.store(true, std::memory_order_relaxed); }
 
  private:
   int device_ = 0;
@@ -36,6 +41,8 @@ class Proxy {
   std::atomic<bool> running_{false};
   std::atomic<bool> started_{false};
   std::atomic<int> numaNode_{-1};
+  std::atomic<uint64_t> maxGapNs_{0};
+  std::atomic<bool> resetGap_{false};
 };
 
 // The NUMA node of a GPU (sysfs of its PCI device), -1 if unknown; numaBind pins the calling

@@ -126,7 +126,19 @@ void Proxy::start(bool blocking) {
     started_.store(true, std::memory_order_release);
     ProxyTrigger t;
     int runCnt = 4096;
+    static const bool gapStats = [] {
+      const char* e = std::getenv("MSCCLPP_AMD_PROXY_GAP_STATS");
+      return e && *e == '1';
+    }();
+    auto last = std::chrono::steady_clock::now();
     for (;;) {
+      if (gapStats) {
+        const auto now = std::chrono::steady_clock::now();
+        const uint64_t gap = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(now - last).count();
+        last = now;
+        if (resetGap_.exchange(false, std::memory_order_relaxed)) maxGapNs_.store(0, std::memory_order_relaxed);
+        else if (gap > maxGapNs_.load(std::memory_order_relaxed)) maxGapNs_.store(gap, std::memory_order_relaxed);
+      }
       if (runCnt-- == 0) {
         runCnt = 4096;
         if (!running_.load(std::memory_order_acquire)) break;
@@ -257,6 +269,10 @@ void ProxyService::stopProxy() {
   if (proxy_) proxy_->stop();
 }
 int ProxyService::proxyNumaNode() const { return proxy_ ? proxy_->numaNode() : -1; }
+uint64_t ProxyService::proxyMaxPollGapNs() const { return proxy_ ? proxy_->maxPollGapNs() : 0; }
+void ProxyService::resetProxyPollGap() {
+  if (proxy_) proxy_->resetPollGap();
+}
 
 namespace {
 // A failure on the proxy thread becomes the device error word's code (first one wins on the host

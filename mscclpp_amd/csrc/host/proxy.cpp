@@ -8,6 +8,7 @@
 // reported (the result's correctness flag and a warning), never dropped.
 #include <sched.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <fstream>
@@ -246,9 +247,11 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
 // registerMemory / sendMemory / recvMemory + ProxyService::buildAndAddSemaphore / addMemory /
 // portChannel, device handles copied to the GPU.
 // =============================================================================================
-extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int mode, int iters, double* out) {
+extern "C" int mscclppAmdPortChannelAllToAllStats(ncclComm_t comm, size_t chunk, int mode, int iters, double* out,
+                                                  int outLen) {
   return guarded([&] {
-    if (!comm || !out || chunk == 0 || chunk % 4 || mode < 0 || mode > 2) return (int)ncclInvalidArgument;
+    if (!comm || !out || outLen < 3 || chunk == 0 || chunk % 4 || mode < 0 || mode > 2 || iters <= 0)
+      return (int)ncclInvalidArgument;
     const int n = comm->nranks, rank = comm->rank;
     if (n < 2) return (int)ncclInvalidArgument;
     const size_t bytes = chunk * n;
@@ -265,6 +268,8 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
     bool ok = true;
     uint32_t e = 0;
     int numa = -1;
+    std::vector<double> per;  // us per iteration (HIP events)
+    double maxGapUs = 0;      // longest proxy-thread gap between FIFO polls (MSCCLPP_AMD_PROXY_GAP_STATS=1)
     {
       Communicator cx(comm);
       ProxyService proxy;
@@ -300,14 +305,34 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
       HIPCHECK(hipMemcpy(dch, ch.data(), ch.size() * sizeof(ch[0]), hipMemcpyHostToDevice));
       hipStream_t st;
       HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      // one untimed launch first: the kernel's code object loads at its first launch in a process
+      // (milliseconds), and the proxy thread's first trigger of each connection opens its copy path
+      if (mscclppAmdLaunchPortChannelPut(dch, (int)ch.size(), dOffs, dOffs + ch.size(), chunk, mode, st))
+        throw std::runtime_error("launch");
+      HIPCHECK(hipStreamSynchronize(st));
+      // iters launches back to back (the ranks start together at the barrier); an event before each
+      // launch and one after the last give every iteration's own duration on the stream
+      std::vector<hipEvent_t> ev((size_t)iters + 1);
+      for (auto& x : ev) HIPCHECK(hipEventCreate(&x));
       comm->boot->barrier();
+      proxy.resetProxyPollGap();
       t0 = nowSec();
       for (int i = 0; i < iters; ++i) {
+        HIPCHECK(hipEventRecord(ev[(size_t)i], st));
         if (mscclppAmdLaunchPortChannelPut(dch, (int)ch.size(), dOffs, dOffs + ch.size(), chunk, mode, st))
           throw std::runtime_error("launch");
       }
+      HIPCHECK(hipEventRecord(ev[(size_t)iters], st));
       HIPCHECK(hipStreamSynchronize(st));
       t1 = nowSec();
+      maxGapUs = (double)proxy.proxyMaxPollGapNs() * 1e-3;
+      per.resize((size_t)iters);
+      for (int i = 0; i < iters; ++i) {
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, ev[(size_t)i], ev[(size_t)i + 1]));
+        per[(size_t)i] = ms * 1e3;
+      }
+      for (auto& x : ev) (void)hipEventDestroy(x);
       comm->boot->barrier();
       // check: peer p's chunk addressed to me (its src chunk `rank`) sits at offset p*chunk of my dst
       std::vector<uint32_t> back(bytes / 4);
@@ -340,10 +365,24 @@ extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int 
     out[0] = (t1 - t0) * 1e6 / iters;
     out[1] = (ok && e == 0) ? 1.0 : 0.0;
     out[2] = (double)numa;
+    if (outLen >= 7) {  // per-iteration spread: median, min, max and the slowest iteration's index
+      std::vector<double> s = per;
+      std::sort(s.begin(), s.end());
+      const size_t m = s.size();
+      out[3] = m % 2 ? s[m / 2] : 0.5 * (s[m / 2 - 1] + s[m / 2]);
+      out[4] = s.front();
+      out[5] = s.back();
+      out[6] = (double)(std::max_element(per.begin(), per.end()) - per.begin());
+    }
+    if (outLen >= 8) out[7] = maxGapUs;
     freeDevice(src);
     freeDevice(dst);
     return (int)ncclSuccess;
   });
+}
+
+extern "C" int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int mode, int iters, double* out) {
+  return mscclppAmdPortChannelAllToAllStats(comm, chunk, mode, iters, out, 3);
 }
 
 // =============================================================================================

@@ -8,8 +8,9 @@
 // result came back wrong through .cpu() (k5 in the full `-m gpu` session, 6 of 6 sessions; the
 // buffer sat exactly where 1-2 MiB uncached buffers had been allocated and freed).  Uncached memory
 // is therefore never returned to HIP while the process runs: a freed block goes to a free list
-// (after a synchronize of the device that owns it, as hipFree does) and is handed out again, its
-// requested bytes zeroed, for a later request of its size class on the same device.
+// and is handed out again, its requested bytes zeroed, for a later request of its size class on the
+// same device -- after one device synchronize at that reuse (a free never synchronizes: kernels
+// queued before it may still use the block, so it waits in a pending list until then).
 //
 // Size classes: powers of two from 64 KiB up to 64 MiB; above that, multiples of 2 MiB (a 129 MiB
 // scratch holds 130 MiB, not 256).  A large request is served best-fit by a free block of at most
@@ -32,6 +33,9 @@ struct Block {
 struct UncachedPool {
   std::mutex mu;
   std::map<std::pair<int, size_t>, std::vector<void*>> freeBlocks;  // (device, class bytes) -> blocks
+  // freed by their owner, but kernels queued before the free may still use them: they join the free
+  // lists at the next device synchronize, which only an allocation that could reuse them pays
+  std::map<std::pair<int, size_t>, std::vector<void*>> pending;
   std::unordered_map<void*, Block> live;                            // block -> owner device, class
   std::map<int, hipStream_t> zeroStreams;  // per device: the stream the zero fill runs on
   size_t held = 0;                         // bytes allocated from HIP and never freed
@@ -72,9 +76,56 @@ void* takeFree(UncachedPool& P, int dev, size_t cls, size_t* got) {
   return nullptr;
 }
 
-// Zero the first `bytes` of a block on the pool's own stream of `dev` (never the null stream: a
-// legacy-stream memset would join, or break, another thread's graph capture).
+// Is a pending block of `dev` able to serve `cls` (caller holds the lock)?
+bool pendingFits(UncachedPool& P, int dev, size_t cls) {
+  auto it = P.pending.lower_bound({dev, cls});
+  const size_t limit = cls > kPow2Max ? cls + cls / 4 : cls;
+  for (; it != P.pending.end() && it->first.first == dev && it->first.second <= limit; ++it)
+    if (!it->second.empty()) return true;
+  return false;
+}
+
+// Move every pending block of `dev` to the free lists once the device has drained (the current
+// device is `dev`); blocks of a device that cannot synchronize are leaked.
+void drainPending(UncachedPool& P, int dev) {
+  const hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) (void)hipGetLastError();
+  std::lock_guard<std::mutex> lk(P.mu);
+  for (auto it = P.pending.lower_bound({dev, 0}); it != P.pending.end() && it->first.first == dev; ++it) {
+    for (void* b : it->second) {
+      if (e == hipSuccess) P.freeBlocks[it->first].push_back(b);
+      else P.leaked += it->first.second;
+    }
+    it->second.clear();
+  }
+}
+
+// Zero the first `bytes` of a block of `dev`.
 void zeroFill(UncachedPool& P, int dev, void* p, size_t bytes) {
+  // The fill runs on a stream created for it and destroyed after it (default): never the null
+  // stream (a legacy-stream memset would join, or break, another thread's graph capture), and no
+  // stream left behind -- a persistent extra stream in the process made every PortChannel put
+  // 1.4-1.7x slower (round 4: 108 -> 183 us putWithSignal at 1 MiB; tools/portchannel_ab.py,
+  // profiles/r5_portchannel_ab.json).  MSCCLPP_AMD_POOL_ZERO (diagnosis): "legacy" = the null-stream
+  // hipMemset of round 3, "stream" = the persistent per-device stream of round 4.
+  static const int how = [] {
+    const char* e = std::getenv("MSCCLPP_AMD_POOL_ZERO");
+    const std::string v = e ? e : "";
+    return v == "legacy" ? 1 : v == "stream" ? 0 : 2;
+  }();
+  if (how == 1) {
+    HIPCHECK(hipMemset(p, 0, bytes));
+    return;
+  }
+  if (how == 2) {
+    hipStream_t t = nullptr;
+    HIPCHECK(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
+    const hipError_t e1 = hipMemsetAsync(p, 0, bytes, t);
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamSynchronize(t) : e1;
+    (void)hipStreamDestroy(t);
+    HIPCHECK(e2);
+    return;
+  }
   hipStream_t s = nullptr;
   {
     std::lock_guard<std::mutex> lk(P.mu);
@@ -114,6 +165,23 @@ void* allocUncached(size_t bytes) {
       }
     }
   }
+  if (!p && P.enabled) {
+    bool reuse = false;
+    {
+      std::lock_guard<std::mutex> lk(P.mu);
+      reuse = pendingFits(P, dev, cls);
+    }
+    if (reuse) {  // a freed block fits: wait for the device once, then take it
+      drainPending(P, dev);
+      std::lock_guard<std::mutex> lk(P.mu);
+      size_t got = 0;
+      p = takeFree(P, dev, cls, &got);
+      if (p) {
+        cls = got;
+        P.live[p] = Block{dev, cls};
+      }
+    }
+  }
   if (!p) {
     HIPCHECK(hipExtMallocWithFlags(&p, cls, hipDeviceMallocUncached));
     std::lock_guard<std::mutex> lk(P.mu);
@@ -122,7 +190,14 @@ void* allocUncached(size_t bytes) {
       P.held += cls;
     }
   }
-  zeroFill(P, dev, p, bytes);
+  try {
+    zeroFill(P, dev, p, bytes);
+  } catch (...) {  // the caller never receives the block: it must not stay live (counted, never reused)
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (P.live.erase(p)) P.pending[{dev, cls}].push_back(p);
+    else (void)hipFree(p);
+    throw;
+  }
   return p;
 }
 
@@ -130,32 +205,14 @@ bool releaseUncached(void* p, hipError_t* syncError) noexcept {
   if (syncError) *syncError = hipSuccess;
   if (!p) return true;
   UncachedPool& P = pool();
-  Block b{};
-  {
-    std::lock_guard<std::mutex> lk(P.mu);
-    auto it = P.live.find(p);
-    if (it == P.live.end()) return false;  // not a pooled block
-    b = it->second;
-  }
-  // as hipFree: no queued kernel of the owning device may still use the block when it is handed
-  // out again.  If that device cannot be synchronized (a sticky error), the block is leaked -- it
-  // leaves the live set but never reaches the free list.
-  int cur = -1;
-  hipError_t e = hipGetDevice(&cur);
-  if (e == hipSuccess && cur != b.device) e = hipSetDevice(b.device);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
-  if (cur >= 0 && cur != b.device) (void)hipSetDevice(cur);
-  if (e != hipSuccess) (void)hipGetLastError();
+  // No synchronize here: the block waits in `pending` -- kernels queued before
+  // this free may still use it -- until an allocation that could reuse it drains the device once
+  // (as hipFree would have, but only when reuse is possible, never on the free path).
   std::lock_guard<std::mutex> lk(P.mu);
   auto it = P.live.find(p);
-  if (it == P.live.end()) return true;
+  if (it == P.live.end()) return false;  // not a pooled block
+  P.pending[{it->second.device, it->second.cls}].push_back(p);
   P.live.erase(it);
-  if (e == hipSuccess) {
-    P.freeBlocks[{b.device, b.cls}].push_back(p);
-  } else {
-    P.leaked += b.cls;
-    if (syncError) *syncError = e;
-  }
   return true;
 }
 
@@ -176,6 +233,7 @@ void uncachedPoolStats(size_t* held, size_t* inUse, size_t* freeBytes) {
   size_t used = 0, fr = 0;
   for (const auto& e : P.live) used += e.second.cls;
   for (const auto& e : P.freeBlocks) fr += e.first.second * e.second.size();
+  for (const auto& e : P.pending) fr += e.first.second * e.second.size();
   if (held) *held = P.held;
   if (inUse) *inUse = used;
   if (freeBytes) *freeBytes = fr;

@@ -13,6 +13,9 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+PC_ITERS = 20  # PortChannel all-to-all iterations per mode (median / min / max over >= 20)
+
+
 def worker(rank, n, uid, size, q):
     try:
         import torch
@@ -24,8 +27,8 @@ def worker(rank, n, uid, size, q):
         L = m.lib()
         L.mscclppAmdHostOffloadAllGather.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                                      ctypes.POINTER(ctypes.c_double)]
-        L.mscclppAmdPortChannelAllToAll.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
-                                                    ctypes.POINTER(ctypes.c_double)]
+        L.mscclppAmdPortChannelAllToAllStats.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                                         ctypes.POINTER(ctypes.c_double), ctypes.c_int]
         comm = m.Communicator(rank, n, uid)
         out = (ctypes.c_double * 4)()
         print(f"[host_proxy rank {rank}/{n}] host-offload loop", file=sys.stderr, flush=True)
@@ -35,10 +38,14 @@ def worker(rank, n, uid, size, q):
                "proxy_numa_node": int(out[3])}
         pc = {}
         for mode in (0, 1, 2):
-            o = (ctypes.c_double * 3)()
-            m.check(L.mscclppAmdPortChannelAllToAll(comm.comm, 1 << 20, mode, 5, o), "portchannel")
-            pc[["put+signal", "putWithSignal", "putWithSignalAndFlush"][mode]] = {"us": round(o[0], 2),
-                                                                                  "correct": o[1] == 1.0}
+            # PC_ITERS back-to-back iterations after one untimed launch; each iteration's own time from
+            # HIP events: median (the row's figure), min and max, and the slowest iteration's index
+            o = (ctypes.c_double * 8)()
+            m.check(L.mscclppAmdPortChannelAllToAllStats(comm.comm, 1 << 20, mode, PC_ITERS, o, 8), "portchannel")
+            pc[["put+signal", "putWithSignal", "putWithSignalAndFlush"][mode]] = {
+                "us": round(o[3], 2), "min_us": round(o[4], 2), "max_us": round(o[5], 2),
+                "mean_us_wall": round(o[0], 2), "slowest_iteration": int(o[6]), "iterations": PC_ITERS,
+                "correct": o[1] == 1.0}
         res["portchannel_alltoall_1MiB"] = pc
         comm.destroy()
         q.put((rank, res, None))
