@@ -1,0 +1,11 @@
+// <mscclpp/memory_channel_device.hpp> on this library: MemoryChannelDeviceHandle: put / get / putPackets / unpackPackets / signal / wait.
+// A caller written against the reference's include/mscclpp/memory_channel_device.hpp compiles unchanged with
+// `-I include`: the declarations live in mscclpp_amd/memory_channel_device.hpp, and namespace mscclpp names them through
+// a using-directive (qualified lookup of mscclpp::X finds mscclpp_amd::X; include/mscclpp/namespace.hpp).
+#ifndef MSCCLPP_AMD_FWD_MEMORY_CHANNEL_DEVICE_HPP_
+#define MSCCLPP_AMD_FWD_MEMORY_CHANNEL_DEVICE_HPP_
+
+#include "mscclpp_amd/memory_channel_device.hpp"
+#include "mscclpp/namespace.hpp"
+
+#endif  // MSCCLPP_AMD_FWD_MEMORY_CHANNEL_DEVICE_HPP_

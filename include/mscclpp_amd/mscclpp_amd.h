@@ -91,8 +91,9 @@ typedef struct {
 /* ---- memory ------------------------------------------------------------------------------- */
 /* Uncached memory (hipDeviceMallocUncached, zeroed; the reference's GpuBuffer on AMD,
  * gpu_utils.cc:139-147) comes from a process-lifetime pool: mscclppAmdFree hands a pooled block back
- * to the pool (after a device synchronize, as hipFree does), never to HIP, so no later allocation is
- * placed where uncached memory was.  mscclppAmdFree hipFree's anything else.
+ * to the pool, never to HIP, so no later allocation is placed where uncached memory was (DESIGN.md
+ * §21).  The free does not synchronize: the block is reused only after a device synchronize, paid by
+ * the allocation that reuses it.  mscclppAmdFree hipFree's anything else.
  * mscclppAmdUncachedPoolStats: bytes allocated from HIP, in use, and free in the pool. */
 int mscclppAmdMallocUncached(void** ptr, size_t bytes);
 int mscclppAmdMalloc(void** ptr, size_t bytes);
@@ -237,8 +238,14 @@ int mscclppAmdCommAllGatherHost(ncclComm_t comm, const void* sendbuf, void* recv
  * gathered data is correct, out[3] = NUMA node the proxy thread was bound to (-1 if none). */
 int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, int iters, int graphIters, double* out);
 /* PortChannel all-to-all through the proxy (mode 0: put+signal, 1: putWithSignal,
- * 2: putWithSignalAndFlush).  out[0] = us per iteration, out[1] = 1 if correct, out[2] = NUMA node. */
+ * 2: putWithSignalAndFlush).  out[0] = us per iteration (wall clock over `iters` back-to-back
+ * launches after one untimed launch), out[1] = 1 if correct, out[2] = NUMA node. */
 int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int mode, int iters, double* out);
+/* The same with each iteration's own duration (a HIP event before every launch): with outLen >= 7,
+ * out[3] = median, out[4] = min, out[5] = max us per iteration, out[6] = index of the slowest one;
+ * with outLen >= 8, out[7] = the proxy thread's longest gap between FIFO polls in us over the timed
+ * iterations (measured with MSCCLPP_AMD_PROXY_GAP_STATS=1, else 0). */
+int mscclppAmdPortChannelAllToAllStats(ncclComm_t comm, size_t chunk, int mode, int iters, double* out, int outLen);
 /* mscclpp-test allreduce1 (test/mscclpp-test/allreduce_test.cu:730-839): int32 ring RS + AG whose data
  * moves through PortChannels and the host proxy (hipMemcpyAsync).  out[0] = us per AllReduce (graph of
  * `iters` kernels replayed `graphLaunches` times), out[1] = 1 if every element is n(n-1)/2, out[2] =

@@ -535,7 +535,12 @@ int mscclppAmdCommRegistrationStats(ncclComm_t comm, size_t* userRegistrations, 
   std::lock_guard<std::mutex> lk(comm->mu);
   if (userRegistrations) *userRegistrations = comm->userRegs.size();
   if (liveMappings) *liveMappings = liveIpcMappings();
-  if (retiredMappings) *retiredMappings = comm->retired.size();
+  if (retiredMappings) {  // mappings still waiting for their last launches to complete
+    comm->flushRetired();
+    size_t k = 0;
+    for (const auto& r : comm->retired) k += r.maps.size();
+    *retiredMappings = k;
+  }
   return ncclSuccess;
 }
 

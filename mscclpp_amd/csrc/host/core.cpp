@@ -13,6 +13,9 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <thread>
 #include <random>
 #include <unordered_map>
 
@@ -65,6 +68,68 @@ std::shared_ptr<void> openIpcHandle(const hipIpcMemHandle_t& handle) {
   return p;
 }
 
+namespace {
+// Mappings whose last user has gone, closed on a thread of their own: hipIpcCloseMemHandle waits for
+// the whole device to go idle, so a close on a caller's thread would stall that caller behind every
+// stream of the device.  The thread is started on first use and never joined
+// (its state is never destroyed, like the pool's): closes still queued at exit are left to the OS.
+struct Closer {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<int, std::shared_ptr<void>>> q;
+  size_t inFlight = 0;  // queued or being closed
+  bool started = false;
+};
+Closer& closer() {
+  static Closer* c = new Closer();
+  return *c;
+}
+void closerLoop() {
+  Closer& c = closer();
+  for (;;) {
+    std::pair<int, std::shared_ptr<void>> item;
+    {
+      std::unique_lock<std::mutex> lk(c.mu);
+      c.cv.wait(lk, [&] { return !c.q.empty(); });
+      item = std::move(c.q.front());
+      c.q.pop_front();
+    }
+    if (item.first >= 0) (void)hipSetDevice(item.first);
+    item.second.reset();  // the last reference: the deleter closes the mapping here
+    std::lock_guard<std::mutex> lk(c.mu);
+    --c.inFlight;
+    c.cv.notify_all();
+  }
+}
+// At exit, before the HIP runtime's own teardown (this handler is registered after HIP started):
+// let the queued closes finish, for at most 10 s, so no close is still inside HIP when it unloads.
+void drainCloser() {
+  Closer& c = closer();
+  std::unique_lock<std::mutex> lk(c.mu);
+  c.cv.wait_for(lk, std::chrono::seconds(10), [&] { return c.inFlight == 0; });
+}
+}  // namespace
+
+void releaseMappingLater(int device, std::shared_ptr<void> map) {
+  if (!map) return;
+  Closer& c = closer();
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (!c.started) {
+    std::thread(closerLoop).detach();
+    std::atexit(drainCloser);
+    c.started = true;
+  }
+  c.q.emplace_back(device, std::move(map));
+  ++c.inFlight;
+  c.cv.notify_all();
+}
+
+size_t pendingMappingReleases() {
+  Closer& c = closer();
+  std::lock_guard<std::mutex> lk(c.mu);
+  return c.inFlight;
+}
+
 size_t liveIpcMappings() {
   std::lock_guard<std::mutex> lk(gIpcMu);
   size_t n = 0;
@@ -101,7 +166,11 @@ std::map<std::pair<uint64_t, uint64_t>, Kept> gKept;  // (owner, base) -> mappin
 
 std::shared_ptr<void> openIpcImport(const hipIpcMemHandle_t& handle, uint64_t owner, uint64_t base, uint64_t bytes,
                                     bool pooled) {
-  if (!pooled || !owner) return openIpcHandle(handle);
+  static const bool keep = [] {  // diagnosis (tools/portchannel_ab.py): "0" opens every import afresh
+    const char* e = std::getenv("MSCCLPP_AMD_IPC_KEEP");
+    return !(e && std::string(e) == "0");
+  }();
+  if (!pooled || !owner || !keep) return openIpcHandle(handle);
   std::lock_guard<std::mutex> lk(gKeptMu);
   const auto key = std::make_pair(owner, base);
   auto it = gKept.find(key);

@@ -13,6 +13,10 @@ if TESTS not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
+    # rank processes decide their hardware-queue count from this before HIP starts (tests/mp_util.py)
+    import mp_util
+
+    mp_util.export_device_count()
 
 
 @pytest.fixture(scope="session")

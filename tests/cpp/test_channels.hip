@@ -1,6 +1,9 @@
-// Two ranks (processes), channels built with the host API of include/mscclpp_amd (core.hpp,
-// semaphore.hpp, memory_channel.hpp, port_channel.hpp) exactly as a user of the reference builds
-// them, driven by kernels written with the reference's device spellings (namespace alias only):
+// Two ranks (processes), channels built with the host API (core.hpp, semaphore.hpp,
+// memory_channel.hpp, port_channel.hpp) exactly as a user of the reference builds them, driven by
+// kernels written with the reference's device spellings.  Everything is included through the
+// reference's paths (include/mscclpp/*.hpp, forwarding to include/mscclpp_amd) and spelled
+// mscclpp::..., with no alias or rename; only the harness's C entry points come
+// from mscclpp_amd.h:
 //   memory channel  LL8 / LL16 packet ping-pong     test/mp_unit/memory_channel_tests.cu:246-325
 //                   put + signal / wait ping-pong    memory_channel_tests.cu (put ping-pong)
 //                   get ping-pong                    memory_channel_tests.cu (get ping-pong)
@@ -20,14 +23,17 @@
 #include <type_traits>
 #include <vector>
 
-#include "mscclpp_amd/core.hpp"
-#include "mscclpp_amd/gpu_utils.hpp"
-#include "mscclpp_amd/memory_channel.hpp"
-#include "mscclpp_amd/mscclpp_amd.h"
-#include "mscclpp_amd/nccl.h"
-#include "mscclpp_amd/port_channel.hpp"
+#include <mscclpp/core.hpp>
+#include <mscclpp/ext/nccl/nccl.h>
+#include <mscclpp/gpu_utils.hpp>
+#include <mscclpp/memory_channel.hpp>
+#include <mscclpp/memory_channel_device.hpp>
+#include <mscclpp/packet_device.hpp>
+#include <mscclpp/port_channel.hpp>
+#include <mscclpp/port_channel_device.hpp>
 
-namespace mscclpp = mscclpp_amd;  // the kernels below are spelled as against include/mscclpp
+#include "mscclpp_amd/mscclpp_amd.h"
+
 using mscclpp::DeviceHandle;
 
 #define CHECK(cond)                                                                              \

@@ -8,9 +8,11 @@
   ProxyService, driven by kernels written with the reference's spellings (LL8/LL16 packet ping-pong
   of test/mp_unit/memory_channel_tests.cu:246-325, unpackPacket, put/get ping-pong, the proxy LL
   ping-pong of port_channel_tests.cu:337-446 with copyToPackets / copyFromPackets);
-* tests/cpp/test_customized_allgather.hip -- the reference's plugin example
-  (examples/customized-collective-algorithm/customized_allgather.cu) with PortChannels through
-  ProxyService, reached through ncclAllGather, direct and graph-captured, exact."""
+* tests/cpp/test_customized_allgather.hip -- a user AllGather plugged in through the C++ algorithm
+  interface with the API sequence of the reference's plugin example (examples/customized-collective-
+  algorithm/): PortChannels through ProxyService, reached through ncclAllGather, direct and
+  graph-captured, exact.
+Both C++ programs include the reference's header paths (include/mscclpp/*.hpp) and spell mscclpp::."""
 import os
 import subprocess
 
