@@ -295,7 +295,9 @@ size_t RegisteredMemory::size() const { return pimpl_ ? (size_t)pimpl_->size : 0
 TransportFlags RegisteredMemory::transports() const { return pimpl_ ? pimpl_->transports : TransportFlags(); }
 int RegisteredMemory::rank() const { return pimpl_ ? pimpl_->rank : -1; }
 bool RegisteredMemory::coherent() const { return pimpl_ && pimpl_->coherent; }
-bool RegisteredMemory::remote() const { return pimpl_ && pimpl_->pid != (int32_t)getpid(); }
+// Local or remote by the owner's process nonce, not its PID: ranks in separate PID namespaces that
+// share the GPU's IPC namespace (containers with host IPC) can share a PID.
+bool RegisteredMemory::remote() const { return pimpl_ && pimpl_->owner != host::processNonce(); }
 
 std::vector<char> RegisteredMemory::serialize() const {
   if (!pimpl_) throw Error("serialize: empty RegisteredMemory", ErrorCode::InvalidUsage);
@@ -329,7 +331,7 @@ RegisteredMemory RegisteredMemory::deserialize(const std::vector<char>& data) {
   impl->owner = w.owner;
   impl->pooled = (w.flags & 1u) != 0;
   impl->coherent = (w.flags & 2u) != 0;
-  if (w.pid == (int32_t)getpid()) {
+  if (w.owner == host::processNonce()) {
     impl->data = (void*)w.original;  // same process (in-process ranks): the pointer is usable as is
   } else {
     try {
@@ -488,7 +490,11 @@ RegisteredMemory Communicator::registerMemory(void* ptr, size_t size, TransportF
   {
     hipPointerAttribute_t attr{};
     if (hipPointerGetAttributes(&attr, ptr) == hipSuccess) {
-      impl->coherent = attr.type == hipMemoryTypeHost;
+      // host memory (pinned, or pageable: "unregistered" on ROCm 6), and device memory allocated
+      // fine-grained or uncached (hipExtMallocWithFlags: both flags carry the fine-grained bit) are
+      // coherent with the proxy's copies; the pool's blocks are recognised below
+      impl->coherent = attr.type == hipMemoryTypeHost || attr.type == hipMemoryTypeUnregistered ||
+                       (attr.type == hipMemoryTypeDevice && (attr.allocationFlags & hipDeviceMallocFinegrained) != 0);
     } else {
       (void)hipGetLastError();
       impl->coherent = true;  // pageable host memory, unknown to HIP

@@ -200,17 +200,18 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
 // The packets still go through the packet buffer in memory with their flags polled; what goes away
 // is the wait for a partner workgroup that the dispatcher started up to ~0.6 us later on another
 // XCD: 64-256 KiB 3.44-3.46 against 4.04-4.12 us, 1 MiB 3.40 / 4.57, 2 MiB 4.11 / 5.93, 4 MiB
-// 6.2 / 8.1 (graph-captured, one box).  Earlier notes:
+// 6.2 / 8.1 (graph-captured, one box).  The shape rule below (current since round 4):
 // 4 waves x 1 KiB per workgroup and round, one workgroup per 4 KiB tile up to 1024 workgroups (4 per
-// CU, all resident, so every partner pair is co-resident); 8 waves per workgroup for 1-4 MiB.
-//  * one round (up to 4 MiB): payload read and written with the default cache policy (a bucket just
-//    written or read by the caller is served from the caches): 3.6-3.7 us at 64-256 KiB, against
-//    4.6 us with one-wave workgroups per KiB and 5.0 us for round 2's 8 KiB tiles;
-//  * two rounds: unskewed; 3-7 rounds: partner tiles consumed one round late; from 8 rounds (48 MiB:
-//    12) two rounds late; nt payload accesses.  The skew gives a packet time to land before its first
-//    poll: at 48 MiB 2.7 % of the packets miss it with two rounds (6.6 % with one, 13.9 % with none),
-//    52.7 us against 53.1 us (one round late) and 54.1 us (round 2's 2 KiB per wave); with 4 rounds
-//    the second drain round costs more than it saves (16 MiB: 24.5 against 21.8 us).
+// CU, all resident); 8 waves per workgroup for 1-4 MiB.  In every form the partner is the same
+// workgroup's neighbouring wave (PMASK 0).
+//  * one round (up to 4 MiB): unskewed, payload read and written with the default cache policy (a
+//    bucket just written or read by the caller is served from the caches);
+//  * 2-7 rounds: the partner's tile is consumed one round late (skew 1); from 8 rounds (48 MiB: 12)
+//    two rounds late (skew 2); nt payload accesses.  The skew gives a packet time to land before its
+//    first poll.
+// Superseded round-3 figures (cross-XCD partner workgroup b ^ 1, two rounds unskewed): 3.6-3.7 us at
+// 64-256 KiB; at 48 MiB 2.7 % of the packets missed their first poll with skew 2 (6.6 % with one,
+// 13.9 % with none).
 struct SelfReduceShape {
   int waves, units, nblocks;
   int skew;    // rounds between packing a tile and its partner consuming it

@@ -8,7 +8,7 @@
 // own: one workgroup per peer, whose lane 0 issues putWithSignalAndFlush and waits for the peer's
 // signal.  Everything is included and spelled as against the reference (<mscclpp/...>, mscclpp::).
 //
-//   test_customized_allgather gpu <nranks> [floats per rank] [cached | uncached | refuse]
+//   test_customized_allgather gpu <nranks> [floats per rank] [cached | uncached | refuse | direct]
 //
 // The PortChannel destination contract: `cached` (hipMalloc receive buffer) is
 // exact -- the receiving kernel only waits for the signal, the data is read after it -- and
@@ -16,7 +16,9 @@
 // receive buffer from the uncached pool (no warning); `refuse` runs with
 // MSCCLPP_AMD_PORT_CHANNEL_DST=strict and expects the first ncclAllGather to return
 // ncclInvalidUsage on every rank (ProxyService::addMemory refuses the peer's buffer before any
-// semaphore is built, so no rank is left waiting for another).
+// semaphore is built, so no rank is left waiting for another); `direct` allocates the receive buffer
+// with hipExtMallocWithFlags(hipDeviceMallocUncached) itself -- not from the pool -- and runs under
+// strict: it is coherent, so it must be accepted, exact, with no warning.
 #include <hip/hip_runtime.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -178,9 +180,11 @@ int runRank(int rank, int n, ncclUniqueId id, size_t count, const std::string& m
   REQUIRE(hipMalloc(&send, bytes) == hipSuccess);
   if (mode == "uncached")
     REQUIRE(mscclppAmdMallocUncached((void**)&recv, bytes * n) == 0);
+  else if (mode == "direct")
+    REQUIRE(hipExtMallocWithFlags((void**)&recv, bytes * n, hipDeviceMallocUncached) == hipSuccess);
   else
     REQUIRE(hipMalloc(&recv, bytes * n) == hipSuccess);
-  if (mode == "refuse") setenv("MSCCLPP_AMD_PORT_CHANNEL_DST", "strict", 1);
+  if (mode == "refuse" || mode == "direct") setenv("MSCCLPP_AMD_PORT_CHANNEL_DST", "strict", 1);
   std::vector<float> mine(count);
   for (size_t i = 0; i < count; ++i) mine[i] = expectedValue(rank, i);
   REQUIRE(hipMemcpy(send, mine.data(), bytes, hipMemcpyHostToDevice) == hipSuccess);
@@ -253,13 +257,13 @@ int runRank(int rank, int n, ncclUniqueId id, size_t count, const std::string& m
 
 int main(int argc, char** argv) {
   if (argc < 3 || std::string(argv[1]) != "gpu") {
-    std::fprintf(stderr, "usage: %s gpu <nranks> [floats per rank] [cached | uncached | refuse]\n", argv[0]);
+    std::fprintf(stderr, "usage: %s gpu <nranks> [floats per rank] [cached | uncached | refuse | direct]\n", argv[0]);
     return 2;
   }
   const int n = std::atoi(argv[2]);
   const size_t count = argc >= 4 ? (size_t)std::atoll(argv[3]) : (size_t)1 << 20;
   const std::string mode = argc >= 5 ? argv[4] : "cached";
-  if (n < 2 || (mode != "cached" && mode != "uncached" && mode != "refuse")) return 2;
+  if (n < 2 || (mode != "cached" && mode != "uncached" && mode != "refuse" && mode != "direct")) return 2;
   ncclUniqueId id;
   if (ncclGetUniqueId(&id) != ncclSuccess) return 1;
   std::vector<pid_t> kids;

@@ -49,10 +49,11 @@ def test_memory_and_port_channels_reference_spellings(built):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [2, 4])
-@pytest.mark.parametrize("mode", ["cached", "uncached"])
+@pytest.mark.parametrize("mode", ["cached", "uncached", "direct"])
 def test_customized_allgather_port_channels(built, n, mode):
     """PortChannel destinations: the example's hipMalloc receive
-    buffer is exact and gets the one-time warning; a pool (uncached) receive buffer gets none."""
+    buffer is exact and gets the one-time warning; a pool (uncached) receive buffer gets none; an
+    uncached buffer from hipExtMallocWithFlags itself is accepted even under strict."""
     out = _run("test_customized_allgather", ["gpu", str(n), str(1 << 18), mode], 200)
     assert "gpu OK" in out and all(f"rank {r} OK" in out for r in range(n)), out
     assert ("is cached device memory" in out) == (mode == "cached"), out
