@@ -421,6 +421,7 @@ struct ncclComm {
   // After a launch on `stream`: the registrations it used record their use there.  Under capture
   // nothing is recorded -- those registrations are pinned (never retired while a graph may replay).
   void recordUses(hipStream_t stream) {
+    if (touched.empty()) return;  // the LL paths register nothing: no extra host call per launch
     if (!capturing(stream))
       for (UseEvents* u : touched) u->record(stream);
     touched.clear();
