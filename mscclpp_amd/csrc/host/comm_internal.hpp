@@ -314,14 +314,21 @@ struct ncclComm {
   // right after that launch (re-recorded by later launches on the same stream).
   struct UseEvents {
     std::vector<std::pair<hipStream_t, hipEvent_t>> ev;
-    void record(hipStream_t s) {
+    // `device`: the communicator's (and the stream's); the event is created there whatever device
+    // the calling thread has current
+    void record(hipStream_t s, int device) {
       for (auto& e : ev)
         if (e.first == s) {
           HIPCHECK(hipEventRecord(e.second, s));
           return;
         }
+      int cur = device;
+      HIPCHECK(hipGetDevice(&cur));
+      if (cur != device) HIPCHECK(hipSetDevice(device));
       hipEvent_t x = nullptr;
-      HIPCHECK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+      const hipError_t e = hipEventCreateWithFlags(&x, hipEventDisableTiming);
+      if (cur != device) (void)hipSetDevice(cur);
+      HIPCHECK(e);
       ev.push_back({s, x});
       HIPCHECK(hipEventRecord(x, s));
     }
@@ -423,7 +430,7 @@ struct ncclComm {
   void recordUses(hipStream_t stream) {
     if (touched.empty()) return;  // the LL paths register nothing: no extra host call per launch
     if (!capturing(stream))
-      for (UseEvents* u : touched) u->record(stream);
+      for (UseEvents* u : touched) u->record(stream, device);
     touched.clear();
   }
 
@@ -602,7 +609,7 @@ struct ncclComm {
       v.peerInput[root] = (char*)m.get() + all[root].offset;
     }
     const int rc = launchBroadcast(&v, 1, nranks, bytes, root, nblocks, nthreads, spinBudgetTicks(), stream);
-    if (rank != root && rc == 0 && !capturing(stream)) bcastUses[(size_t)root].record(stream);
+    if (rank != root && rc == 0 && !capturing(stream)) bcastUses[(size_t)root].record(stream, device);
     flushRetired();
     return rc;
   }
