@@ -45,7 +45,7 @@ def worker(rank, n, uid, size, q):
             pc[["put+signal", "putWithSignal", "putWithSignalAndFlush"][mode]] = {
                 "us": round(o[3], 2), "min_us": round(o[4], 2), "max_us": round(o[5], 2),
                 "mean_us_wall": round(o[0], 2), "slowest_iteration": int(o[6]), "iterations": PC_ITERS,
-                "correct": o[1] == 1.0}
+                "proxy_max_poll_gap_us": round(o[7], 1), "correct": o[1] == 1.0}
         res["portchannel_alltoall_1MiB"] = pc
         comm.destroy()
         q.put((rank, res, None))
@@ -58,12 +58,18 @@ def worker(rank, n, uid, size, q):
 def run(n=2, size=4096, timeout=180):
     import mscclpp_amd as m
 
+    # every proxy thread records its longest gap between FIFO polls (a clock read per poll): a gap
+    # near an iteration's stall says the thread was off the CPU (host side), DESIGN.md §9
+    saved = os.environ.get("MSCCLPP_AMD_PROXY_GAP_STATS")
+    os.environ.setdefault("MSCCLPP_AMD_PROXY_GAP_STATS", "1")  # inherited by the spawned ranks only
     uid = m.Communicator.unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=worker, args=(r, n, uid, size, q)) for r in range(n)]
     for p in ps:
         p.start()
+    if saved is None:
+        del os.environ["MSCCLPP_AMD_PROXY_GAP_STATS"]
     got = {}
     deadline = time.monotonic() + timeout
     try:
