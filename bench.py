@@ -1283,7 +1283,10 @@ def bench_extras(args, comm, n, dev, tmax, barrier, vf=None):
         a0, a1 = lcg_pair(nbytes // 2)
         o = torch.empty_like(a0)
         peers = n - 1
-        shapes = [(0, 0), (peers * 16, 512), (peers * 32, 512)]
+        # rehearsals at 2-4 ranks: wider grids win at this size (4 ranks: 48 workgroups 605 us,
+        # 96 workgroups 352 us; profiles/r5_bench_n4_rehearsal_line.json), so the node tries up to 64
+        # per peer (448 at 8 ranks, all resident on one GPU)
+        shapes = [(0, 0), (peers * 16, 512), (peers * 32, 512), (peers * 64, 512)]
         if ndev_shared(n):  # rehearsal: every rank's grid resident on the shared device
             shapes = [s for s in shapes if s[0] * n <= 512]
         row, ok = {}, True
