@@ -747,7 +747,7 @@ def bench_multi(args):
     algos = [args.algo] if args.algo else ([sel] + [a for a in ("fullmesh", "rsag_zc", "rsag_pipeline") if a != sel]
                                            if sel in ("fullmesh", "rsag_zc", "rsag_pipeline") else [sel])
     cands = []
-    shared = ndev < world  # rehearsal: ranks share a device, so every rank's grid must fit on it at once
+    shared = ndev_shared(world)  # rehearsal: ranks share a device, so every rank's grid must fit on it at once
     # rehearsal shapes: small enough that every rank's grid is resident on the one shared device
     bulk_shapes = ((32, 512), (64, 512), (128, 512), (256, 512), (128, 256), (256, 256)) if not shared else \
         tuple((nb_, 512) for nb_ in (16, 32, 64, 128) if nb_ * world <= 256)
@@ -1181,8 +1181,10 @@ def graph_time_per_call(fn, calls=20, replays=10, sync=None, keep=False):
 
 
 def ndev_shared(n):
-    """True in a rehearsal where n ranks share fewer devices (grids must then fit together)."""
-    return torch.cuda.device_count() < n
+    """True in a rehearsal where n ranks share fewer devices, so every rank's grid must fit on the
+    device at once and the launch shapes are cut down.  BENCH_NODE_SHAPES=1 (diagnosis) keeps the
+    node's shapes anyway: a 2-rank run on one GPU then walks the node-only branches of this file."""
+    return torch.cuda.device_count() < n and os.environ.get("BENCH_NODE_SHAPES") != "1"
 
 
 LL_SWEEP_KIB = tuple(1 << k for k in range(11))  # BASELINE configs[3]: 1 KiB .. 1 MiB, x2 steps
