@@ -1470,7 +1470,10 @@ def bench_extras(args, comm, n, dev, tmax, barrier, vf=None):
             row.update({"ms": round(t * 1e3, 3), "algbw_GBs": round(ach, 2),
                         "busbw_GBs": round(ach * 2 * (n - 1) / n, 2), "peak": round(peak, 1),
                         "frac": round(ach / peak, 4),
-                        "peak_source": "n * 153.6 / 2 GB/s, the all-pairs AllReduce algbw ceiling (BASELINE.md §2)"})
+                        "peak_source": "n * 153.6 / 2 GB/s, the all-pairs AllReduce algbw ceiling (BASELINE.md §2)",
+                        # SURVEY §8(d) config 5's contrast: one ring over one link per hop moves
+                        # 2(n-1)/n * S through each link, algbw <= 153.6 * n / (2(n-1)) GB/s
+                        "ring_one_link_bound": round(XGMI_LINK_GBS * n / (2 * (n - 1)), 1)})
             extras[f"fp32_1GiB_{a}"] = row
         del x0, x1, os_
     except Exception as e:
