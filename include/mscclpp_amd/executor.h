@@ -38,6 +38,8 @@ enum {
   MSCCLPP_AMD_DT_FLOAT8_E4M3FNUZ = 6, /* not native on gfx950: rejected, as the reference does */
   MSCCLPP_AMD_DT_FLOAT8_E5M2 = 7,     /* OCP */
   MSCCLPP_AMD_DT_FLOAT8_E5M2FNUZ = 8, /* not native on gfx950: rejected */
+  MSCCLPP_AMD_DT_UINT8 = 9,
+  MSCCLPP_AMD_DT_FLOAT8_E4M3B15 = 10, /* software fp8, bias 15 (execution_kernel.hpp:997-1007) */
 };
 /* mscclpp::PacketType (executor.hpp:15-18) */
 enum { MSCCLPP_AMD_PACKET_LL8 = 0, MSCCLPP_AMD_PACKET_LL16 = 1 };

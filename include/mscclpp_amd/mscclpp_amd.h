@@ -43,7 +43,15 @@ enum {
   MSCCLPP_AMD_E5M2_ACC_F16 = 8,
   MSCCLPP_AMD_E4M3_ACC_F32 = 9,
   MSCCLPP_AMD_E5M2_ACC_F32 = 10,
-  MSCCLPP_AMD_NUM_DTYPES = 11
+  /* uint8 (ncclUint8; Adapter<Op, uint8_t, uint8_t>, common.hpp:132-133): wrapping add / unsigned
+   * min per byte (gpu_data_types.hpp:577-640) */
+  MSCCLPP_AMD_U8 = 11,
+  /* the software float8 e4m3b15 (DataType::FLOAT8_E4M3B15, gpu_data_types.hpp:78-155; no NCCL
+   * dtype): accumulated in itself, half or float, as the OCP codes above */
+  MSCCLPP_AMD_E4M3B15 = 12,
+  MSCCLPP_AMD_E4M3B15_ACC_F16 = 13,
+  MSCCLPP_AMD_E4M3B15_ACC_F32 = 14,
+  MSCCLPP_AMD_NUM_DTYPES = 15
 };
 enum { MSCCLPP_AMD_SUM = 0, MSCCLPP_AMD_MIN = 1 };
 

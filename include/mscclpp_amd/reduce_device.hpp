@@ -15,20 +15,27 @@
 
 namespace mscclpp_amd {
 
-// Reduce types.  0..4 accumulate in the element type.  The FP8 codes (OCP e4m3 / e5m2, the
-// gfx950 hardware formats) carry the accumulation type of calVectorAccum<T, AccumT, Op>
-// (reduce_kernel.hpp:171-189, dispatchFp8Accum common.hpp:89-100): T, half or float.
+// Reduce types.  0..4 and 11 accumulate in the element type.  The FP8 codes (OCP e4m3 / e5m2, the
+// gfx950 hardware formats, and the software e4m3b15) carry the accumulation type of
+// calVectorAccum<T, AccumT, Op> (reduce_kernel.hpp:171-189, dispatchFp8Accum common.hpp:89-100):
+// T, half or float.  The dispatch of dispatchByDtype (common.hpp:103-135) on gfx950 is complete with
+// these: fp16, fp32, bf16, OCP e4m3 / e5m2, e4m3b15, int32 / uint32, uint8.
 enum DType : int {
   kF16 = 0, kBF16 = 1, kF32 = 2, kI32 = 3, kU32 = 4,
   kE4M3 = 5, kE5M2 = 6,              // AccumT = T
   kE4M3AccF16 = 7, kE5M2AccF16 = 8,  // AccumT = half
-  kE4M3AccF32 = 9, kE5M2AccF32 = 10  // AccumT = float
+  kE4M3AccF32 = 9, kE5M2AccF32 = 10, // AccumT = float
+  kU8 = 11,                          // uint8_t (Adapter<Op, uint8_t, uint8_t>, common.hpp:132-133)
+  kB15 = 12, kB15AccF16 = 13, kB15AccF32 = 14  // __fp8_e4m3b15, AccumT = T / half / float
 };
 enum ROp : int { kSum = 0, kMin = 1 };
 
-__host__ __device__ constexpr bool is_fp8(int dt) { return dt >= kE4M3 && dt <= kE5M2AccF32; }
+__host__ __device__ constexpr bool is_fp8(int dt) { return dt >= kE4M3 && dt <= kE5M2AccF32; }  // OCP, hardware
+__host__ __device__ constexpr bool is_b15(int dt) { return dt >= kB15 && dt <= kB15AccF32; }
 __host__ __device__ constexpr bool is_e5m2(int dt) { return dt == kE5M2 || dt == kE5M2AccF16 || dt == kE5M2AccF32; }
-__host__ __device__ constexpr int elem_bytes(int dt) { return (dt == kF16 || dt == kBF16) ? 2 : (is_fp8(dt) ? 1 : 4); }
+__host__ __device__ constexpr int elem_bytes(int dt) {
+  return (dt == kF16 || dt == kBF16) ? 2 : ((is_fp8(dt) || is_b15(dt) || dt == kU8) ? 1 : 4);
+}
 
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef float float2_t __attribute__((ext_vector_type(2)));
@@ -166,9 +173,69 @@ __device__ __forceinline__ uint32_t fp8x4_reduce(uint32_t a, uint32_t b) {
   }
 }
 
+// ---- uint8 (gpu_data_types.hpp:577-589, :622-640): four lanes per word, wrapping add and
+// unsigned min per byte -------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t u8x4_add(uint32_t a, uint32_t b) {
+  constexpr uint32_t even = 0x00ff00ffu;
+  return (((a & even) + (b & even)) & even) | (((a & ~even) + (b & ~even)) & ~even);
+}
+__device__ __forceinline__ uint32_t u8x4_min(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 32; k += 8) {
+    const uint32_t x = (a >> k) & 0xffu, y = (b >> k) & 0xffu;
+    r |= (x < y ? x : y) << k;
+  }
+  return r;
+}
+
+// ---- e4m3b15: software fp8, bias 15, no inf / NaN (gpu_data_types.hpp:78-155, 1008-1300) --------
+// decode: the fp16 bits sign | (byte & 0x7f) << 7 (exponent E4 -> E5, same bias), exact;
+// encode from fp16 h: |h| clamped to 0x3f80 (1.875), then (|h| * 2 + 0x80) >> 8 with h's sign --
+// a round-half-up of the three kept mantissa bits; from float: RNE to fp16 first (fromFloat).
+// The gfx950 build takes the reference's generic branches (its packed paths are gfx942 / CUDA):
+//   T == AccumT:  a + b = enc(dec(a) + dec(b)) in float; min = enc(fminf(dec(a), dec(b)))
+//   AccumT half:  up = dec as fp16, plain __half add / (a < b ? a : b), down = enc(half)
+//   AccumT float: up = dec, float add / (a < b ? a : b), down = enc(float)
+__device__ __forceinline__ uint32_t b15_to_h16(uint32_t b) { return ((b & 0x80u) << 8) | ((b & 0x7fu) << 7); }
+__device__ __forceinline__ uint32_t b15_from_h16(uint32_t h) {
+  uint32_t a = h & 0x7fffu;
+  a = a < 0x3f80u ? a : 0x3f80u;
+  return (((a * 2u + 0x80u) | (h & 0x8000u)) >> 8) & 0xffu;
+}
+__device__ __forceinline__ half4_t b15x4_to_half4(uint32_t w) {
+  return half4_t{__builtin_bit_cast(_Float16, (uint16_t)b15_to_h16(w & 0xffu)),
+                 __builtin_bit_cast(_Float16, (uint16_t)b15_to_h16((w >> 8) & 0xffu)),
+                 __builtin_bit_cast(_Float16, (uint16_t)b15_to_h16((w >> 16) & 0xffu)),
+                 __builtin_bit_cast(_Float16, (uint16_t)b15_to_h16(w >> 24))};
+}
+__device__ __forceinline__ float4_t b15x4_decode(uint32_t w) {
+  const half4_t h = b15x4_to_half4(w);
+  return float4_t{(float)h.x, (float)h.y, (float)h.z, (float)h.w};
+}
+__device__ __forceinline__ uint32_t b15x4_from_half4(half4_t h) {
+  // Bit-cast the whole vector: this clang (roc-7.2.0) lowers __builtin_bit_cast of an
+  // ext_vector element lvalue (h.y, h.z, h.w) to a read of element 0.
+  const u32x2 p = __builtin_bit_cast(u32x2, h);
+  return b15_from_h16(p.x & 0xffffu) | (b15_from_h16(p.x >> 16) << 8) | (b15_from_h16(p.y & 0xffffu) << 16) |
+         (b15_from_h16(p.y >> 16) << 24);
+}
+__device__ __forceinline__ uint32_t b15x4_encode(float4_t f) {  // float -> fp16 RNE -> e4m3b15
+  return b15x4_from_half4(half4_t{(_Float16)f.x, (_Float16)f.y, (_Float16)f.z, (_Float16)f.w});
+}
+template <int OP>
+__device__ __forceinline__ uint32_t b15x4_reduce(uint32_t a, uint32_t b) {
+  const float4_t x = b15x4_decode(a), y = b15x4_decode(b);
+  if constexpr (OP == kMin)
+    return b15x4_encode(float4_t{fminf(x.x, y.x), fminf(x.y, y.y), fminf(x.z, y.z), fminf(x.w, y.w)});
+  return b15x4_encode(x + y);
+}
+
 // Word accumulator: up(word) -> acc; add(acc, word) -> acc; down(acc) -> word.
 template <int DT, int OP, int KIND = (DT == kE4M3AccF16 || DT == kE5M2AccF16) ? 1
-                                     : ((DT == kE4M3AccF32 || DT == kE5M2AccF32) ? 2 : 0)>
+                                     : (DT == kE4M3AccF32 || DT == kE5M2AccF32) ? 2
+                                     : DT == kB15AccF16 ? 3
+                                     : DT == kB15AccF32 ? 4 : 0>
 struct AccWord;
 
 template <int DT, int OP>
@@ -201,6 +268,23 @@ struct AccWord<DT, OP, 2> {  // AccumT == float
   static __device__ __forceinline__ uint32_t down(W a) { return fp8x4_encode<is_e5m2(DT)>(a); }
 };
 
+template <int DT, int OP>
+struct AccWord<DT, OP, 3> {  // e4m3b15, AccumT == half
+  static constexpr bool kWide = true;
+  typedef half4_t W;
+  static __device__ __forceinline__ W up(uint32_t w) { return b15x4_to_half4(w); }
+  static __device__ __forceinline__ W add(W a, uint32_t w) { return acc_op<OP>(a, b15x4_to_half4(w)); }
+  static __device__ __forceinline__ uint32_t down(W a) { return b15x4_from_half4(a); }
+};
+template <int DT, int OP>
+struct AccWord<DT, OP, 4> {  // e4m3b15, AccumT == float
+  static constexpr bool kWide = true;
+  typedef float4_t W;
+  static __device__ __forceinline__ W up(uint32_t w) { return b15x4_decode(w); }
+  static __device__ __forceinline__ W add(W a, uint32_t w) { return acc_op<OP>(a, b15x4_decode(w)); }
+  static __device__ __forceinline__ uint32_t down(W a) { return b15x4_encode(a); }
+};
+
 // N-word accumulator over a u32x2 / u32x4 payload (the order of add() calls is the sum order).
 template <int DT, int OP, int N>
 struct Accum {
@@ -229,7 +313,11 @@ template <int DT, int OP>
 __device__ __forceinline__ uint32_t reduce_word(uint32_t acc, uint32_t val) {
   if constexpr (DT == kE4M3 || DT == kE5M2) {
     return fp8x4_reduce<DT == kE5M2, OP>(acc, val);
-  } else if constexpr (is_fp8(DT)) {
+  } else if constexpr (DT == kB15) {
+    return b15x4_reduce<OP>(acc, val);
+  } else if constexpr (DT == kU8) {
+    return OP == kSum ? u8x4_add(acc, val) : u8x4_min(acc, val);
+  } else if constexpr (is_fp8(DT) || is_b15(DT)) {
     // one accumulation step of calVectorAccum<T, AccumT>: down(up(acc) (op) up(val))
     typedef AccWord<DT, OP> A;
     return A::down(A::add(A::up(acc), val));
@@ -288,7 +376,8 @@ __device__ __forceinline__ u32x4 reduce4(u32x4 a, u32x4 b) {
   case DT * 2 + kSum: FN<DT, kSum>(__VA_ARGS__); break;     \
   case DT * 2 + kMin: FN<DT, kMin>(__VA_ARGS__); break;
 
-// As MSCCLPP_AMD_DISPATCH, plus the FP8 reduce types (dispatchFp8Accum, common.hpp:89-100).
+// As MSCCLPP_AMD_DISPATCH, plus the 1-byte reduce types: OCP FP8 and e4m3b15 with their
+// accumulation types (dispatchFp8Accum, common.hpp:89-100) and uint8.
 #define MSCCLPP_AMD_DISPATCH_ALL(dtype, op, FN, ...)     \
   switch ((dtype) * 2 + (op)) {                          \
     MSCCLPP_AMD_CASE2(kF16, FN, __VA_ARGS__)             \
@@ -302,6 +391,10 @@ __device__ __forceinline__ u32x4 reduce4(u32x4 a, u32x4 b) {
     MSCCLPP_AMD_CASE2(kE5M2AccF16, FN, __VA_ARGS__)      \
     MSCCLPP_AMD_CASE2(kE4M3AccF32, FN, __VA_ARGS__)      \
     MSCCLPP_AMD_CASE2(kE5M2AccF32, FN, __VA_ARGS__)      \
+    MSCCLPP_AMD_CASE2(kU8, FN, __VA_ARGS__)              \
+    MSCCLPP_AMD_CASE2(kB15, FN, __VA_ARGS__)             \
+    MSCCLPP_AMD_CASE2(kB15AccF16, FN, __VA_ARGS__)       \
+    MSCCLPP_AMD_CASE2(kB15AccF32, FN, __VA_ARGS__)       \
     default: return 4; /* invalid argument */            \
   }
 

@@ -20,6 +20,9 @@ LIB_PATH = os.path.join(_HERE, "lib", "libmscclpp_amd.so")
 F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
 # OCP fp8 reduce types: element type x accumulation type (Algorithm::execute accumDtype)
 E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32 = 5, 6, 7, 8, 9, 10
+# uint8, and the software fp8 e4m3b15 accumulated in itself / half / float (no torch dtype: pass
+# uint8 tensors with accum=E4M3B15..., an explicit reduce-type code)
+U8, E4M3B15, E4M3B15_ACC_F16, E4M3B15_ACC_F32 = 11, 12, 13, 14
 SUM, MIN = 0, 1
 ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC, ALGO_RSAG_PIPELINE = 0, 1, 2, 3, 4, 5, 6
 ALGO_TEST_K5, ALGO_TEST_K6, ALGO_TEST_K7 = 105, 106, 107  # mscclpp-test allreduce5 / 6 / 7 (int32)
@@ -30,10 +33,10 @@ FLAG_SLOTS = 4096
 MAX_CHANNELS = 256
 
 # ncclDataType_t / ncclRedOp_t (include/mscclpp_amd/nccl.h, values of the reference nccl.h:217-253)
-NCCL_DTYPES = {torch.float16: 6, torch.bfloat16: 9, torch.float32: 7, torch.int32: 2,
+NCCL_DTYPES = {torch.float16: 6, torch.bfloat16: 9, torch.float32: 7, torch.int32: 2, torch.uint8: 1,
                torch.float8_e4m3fn: 10, torch.float8_e5m2: 11}
 NCCL_OPS = {"sum": 0, "min": 3}
-DTYPE_CODES = {torch.float16: F16, torch.bfloat16: BF16, torch.float32: F32, torch.int32: I32,
+DTYPE_CODES = {torch.float16: F16, torch.bfloat16: BF16, torch.float32: F32, torch.int32: I32, torch.uint8: U8,
                torch.float8_e4m3fn: E4M3, torch.float8_e5m2: E5M2}
 # accumulation dtype (ncclDataType_t) -> reduce-type code, for fp8 buffers
 ACCUM_CODES = {(torch.float8_e4m3fn, torch.float16): E4M3_ACC_F16, (torch.float8_e5m2, torch.float16): E5M2_ACC_F16,
@@ -41,7 +44,10 @@ ACCUM_CODES = {(torch.float8_e4m3fn, torch.float16): E4M3_ACC_F16, (torch.float8
 
 
 def reduce_code(dtype, accum=None):
-    """Reduce-type code of a buffer dtype accumulated in `accum` (None: the element type)."""
+    """Reduce-type code of a buffer dtype accumulated in `accum` (None: the element type; an int:
+    that reduce-type code itself, e.g. E4M3B15_ACC_F32 over a uint8 buffer)."""
+    if isinstance(accum, int):
+        return accum
     if accum is None or accum == dtype:
         return DTYPE_CODES[dtype]
     return ACCUM_CODES[(dtype, accum)]
@@ -585,12 +591,13 @@ class DataType:
     """mscclpp.DataType values (gpu_data_types.hpp:169-183)."""
     int32, uint32, float16, float32, bfloat16 = 0, 1, 2, 3, 4
     float8_e4m3fn, float8_e4m3fnuz, float8_e5m2, float8_e5m2fnuz = 5, 6, 7, 8
+    uint8, float8_e4m3b15 = 9, 10  # e4m3b15 has no torch dtype: pass it explicitly over a uint8 buffer
 
 
 EXEC_DTYPES = {torch.int32: DataType.int32, torch.float16: DataType.float16, torch.float32: DataType.float32,
                torch.bfloat16: DataType.bfloat16, torch.float8_e4m3fn: DataType.float8_e4m3fn,
                torch.float8_e5m2: DataType.float8_e5m2, torch.float8_e4m3fnuz: DataType.float8_e4m3fnuz,
-               torch.float8_e5m2fnuz: DataType.float8_e5m2fnuz}
+               torch.float8_e5m2fnuz: DataType.float8_e5m2fnuz, torch.uint8: DataType.uint8}
 
 
 class PacketType:

@@ -48,7 +48,13 @@ static int reduceTypeOf(DataType dt, DataType accum) {
              : accum == DataType::FLOAT16 ? MSCCLPP_AMD_E5M2_ACC_F16
              : accum == DataType::FLOAT32 ? MSCCLPP_AMD_E5M2_ACC_F32
                                           : -1;
-    default: return -1;  // FNUZ / e4m3b15 have no gfx950 hardware conversion
+    case DataType::UINT8: return accum == dt ? MSCCLPP_AMD_U8 : -1;
+    case DataType::FLOAT8_E4M3B15:  // software on every platform (gpu_data_types.hpp:78-155)
+      return accum == dt                  ? MSCCLPP_AMD_E4M3B15
+             : accum == DataType::FLOAT16 ? MSCCLPP_AMD_E4M3B15_ACC_F16
+             : accum == DataType::FLOAT32 ? MSCCLPP_AMD_E4M3B15_ACC_F32
+                                          : -1;
+    default: return -1;  // FNUZ: the reference's gfx950 build has no FNUZ kernels either (common.hpp:110-126)
   }
 }
 
@@ -146,9 +152,7 @@ CommResult DslAlgorithm::execute(std::shared_ptr<Communicator> comm, const void*
                                  std::shared_ptr<Executor> executor, int, int, bool,
                                  const std::unordered_map<std::string, uintptr_t>&, DataType) {
   if (!executor) throw std::logic_error("Executor is null in DslAlgorithm::execute");  // algorithm.cc:178-180
-  if (dtype != DataType::FLOAT16 && dtype != DataType::FLOAT32 && dtype != DataType::BFLOAT16 &&
-      dtype != DataType::INT32 && dtype != DataType::UINT32)
-    return CommResult::CommInvalidArgument;
+  if (dtype == DataType::AUTO) return CommResult::CommInvalidArgument;  // the executor checks the rest
   return executor->execute(comm->rank(), const_cast<void*>(input), output, inputSize, outputSize, dtype, *plan_,
                            stream);
 }

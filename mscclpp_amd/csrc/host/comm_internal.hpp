@@ -152,6 +152,7 @@ inline int dtypeFromNccl(ncclDataType_t t) {
     case ncclUint32: return MSCCLPP_AMD_U32;
     case ncclFloat8e4m3: return MSCCLPP_AMD_E4M3;  // OCP on gfx950 (datatype_conversion.hpp:29-40)
     case ncclFloat8e5m2: return MSCCLPP_AMD_E5M2;
+    case ncclUint8: return MSCCLPP_AMD_U8;  // datatype_conversion.hpp:21-22
     default: return -1;
   }
 }

@@ -592,6 +592,8 @@ struct mscclppAmdExecutor {
       // (:952-960, :975-983), rejects FNUZ
       case MSCCLPP_AMD_DT_FLOAT8_E4M3FN: dt = MSCCLPP_AMD_E4M3; break;
       case MSCCLPP_AMD_DT_FLOAT8_E5M2: dt = MSCCLPP_AMD_E5M2; break;
+      case MSCCLPP_AMD_DT_FLOAT8_E4M3B15: dt = MSCCLPP_AMD_E4M3B15; break;  // execution_kernel.hpp:997-1007
+      case MSCCLPP_AMD_DT_UINT8: dt = MSCCLPP_AMD_U8; break;                 // :1008-1018
       case MSCCLPP_AMD_DT_FLOAT8_E4M3FNUZ:
       case MSCCLPP_AMD_DT_FLOAT8_E5M2FNUZ:
         warn("execution plan: FNUZ fp8 is not natively supported on gfx950; use the OCP FLOAT8_E4M3FN / FLOAT8_E5M2");

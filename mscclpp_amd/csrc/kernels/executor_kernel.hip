@@ -596,6 +596,8 @@ int launchExecutionKernel(const exec::TbPlan* plans, int nblocks, int nthreads, 
     MSCCLPP_AMD_EXEC_CASE(kU32)
     MSCCLPP_AMD_EXEC_CASE(kE4M3)
     MSCCLPP_AMD_EXEC_CASE(kE5M2)
+    MSCCLPP_AMD_EXEC_CASE(kB15)
+    MSCCLPP_AMD_EXEC_CASE(kU8)
     default: return 4;
   }
 #undef MSCCLPP_AMD_EXEC_CASE

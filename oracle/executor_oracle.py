@@ -35,7 +35,8 @@ OPS = {"nop", "barrier", "put", "pws", "pwsf", "get", "copy", "signal", "wait", 
 BUF = {"i": 0, "o": 1, "s": 2}
 PREDEFINED_SCRATCH = 1 << 26
 DEFAULT_REUSE_SCRATCH = 1 << 27
-DT_CODES = {"i32": 3, "u32": 4, "f16": 0, "f32": 2, "bf16": 1, "e4m3": 5, "e5m2": 6}  # oracle dtype codes
+DT_CODES = {"i32": 3, "u32": 4, "f16": 0, "f32": 2, "bf16": 1, "e4m3": 5, "e5m2": 6,  # oracle dtype codes
+            "u8": 11, "b15": 12}  # e4m3b15 in the executor: T == AccumT (execution_kernel.hpp:997-1007)
 
 
 def _lib():

@@ -27,16 +27,21 @@ enum { ORC_F16 = 0, ORC_BF16 = 1, ORC_F32 = 2, ORC_I32 = 3, ORC_U32 = 4 };
  * (calVectorAccum<T, AccumT>, src/core/include/reduce_kernel.hpp:139-189; common.hpp:89-100). */
 enum { ORC_E4M3 = 5, ORC_E5M2 = 6, ORC_E4M3_ACC_F16 = 7, ORC_E5M2_ACC_F16 = 8, ORC_E4M3_ACC_F32 = 9,
        ORC_E5M2_ACC_F32 = 10 };
+/* uint8 (Adapter<Op, uint8_t, uint8_t>, common.hpp:132-133) and the software fp8 e4m3b15
+ * accumulated in itself, half or float (dispatchFp8Accum, common.hpp:89-100, :128-129). */
+enum { ORC_U8 = 11, ORC_B15 = 12, ORC_B15_ACC_F16 = 13, ORC_B15_ACC_F32 = 14 };
 enum { ORC_SUM = 0, ORC_MIN = 1 };
 
 static int orc_is_fp8(int dt) { return dt >= ORC_E4M3 && dt <= ORC_E5M2_ACC_F32; }
+static int orc_is_b15(int dt) { return dt >= ORC_B15 && dt <= ORC_B15_ACC_F32; }
+static int orc_is_byte(int dt) { return orc_is_fp8(dt) || orc_is_b15(dt) || dt == ORC_U8; }
 static int orc_is_e5m2(int dt) { return dt == ORC_E5M2 || dt == ORC_E5M2_ACC_F16 || dt == ORC_E5M2_ACC_F32; }
 static int orc_acc_kind(int dt) {
-  if (dt == ORC_E4M3_ACC_F16 || dt == ORC_E5M2_ACC_F16) return 1;
-  if (dt == ORC_E4M3_ACC_F32 || dt == ORC_E5M2_ACC_F32) return 2;
+  if (dt == ORC_E4M3_ACC_F16 || dt == ORC_E5M2_ACC_F16 || dt == ORC_B15_ACC_F16) return 1;
+  if (dt == ORC_E4M3_ACC_F32 || dt == ORC_E5M2_ACC_F32 || dt == ORC_B15_ACC_F32) return 2;
   return 0;
 }
-static int orc_elem_bytes(int dt) { return (dt == ORC_F16 || dt == ORC_BF16) ? 2 : (orc_is_fp8(dt) ? 1 : 4); }
+static int orc_elem_bytes(int dt) { return (dt == ORC_F16 || dt == ORC_BF16) ? 2 : (orc_is_byte(dt) ? 1 : 4); }
 
 /* 32-bit words the LL kernels cover: (count*sizeof(T)+sizeof(T))/4 for 1- and 2-byte T
  * (allreduce_packet.cu:51-54, allreduce_allpair_packet.cu:20).  Deviation: 1-byte T
@@ -276,9 +281,75 @@ static uint8_t fp8_reduce_same(uint8_t a, uint8_t b, int e5m2, int op) {
   return fp8_encode_sat(f, 1);
 }
 
-/* dst[i] = down(up(src[0][i]) (op) up(src[1][i]) (op) ...) for fp8 reduce types, nsrc sources in
- * sum order, over nbytes elements (calVectorAccum, reduce_kernel.hpp:171-189). */
+/* ---- e4m3b15 (gpu_data_types.hpp:78-155): software fp8, bias 15, no inf / NaN ----------------
+ * decode (toFloat, :111-125): the fp16 bits sign | (byte & 0x7f) << 7, exact.
+ * encode (fromFloat, :131-154): RNE to fp16, |h| clamped to 0x3f80 (1.875), then the upper byte of
+ * (|h| * 2 + 0x80) with h's sign: the three kept mantissa bits rounded half up.  The gfx950 build
+ * takes the generic branches of the vector conversions (:1016-1265), which reduce to these two. */
+static uint16_t b15_to_h16(uint8_t b) { return (uint16_t)(((b & 0x80u) << 8) | ((b & 0x7fu) << 7)); }
+static float b15_decode(uint8_t b) { return half_to_float(b15_to_h16(b)); }
+static uint8_t b15_from_h16(uint16_t h) {
+  uint32_t a = h & 0x7fffu;
+  if (a > 0x3f80u) a = 0x3f80u;
+  return (uint8_t)((((a * 2u + 0x80u) | (h & 0x8000u)) >> 8) & 0xffu);
+}
+static uint8_t b15_encode(float f) { return b15_from_h16(float_to_half_rne(f)); }
+uint8_t oracle_b15_encode(float f) { return b15_encode(f); }
+float oracle_b15_decode(uint8_t b) { return b15_decode(b); }
+
+/* T == AccumT (:1269-1300): a + b = enc(dec(a) + dec(b)); min = enc(fminf(dec(a), dec(b))) */
+static uint8_t b15_reduce_same(uint8_t a, uint8_t b, int op) {
+  float x = b15_decode(a), y = b15_decode(b);
+  return b15_encode(op == ORC_MIN ? fminf_dev(x, y) : x + y);
+}
+
+/* uint8 (gpu_data_types.hpp:577-589, :622-640): wrapping add, unsigned min */
+static uint8_t u8_reduce(uint8_t a, uint8_t b, int op) {
+  if (op == ORC_SUM) return (uint8_t)(a + b);
+  return a < b ? a : b;
+}
+
+static void b15_reduce_seq(int dt, int op, int nsrc, const uint8_t* const* src, size_t nbytes, uint8_t* dst) {
+  int kind = orc_acc_kind(dt);
+  for (size_t i = 0; i < nbytes; i++) {
+    if (kind == 0) {
+      uint8_t a = src[0][i];
+      for (int k = 1; k < nsrc; k++) a = b15_reduce_same(a, src[k][i], op);
+      dst[i] = a;
+    } else if (kind == 2) { /* AccumT float: up = dec, float add / (a < v ? a : v), down = enc */
+      float a = b15_decode(src[0][i]);
+      for (int k = 1; k < nsrc; k++) {
+        float v = b15_decode(src[k][i]);
+        a = (op == ORC_SUM) ? a + v : (a < v ? a : v);
+      }
+      dst[i] = b15_encode(a);
+    } else { /* AccumT half: up = the exact fp16 image, __half add / compare, down = enc(half) */
+      uint16_t a = b15_to_h16(src[0][i]);
+      for (int k = 1; k < nsrc; k++) {
+        uint16_t v = b15_to_h16(src[k][i]);
+        a = (op == ORC_SUM) ? half_add_noclip(a, v) : half_lt_min(a, v);
+      }
+      dst[i] = b15_from_h16(a);
+    }
+  }
+}
+
+/* dst[i] = down(up(src[0][i]) (op) up(src[1][i]) (op) ...) for the 1-byte reduce types (OCP fp8,
+ * e4m3b15, uint8), nsrc sources in sum order, over nbytes elements (calVectorAccum,
+ * reduce_kernel.hpp:171-189). */
 static void fp8_reduce_seq(int dt, int op, int nsrc, const uint8_t* const* src, size_t nbytes, uint8_t* dst) {
+  if (orc_is_b15(dt)) {
+    b15_reduce_seq(dt, op, nsrc, src, nbytes, dst);
+    return;
+  }
+  if (dt == ORC_U8) {
+    for (size_t i = 0; i < nbytes; i++) {
+      uint8_t a = src[0][i];
+      for (int k = 1; k < nsrc; k++) a = u8_reduce(a, src[k][i], op);
+      dst[i] = a;
+    }
+    return;
+  }
   int e5 = orc_is_e5m2(dt), kind = orc_acc_kind(dt);
   for (size_t i = 0; i < nbytes; i++) {
     if (kind == 0) {
@@ -305,7 +376,7 @@ static void fp8_reduce_seq(int dt, int op, int nsrc, const uint8_t* const* src, 
 
 /* calVectorAccum<T,T,Op> over one 32-bit word (reduce_kernel.hpp:86-134, 171-175). */
 static uint32_t reduce_word(int dtype, int op, uint32_t acc, uint32_t val) {
-  if (orc_is_fp8(dtype)) { /* one accumulation step: down(up(acc) (op) up(val)) per byte */
+  if (orc_is_byte(dtype)) { /* one accumulation step: down(up(acc) (op) up(val)) per byte */
     uint8_t a[4], v[4], r[4];
     const uint8_t* s[2] = {a, v};
     memcpy(a, &acc, 4);
@@ -349,7 +420,7 @@ void oracle_reduce_words(int dtype, int op, uint32_t* acc, const uint32_t* val, 
  * type's AccumT (upcastVector / calVectorAccum / downcastVector, reduce_kernel.hpp:139-189).
  * dst may alias src[0]. */
 void oracle_reduce_seq(int dtype, int op, int nsrc, const uint32_t* const* src, size_t nwords, uint32_t* dst) {
-  if (orc_is_fp8(dtype)) {
+  if (orc_is_byte(dtype)) {
     fp8_reduce_seq(dtype, op, nsrc, (const uint8_t* const*)src, nwords * 4, (uint8_t*)dst);
     return;
   }
@@ -630,6 +701,10 @@ void oracle_lcg_fill(int dtype, uint64_t count, int rank, int seq, void* dst) {
       ((uint32_t*)dst)[i] = f2u(v);
     else if (orc_is_fp8(dtype))
       ((uint8_t*)dst)[i] = fp8_encode_sat(v, orc_is_e5m2(dtype));
+    else if (orc_is_b15(dtype))
+      ((uint8_t*)dst)[i] = b15_encode(v);
+    else if (dtype == ORC_U8)
+      ((uint8_t*)dst)[i] = (uint8_t)(s % 4096 >> 4);
     else
       ((uint32_t*)dst)[i] = (uint32_t)(int32_t)(v * 2147483647.0f);
   }

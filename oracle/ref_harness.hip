@@ -71,6 +71,12 @@ template <> struct RefFp8<7> { using T = __fp8_e4m3; using A = __half; };
 template <> struct RefFp8<8> { using T = __fp8_e5m2; using A = __half; };
 template <> struct RefFp8<9> { using T = __fp8_e4m3; using A = float; };
 template <> struct RefFp8<10> { using T = __fp8_e5m2; using A = float; };
+// uint8 (u8x4 operator+ / min, gpu_data_types.hpp:577-640) and the software e4m3b15
+// (f8_e4m3b15x4 operator+ / min and its to<> conversions, :1008-1300), as dispatchByDtype pairs them
+template <> struct RefFp8<11> { using T = uint8_t; using A = uint8_t; };
+template <> struct RefFp8<12> { using T = __fp8_e4m3b15; using A = __fp8_e4m3b15; };
+template <> struct RefFp8<13> { using T = __fp8_e4m3b15; using A = __half; };
+template <> struct RefFp8<14> { using T = __fp8_e4m3b15; using A = float; };
 
 template <int DT, int OP>
 __global__ void refFp8AccumKernel(const uint32_t* src, int nsrc, size_t n, uint32_t* out) {
@@ -115,6 +121,27 @@ __global__ void refFp8ConvertKernel(const float* in, size_t n, uint8_t* e4, uint
   }
 }
 
+// e4m3b15 conversions of the reference, every path of its unit test (gpu_data_types_tests.cu:37-92):
+// encode by __fp8_e4m3b15(float) and by to<f8_e4m3b15x4>(f32x4); decode by float() and to<f32x4>.
+__global__ void refB15ConvertKernel(const float* in, size_t n, uint8_t* enc, uint8_t* encX4, float* dec,
+                                    float* decX4) {
+  const size_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) enc[i] = __fp8_e4m3b15(in[i]).__x;
+  if (i * 4 + 3 < n) {
+    mscclpp::f32x4 v;
+    for (int k = 0; k < 4; ++k) v.data[k] = in[i * 4 + k];
+    const mscclpp::f8_e4m3b15x4 e = mscclpp::to<mscclpp::f8_e4m3b15x4>(v);
+    for (int k = 0; k < 4; ++k) encX4[i * 4 + k] = e.data[k].__x;
+  }
+  if (i < 256) dec[i] = float(__fp8_e4m3b15::fromRaw((uint8_t)i));
+  if (i < 64) {
+    mscclpp::f8_e4m3b15x4 r;
+    for (int k = 0; k < 4; ++k) r.data[k] = __fp8_e4m3b15::fromRaw((uint8_t)(i * 4 + k));
+    const mscclpp::f32x4 f = mscclpp::to<mscclpp::f32x4>(r);
+    for (int k = 0; k < 4; ++k) decX4[i * 4 + k] = f.data[k];
+  }
+}
+
 #define REF_DISPATCH(dtype, op, KERNEL, ...)                                         \
   do {                                                                               \
     int key = (dtype) * 2 + (op);                                                    \
@@ -154,14 +181,16 @@ int refSelfReduceLL16(int dtype, int op, const void* x, const void* y, void* pkt
 }
 
 // dst = src[0] (op) ... (op) src[nsrc-1] (src: nsrc arrays of nwords words, back to back), fp8
-// reduce type dtype 5..10 (element e4m3/e5m2 x AccumT element/half/float).
+// reduce type dtype 5..10 (element e4m3/e5m2 x AccumT element/half/float), 11 (uint8) or 12..14
+// (e4m3b15 x AccumT element/half/float).
 int refFp8Accum(int dtype, int op, const uint32_t* src, int nsrc, size_t nwords, uint32_t* out, void* stream) {
   const int key = dtype * 2 + op;
   hipStream_t s = (hipStream_t)stream;
 #define REF_FP8(D)                                                                                          \
   if (key == D * 2) hipLaunchKernelGGL((refFp8AccumKernel<D, 0>), dim3(256), dim3(256), 0, s, src, nsrc, nwords, out); \
   else if (key == D * 2 + 1) hipLaunchKernelGGL((refFp8AccumKernel<D, 1>), dim3(256), dim3(256), 0, s, src, nsrc, nwords, out);
-  REF_FP8(5) else REF_FP8(6) else REF_FP8(7) else REF_FP8(8) else REF_FP8(9) else REF_FP8(10) else return 4;
+  REF_FP8(5) else REF_FP8(6) else REF_FP8(7) else REF_FP8(8) else REF_FP8(9) else REF_FP8(10)
+  else REF_FP8(11) else REF_FP8(12) else REF_FP8(13) else REF_FP8(14) else return 4;
 #undef REF_FP8
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
@@ -170,6 +199,14 @@ int refFp8Convert(const float* in, size_t n, uint8_t* e4, uint8_t* e5, float* d4
   const size_t threads = n > 256 ? n : 256;
   hipLaunchKernelGGL(refFp8ConvertKernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream, in, n, e4, e5,
                      d4, d5);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// n floats -> enc[n] (scalar) and encX4[n] (x4 path, n % 4 == 0); dec[256] / decX4[256] of every byte
+int refB15Convert(const float* in, size_t n, uint8_t* enc, uint8_t* encX4, float* dec, float* decX4, void* stream) {
+  const size_t threads = n > 256 ? n : 256;
+  hipLaunchKernelGGL(refB15ConvertKernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream, in, n, enc,
+                     encX4, dec, decX4);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

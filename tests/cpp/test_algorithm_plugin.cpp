@@ -10,6 +10,8 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cmath>
+#include <memory>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -204,6 +206,62 @@ struct UserAllgatherBuilder : AlgorithmBuilder {
   }
 };
 
+// e4m3b15 (gpu_data_types.hpp:78-155): sign, 4-bit exponent with bias 15, 3-bit mantissa, no inf/NaN
+static double b15Value(int b) {
+  const int e = (b >> 3) & 0xf, m = b & 7;
+  const double v = e == 0 ? std::ldexp(m / 8.0, -14) : std::ldexp(1.0 + m / 8.0, e - 15);
+  return (b & 0x80) ? -v : v;
+}
+static int b15Exact(double v) {  // the byte that holds v exactly, or -1
+  for (int b = 0; b < 256; ++b)
+    if (b15Value(b) == v && !(v == 0 && b != 0)) return b;
+  return -1;
+}
+static std::shared_ptr<Algorithm> gBuiltinPacket, gBuiltinRsag;
+
+// uint8 and e4m3b15 through the built-in algorithms' Algorithm::execute, the reference's route for
+// DataType::FLOAT8_E4M3B15 (it has no ncclDataType_t): the three accumulation forms, sums exact
+static void byteTypesThroughExecute(int rank, int n, hipStream_t s) {
+  CHECK(gBuiltinPacket && gBuiltinRsag);
+  const size_t bytes = 1 << 16;
+  uint8_t *x, *y;
+  HIP_OK(hipMalloc(&x, bytes));
+  HIP_OK(hipMalloc(&y, bytes));
+  std::vector<uint8_t> hx(bytes), hy(bytes);
+  for (auto algo : {gBuiltinPacket, gBuiltinRsag}) {
+    for (DataType acc : {DataType::AUTO, DataType::FLOAT16, DataType::FLOAT32}) {
+      for (size_t i = 0; i < bytes; ++i) hx[i] = (uint8_t)b15Exact(std::ldexp(1.0 + (i % 8) / 8.0, -5 - (int)(i % 5)));
+      HIP_OK(hipMemcpy(x, hx.data(), bytes, hipMemcpyHostToDevice));
+      CHECK(algo->execute(nullptr, x, y, bytes, bytes, DataType::FLOAT8_E4M3B15, SUM, s, nullptr, 0, 0, false, {},
+                          acc) == CommResult::CommSuccess);
+      HIP_OK(hipStreamSynchronize(s));
+      HIP_OK(hipMemcpy(hy.data(), y, bytes, hipMemcpyDeviceToHost));
+      size_t bad = 0;
+      for (size_t i = 0; i < bytes; ++i) {
+        const int want = b15Exact(n * b15Value(hx[i]));  // n * (1 + m/8) 2^-k: exact for n = 1, 2, 4, 8
+        if (want >= 0 && hy[i] != want) bad++;
+      }
+      if (bad) std::fprintf(stderr, "rank %d %s e4m3b15 accum %d: %zu bad\n", rank, algo->name().c_str(), (int)acc, bad);
+      CHECK(bad == 0);
+    }
+    // uint8: wrapping byte sums (allreduce_test.cu's uint8 check is the same modular sum)
+    for (size_t i = 0; i < bytes; ++i) hx[i] = (uint8_t)(rank * 97 + i * 31);
+    HIP_OK(hipMemcpy(x, hx.data(), bytes, hipMemcpyHostToDevice));
+    CHECK(algo->execute(nullptr, x, y, bytes, bytes, DataType::UINT8, SUM, s, nullptr) == CommResult::CommSuccess);
+    HIP_OK(hipStreamSynchronize(s));
+    HIP_OK(hipMemcpy(hy.data(), y, bytes, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (size_t i = 0; i < bytes; ++i) {
+      unsigned want = 0;
+      for (int r = 0; r < n; ++r) want += (uint8_t)(r * 97 + i * 31);
+      if (hy[i] != (uint8_t)want) bad++;
+    }
+    CHECK(bad == 0);
+  }
+  HIP_OK(hipFree(x));
+  HIP_OK(hipFree(y));
+}
+
 static int worker(int rank, int n, ncclUniqueId id) {
   int ndev = 0;
   HIP_OK(hipGetDeviceCount(&ndev));
@@ -213,6 +271,10 @@ static int worker(int rank, int n, ncclUniqueId id) {
   // the user selector: allgather -> the user algorithm; allreduce of exactly 3 MiB -> the built-in
   // ring-order RS+AG by name; everything else -> nullptr (the built-in fallback selector)
   builder->setAlgorithmSelector([](const AlgoMapByCollective& m, const CollectiveRequest& r) -> std::shared_ptr<Algorithm> {
+    if (r.collective == "allreduce" && !gBuiltinPacket) {
+      gBuiltinPacket = m.at("allreduce").at("default_allreduce_packet");
+      gBuiltinRsag = m.at("allreduce").at("default_allreduce_rsag");
+    }
     if (r.collective == "allgather") return m.at("allgather").at("user_allgather");
     if (r.collective == "allreduce" && r.messageSize == (3u << 20)) return m.at("allreduce").at("default_allreduce_rsag");
     return nullptr;
@@ -259,6 +321,7 @@ static int worker(int rank, int n, ncclUniqueId id) {
     HIP_OK(hipFree(x));
     HIP_OK(hipFree(y));
   }
+  byteTypesThroughExecute(rank, n, s);
   // an unsupported op comes back as an argument error, not a crash
   CHECK(ncclAllReduce(in, in, cnt, ncclInt32, ncclProd, comm, s) == ncclInvalidArgument);
   ncclResult_t async = ncclSuccess;

@@ -12,11 +12,15 @@ F16, BF16, F32, I32, U32 = 0, 1, 2, 3, 4
 # OCP fp8 reduce types: element type (e4m3 / e5m2) x accumulation type (element, half, float)
 E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32 = 5, 6, 7, 8, 9, 10
 FP8_TYPES = (E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32)
+# uint8 and the software fp8 e4m3b15 accumulated in itself / half / float
+U8, B15, B15_ACC_F16, B15_ACC_F32 = 11, 12, 13, 14
+B15_TYPES = (B15, B15_ACC_F16, B15_ACC_F32)
+BYTE_TYPES = FP8_TYPES + B15_TYPES + (U8,)
 SUM, MIN = 0, 1
 
 
 def itemsize(dtype):
-    return 2 if dtype in (F16, BF16) else (1 if dtype in FP8_TYPES else 4)
+    return 2 if dtype in (F16, BF16) else (1 if dtype in BYTE_TYPES else 4)
 
 
 def is_e5m2(dtype):
@@ -53,6 +57,8 @@ def L():
             ("oracle_reduce_seq", [i32, i32, i32, vp, sz, vp], None),
             ("oracle_fp8_encode_sat", [ctypes.c_float, i32], ctypes.c_uint8),
             ("oracle_fp8_decode", [ctypes.c_uint8, i32], ctypes.c_float),
+            ("oracle_b15_encode", [ctypes.c_float], ctypes.c_uint8),
+            ("oracle_b15_decode", [ctypes.c_uint8], ctypes.c_float),
             ("oracle_ll16_pack", [vp, sz, u32, vp], None), ("oracle_ll16_unpack", [vp, sz, u32, vp], sz),
             ("oracle_ll8_pack", [vp, sz, u32, vp], None), ("oracle_ll8_unpack", [vp, sz, u32, vp], sz),
             ("oracle_self_reduce", [i32, i32, vp, vp, sz, u32, vp, vp], sz),
@@ -209,3 +215,11 @@ def fp8_decode(b, e5m2):
 
 def fp8_encode_sat(f, e5m2):
     return int(L().oracle_fp8_encode_sat(float(f), int(e5m2)))
+
+
+def b15_encode(f):
+    return int(L().oracle_b15_encode(float(f)))
+
+
+def b15_decode(b):
+    return L().oracle_b15_decode(int(b))

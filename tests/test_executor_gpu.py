@@ -45,9 +45,14 @@ CASES_REF = [
     # OCP fp8 (execution_kernel.hpp:949-1000: the FP8 kernels, T == AccumT)
     ("ref/allreduce_packet.json", "e4m3", 1 << 16, "LL16", 2),
     ("ref/allreduce.json", "e5m2", 1 << 19, "LL16", 2),
+    # uint8 and the software e4m3b15 (execution_kernel.hpp:997-1007), the latter over a uint8 buffer
+    ("ref/allreduce_packet.json", "u8", 1 << 16, "LL16", 2),
+    ("ref/allreduce_packet.json", "b15", 1 << 16, "LL8", 2),
+    ("ref/allreduce.json", "u8", 1 << 19, "LL16", 2),
+    ("ref/allreduce.json", "b15", 1 << 19, "LL16", 2),
 ]
-DT = {"f16": 0, "bf16": 1, "f32": 2, "e4m3": 5, "e5m2": 6}
-NP_VIEW = {"f32": np.int32, "e4m3": np.uint8, "e5m2": np.uint8}  # others: 16-bit
+DT = {"f16": 0, "bf16": 1, "f32": 2, "e4m3": 5, "e5m2": 6, "u8": 11, "b15": 12}
+NP_VIEW = {"f32": np.int32, "e4m3": np.uint8, "e5m2": np.uint8, "u8": np.uint8, "b15": np.uint8}  # others: 16-bit
 
 
 def _worker(rank, n, uid, cases, q):
@@ -64,7 +69,7 @@ def _worker(rank, n, uid, cases, q):
         comm = m.Communicator(rank, n, uid)
         ex = m.Executor(comm)
         tdt = {"f16": torch.float16, "bf16": torch.bfloat16, "f32": torch.float32, "e4m3": torch.float8_e4m3fn,
-               "e5m2": torch.float8_e5m2}
+               "e5m2": torch.float8_e5m2, "u8": torch.uint8, "b15": torch.uint8}
         results = []
         for ci, (fname, dt, count, pkt, calls) in enumerate(cases):
             plan = m.ExecutionPlan(os.path.join(PLANS, fname), rank)
@@ -75,7 +80,7 @@ def _worker(rank, n, uid, cases, q):
                 y = x if plan.is_in_place() else torch.zeros_like(x)
                 stream = torch.cuda.current_stream()
                 ex.execute(rank, x.data_ptr(), y.data_ptr(), x.numel() * x.element_size(), y.numel() * y.element_size(),
-                           m.EXEC_DTYPES[tdt[dt]], plan, stream,
+                           m.DataType.float8_e4m3b15 if dt == "b15" else m.EXEC_DTYPES[tdt[dt]], plan, stream,
                            m.PacketType.LL16 if pkt == "LL16" else m.PacketType.LL8)
                 torch.cuda.synchronize()
                 outs.append(y.cpu().contiguous().view(torch.uint8).numpy().copy())
