@@ -228,6 +228,16 @@ def _u8_worker(rank, n, uid, q):
                 exp = O.reduce_seq(O.U8, o, [np.pad(a, (0, (-count) % 4)).view(np.uint32) for a in ins]).view(
                     np.uint8)[:count]  # wrapping add / min commute: one result in every order
                 res.append((count, op, int(np.count_nonzero(y.cpu().numpy() != exp))))
+        # ncclReduceScatter over uint8 (blocks of 16-byte multiples): rank r gets block r of the sum
+        blk = 1 << 18
+        ins = [np.random.default_rng(70 + r).integers(0, 256, n * blk, dtype=np.uint16).astype(np.uint8)
+               for r in range(n)]
+        x = torch.from_numpy(ins[rank].copy()).cuda()
+        y = torch.zeros(blk, dtype=torch.uint8, device="cuda")
+        comm.reduce_scatter(x, y, op="sum")
+        torch.cuda.synchronize()
+        exp = O.reduce_seq(O.U8, O.SUM, [a.view(np.uint32) for a in ins]).view(np.uint8)[rank * blk:(rank + 1) * blk]
+        res.append(("rs", "sum", int(np.count_nonzero(y.cpu().numpy() != exp))))
         err = comm.device_error()
         comm.destroy()
         q.put((rank, {"res": res, "err": err}, None))
@@ -235,7 +245,8 @@ def _u8_worker(rank, n, uid, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-def test_ncclallreduce_uint8_two_processes(built):
+def test_nccl_uint8_two_processes(built):
+    """ncclAllReduce (LL8, LL16 and bulk sizes, SUM and MIN) and ncclReduceScatter over ncclUint8."""
     import mscclpp_amd as m
 
     n = 2
