@@ -323,6 +323,15 @@ struct ncclComm {
           HIPCHECK(hipEventRecord(e.second, s));
           return;
         }
+      if (ev.size() >= 8) {  // a caller cycling through many streams: forget the uses that completed
+        size_t k = 0;
+        for (auto& e : ev) {
+          if (hipEventQuery(e.second) == hipSuccess) (void)hipEventDestroy(e.second);
+          else ev[k++] = e;
+        }
+        (void)hipGetLastError();
+        ev.resize(k);
+      }
       int cur = device;
       HIPCHECK(hipGetDevice(&cur));
       if (cur != device) HIPCHECK(hipSetDevice(device));

@@ -43,15 +43,26 @@ struct HandleKeyHash {
 };
 std::mutex gIpcMu;
 std::unordered_map<HandleKey, std::weak_ptr<void>, HandleKeyHash> gIpcOpen;
+// Handles whose mapping is being closed (the closer thread sits in hipIpcCloseMemHandle, which waits
+// for the device to go idle).  An open of the same handle meanwhile waits for that close to finish,
+// so the handle is never opened while its previous mapping is half torn down.
+std::unordered_map<HandleKey, int, HandleKeyHash> gIpcClosing;
+std::condition_variable gIpcClosed;
 }  // namespace
 
 std::shared_ptr<void> openIpcHandle(const hipIpcMemHandle_t& handle) {
-  std::lock_guard<std::mutex> lk(gIpcMu);
+  std::unique_lock<std::mutex> lk(gIpcMu);
   HandleKey key{handle};
-  auto it = gIpcOpen.find(key);
-  if (it != gIpcOpen.end()) {
-    if (auto p = it->second.lock()) return p;
-    gIpcOpen.erase(it);
+  for (;;) {
+    // An entry whose mapping has expired belongs to a deleter that has not reached its lock yet:
+    // that is a close in progress too.  Only the deleter erases the entry.
+    auto it = gIpcOpen.find(key);
+    if (it != gIpcOpen.end()) {
+      if (auto p = it->second.lock()) return p;  // still mapped (possibly queued for closing: revived)
+    } else if (gIpcClosing.find(key) == gIpcClosing.end()) {
+      break;
+    }
+    gIpcClosed.wait(lk);  // rare: a buffer re-registered while its previous mapping is being closed
   }
   void* mapped = nullptr;
   HIPCHECK(hipIpcOpenMemHandle(&mapped, handle, hipIpcMemLazyEnablePeerAccess));
@@ -60,9 +71,16 @@ std::shared_ptr<void> openIpcHandle(const hipIpcMemHandle_t& handle) {
       std::lock_guard<std::mutex> lk2(gIpcMu);
       auto j = gIpcOpen.find(key);
       if (j != gIpcOpen.end() && j->second.expired()) gIpcOpen.erase(j);
+      ++gIpcClosing[key];
     }
     const hipError_t e = hipIpcCloseMemHandle(q);
     if (e != hipSuccess) warn(std::string("hipIpcCloseMemHandle: ") + hipGetErrorString(e));
+    {
+      std::lock_guard<std::mutex> lk2(gIpcMu);
+      auto j = gIpcClosing.find(key);
+      if (j != gIpcClosing.end() && --j->second <= 0) gIpcClosing.erase(j);
+    }
+    gIpcClosed.notify_all();
   });
   gIpcOpen[key] = p;
   return p;
