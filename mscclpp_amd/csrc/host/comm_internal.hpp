@@ -194,6 +194,12 @@ inline bool envSymmetricMemory() {
   return e && std::string(e) != "0";
 }
 
+inline size_t envMaxUserRegs() {
+  const char* e = std::getenv("MSCCLPP_AMD_MAX_USER_REGS");
+  const long v = e ? std::atol(e) : 0;
+  return v > 0 ? (size_t)v : 1024;
+}
+
 inline int envAlgo() {
   const char* e = std::getenv("MSCCLPP_AMD_ALGO");
   if (!e) return MSCCLPP_AMD_ALGO_AUTO;
@@ -499,7 +505,13 @@ struct ncclComm {
   //  * Pinned entries are released only by dropUserRegistrations (mscclppAmdCommDeregisterAll), which
   //    must not run while a graph that captured them is still replayed, or when the address is
   //    re-used by a new allocation (the old one was freed, so its pointers were dead already).
-  static constexpr size_t kMaxUserRegs = 64;
+  // kMaxUserRegs: 1024 by default, MSCCLPP_AMD_MAX_USER_REGS sets it.  The reference's context cache
+  // has no bound (algorithm.cc:52-60); a small one made a caller cycling through more buckets
+  // re-register on every call -- a host exchange, and, with the device busy, a wait for the close of
+  // the same handle still in flight (openIpcHandle; 2.8 s behind a 2.8 s kernel in
+  // tests/test_no_device_sync_gpu.py).  A bound is still kept: each registration keeps the peers'
+  // allocations mapped, so a peer's freed buffer stays held until its registration is retired.
+  const size_t kMaxUserRegs = envMaxUserRegs();
   struct UserReg {
     uint64_t bufferId = 0;
     uint64_t lastUse = 0;

@@ -146,6 +146,7 @@ def _churn_worker(rank, n, uid, q):
         import os
 
         os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "5000")
+        os.environ["MSCCLPP_AMD_MAX_USER_REGS"] = "64"  # 70 allocations below must evict
         import torch
 
         import mscclpp_amd as m
@@ -236,7 +237,7 @@ def _churn_worker(rank, n, uid, q):
 
 def test_captured_buffers_survive_registration_churn(built):
     """A graph keeps the peer pointers of its buffers: their registrations must not be evicted by
-    later eager calls on 140 other buffers (the cache holds 64), or the replay would write through
+    later eager calls on 140 other buffers (the cache is bounded at 64 here), or the replay would write through
     closed mappings.  The pin is checked through the registration count before anything replays."""
     import mscclpp_amd as m
 

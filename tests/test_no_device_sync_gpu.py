@@ -1,6 +1,6 @@
 """No device-wide synchronize on the call path.
 
-Two rank processes cycle 70 distinct output allocations -- more than the registration cache's 64, so
+Two rank processes cycle 70 distinct output allocations -- more than a registration cache bounded at 64 (MSCCLPP_AMD_MAX_USER_REGS=64), so
 the least recently used registrations are retired while the calls go on -- through ncclAllReduce
 while a long kernel (torch.cuda._sleep, ~3 s) runs on another stream of the same device.  A retired
 mapping now closes when the events recorded after its last launches have completed
@@ -27,9 +27,10 @@ NREUSE = 8  # evicted outputs used again while their mappings are being closed
 COUNT = (1 << 20) + 512  # fp16: 2 MiB + 1 KiB, above the LL range at 2 ranks: a registering bulk kernel
 
 
-def _worker(rank, n, uid, q):
+def _worker(rank, n, uid, cap, q):
     try:
         os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "20000")
+        os.environ["MSCCLPP_AMD_MAX_USER_REGS"] = str(cap)
         import torch
 
         import mp_util
@@ -87,10 +88,12 @@ def _worker(rank, n, uid, q):
         # flight (core.cpp openIpcHandle) -- never opens a handle that is half torn down
         ins2 = [O.lcg(O.F16, COUNT, r, 12) for r in range(n)]
         x2 = torch.from_numpy(ins2[rank].view(np.int16).copy()).view(torch.float16).cuda()
+        ex_before = comm.registration_exchanges()[0]  # allocations registered so far (host exchanges)
         t2 = time.perf_counter()
         for o in outs[:NREUSE]:
             comm.all_reduce(x2, o)
         t_reuse = time.perf_counter() - t2  # diagnosis: includes any wait for a close in flight
+        exchanges = (ex_before, comm.registration_exchanges()[0] - ex_before)
         torch.cuda.synchronize()
         slept_ms = s0.elapsed_time(s1)
         _, _, awaiting_after = comm.registration_stats()
@@ -120,28 +123,34 @@ def _worker(rank, n, uid, q):
                       "busy_after_calls": busy_after_calls, "slept_ms": slept_ms,
                       "slowest_call": (max(per_call), per_call.index(max(per_call))),
                       "calls_over_10ms": [i for i, t in enumerate(per_call) if t > 0.01], "busy_after_frees": busy_after_frees, "regs": regs,
-                      "awaiting": awaiting, "fds": (fds0, fds1), "t_reuse": t_reuse, "awaiting_after": awaiting_after, "err": errc, "bad": bad}, None))
+                      "awaiting": awaiting, "fds": (fds0, fds1), "t_reuse": t_reuse, "exchanges": exchanges, "awaiting_after": awaiting_after, "err": errc, "bad": bad}, None))
     except Exception:
         q.put((rank, None, traceback.format_exc()))
 
 
-def test_calls_and_frees_do_not_wait_for_other_streams(built):
+@pytest.mark.parametrize("cap", [64, 128])
+def test_calls_and_frees_do_not_wait_for_other_streams(built, cap):
+    """cap 64 (the default): the calls evict registrations; MSCCLPP_AMD_MAX_USER_REGS=128: they do not,
+    and the reuse pass registers nothing."""
     import mscclpp_amd as m
 
     n = 2
     uid = m.Communicator.unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, n, uid, q)) for r in range(n)]
+    procs = [ctx.Process(target=_worker, args=(r, n, uid, cap, q)) for r in range(n)]
     for p in procs:
         p.start()
     got = mp_util.collect(procs, q, n, 240)
     print({rank: r for rank, r in got.items()})
     for rank, r in got.items():
-        assert r["sel"] not in (1, 2), r  # a bulk algorithm (registers its output), not the LL paths
+        assert r["sel"] == 3, r  # fullmesh: a bulk algorithm that registers its output, not the LL paths
         assert r["err"] == 0 and r["bad"] == [], (rank, r)
-        # the calls evicted registrations (70 > 64) without joining the sleeping stream
-        assert r["regs"] <= 64 + 1, (rank, r)
+        # fullmesh registers its output only: one exchange per new output allocation
+        if cap == 64:  # the calls evicted registrations (70 > 64) without joining the sleeping stream
+            assert r["regs"] <= 64 + 1 and r["exchanges"] == (NBUF, NREUSE), (rank, r)
+        else:  # all 70 stay registered: the reuse pass is a cache hit on every rank
+            assert r["regs"] == NBUF and r["exchanges"] == (NBUF, 0), (rank, r)
         assert r["busy_after_calls"] and r["busy_after_frees"], f"rank {rank}: {r}"
         # and no call waited for it: the 70 calls took a fraction of the sleep
         assert r["t_calls"] < 0.25 * r["slept_ms"] * 1e-3 and r["t_frees"] < 0.5, f"rank {rank}: {r}"
