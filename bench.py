@@ -1502,7 +1502,8 @@ def bench_extras(args, comm, n, dev, tmax, barrier, vf=None):
         # test/deploy/perf_ndmv4.jsonl / perf_ndmv5.jsonl), timed like common.cc:202-227
         # (20 calls in one graph, 15 launches), int32 data = rank
         mt = {}
-        for k, kb, pub in (("k6", 24, "A100 7.24 us / H100 6.18 us"), ("k6", 48, "A100 7.91 us / H100 6.62 us"),
+        for k, kb, pub in (("k2", 8, "A100 6.51 us (8 ranks, perf_ndmv4.jsonl:5)"),
+                           ("k6", 24, "A100 7.24 us / H100 6.18 us"), ("k6", 48, "A100 7.91 us / H100 6.62 us"),
                            ("k6", 72, "A100 8.28 us / H100 6.91 us"), ("k7", 48, None),
                            ("k5", 48 << 10, "A100 397.79 us, 126.52 GB/s")):
             cnt = kb * 256

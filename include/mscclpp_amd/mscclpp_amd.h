@@ -67,6 +67,7 @@ enum {
   MSCCLPP_AMD_ALGO_RSAG_PIPELINE = 6, /* default_allreduce_rsag_pipeline: put / reduce / recv workgroups
                                          pipelined over a circular scratch (allreduce_rsag_pipeline.cu:85-222) */
   /* the int32 kernels of the mscclpp-test harness (test/mscclpp-test/allreduce_test.cu), by number */
+  MSCCLPP_AMD_ALGO_TEST_K2 = 102, /* allreduce2, one node: LL16 one-hop all-pairs, harness scratch layout (:841-943) */
   MSCCLPP_AMD_ALGO_TEST_K5 = 105, /* allreduce5 (AMD branch): in-place RS by remote reads + ring AG by gets (:959-970) */
   MSCCLPP_AMD_ALGO_TEST_K6 = 106, /* allreduce6: LL16 two-hop, harness scratch layout (:972-1034) */
   MSCCLPP_AMD_ALGO_TEST_K7 = 107  /* allreduce7: LL8 two-hop, harness scratch layout (:1036-1093) */

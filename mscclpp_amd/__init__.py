@@ -25,9 +25,9 @@ E4M3, E5M2, E4M3_ACC_F16, E5M2_ACC_F16, E4M3_ACC_F32, E5M2_ACC_F32 = 5, 6, 7, 8,
 U8, E4M3B15, E4M3B15_ACC_F16, E4M3B15_ACC_F32 = 11, 12, 13, 14
 SUM, MIN = 0, 1
 ALGO_AUTO, ALGO_PACKET, ALGO_ALLPAIR, ALGO_FULLMESH, ALGO_RSAG, ALGO_RSAG_ZC, ALGO_RSAG_PIPELINE = 0, 1, 2, 3, 4, 5, 6
-ALGO_TEST_K5, ALGO_TEST_K6, ALGO_TEST_K7 = 105, 106, 107  # mscclpp-test allreduce5 / 6 / 7 (int32)
+ALGO_TEST_K2, ALGO_TEST_K5, ALGO_TEST_K6, ALGO_TEST_K7 = 102, 105, 106, 107  # mscclpp-test allreduce2/5/6/7 (int32)
 ALGO_NAMES = {"auto": 0, "packet": 1, "allpair": 2, "fullmesh": 3, "rsag": 4, "rsag_zc": 5, "rsag_pipeline": 6,
-              "k5": ALGO_TEST_K5, "k6": ALGO_TEST_K6, "k7": ALGO_TEST_K7}
+              "k2": ALGO_TEST_K2, "k5": ALGO_TEST_K5, "k6": ALGO_TEST_K6, "k7": ALGO_TEST_K7}
 MAX_RANKS = 8
 FLAG_SLOTS = 4096
 MAX_CHANNELS = 256

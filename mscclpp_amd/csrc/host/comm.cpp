@@ -106,7 +106,8 @@ int mscclppAmdAllReduceLaunch(int algo, const mscclppAmdRankView* views, int nvi
                                      (hipStream_t)stream);
     }
     const bool ll = algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR ||
-                    algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7;
+                    algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7 ||
+                    algo == MSCCLPP_AMD_ALGO_TEST_K2;
     unsigned seen = 0;
     for (int i = 0; i < nviews; ++i) {
       const mscclppAmdRankView& v = views[i];
@@ -160,6 +161,7 @@ size_t mscclppAmdScratchRequired(int algo, int nranks, size_t bytes, int dtype) 
     return bulkScratchRequired(nranks, bytes, (size_t)1 << 40, nullptr, 64);
   }
   if (algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7) return testLLScratchRequired(nranks, bytes);
+  if (algo == MSCCLPP_AMD_ALGO_TEST_K2) return testK2ScratchRequired(nranks, bytes);
   if (algo == MSCCLPP_AMD_ALGO_RSAG_ZC || algo == MSCCLPP_AMD_ALGO_TEST_K5) return 0;  // peers' buffers read in place
   if (algo == MSCCLPP_AMD_ALGO_RSAG_PIPELINE) return mscclppAmdScratchRequiredShape(algo, nranks, bytes, dtype, 0, 0);
   return 0;
@@ -415,7 +417,7 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     if (comm->fallback && (dt < 0 || o < 0 || forcedFallback("allreduce")))  // nccl.cc:628-632
       return (int)vendorNccl()->AllReduce(sendbuff, recvbuff, count, datatype, op, (ncclComm_t)comm->fallback, stream);
     if (dt < 0 || o < 0) {
-      warn("unsupported dtype/op for AllReduce (supported: fp16, bf16, fp32, int32, uint32, fp8 e4m3/e5m2 x sum, min)");
+      warn("unsupported dtype/op for AllReduce (supported: fp16, bf16, fp32, int32, uint32, uint8, fp8 e4m3/e5m2 x sum, min)");
       return (int)ncclInvalidArgument;
     }
     return selectAndExecute(comm, "allreduce", sendbuff, recvbuff, bytes, bytes, bytes, datatype, op, stream);
@@ -498,16 +500,16 @@ int mscclppAmdReduceType(int ncclDtype, int accumNcclDtype) { return reduceTypeF
 int mscclppAmdCommAllReduceAccum(ncclComm_t comm, const void* sendbuff, void* recvbuff, size_t count, int ncclDtype,
                                  int ncclOp, int accumNcclDtype, int algo, int nblocks, int nthreads, void* stream) {
   return guarded([&] {
-    if (!comm || !sendbuff || !recvbuff || count == 0) return (int)ncclInvalidArgument;
     const size_t tb = ncclTypeBytes((ncclDataType_t)ncclDtype);
-    const int dt = reduceTypeFromNccl(ncclDtype, accumNcclDtype);
-    const int o = opFromNccl((ncclRedOp_t)ncclOp);
-    if (dt < 0 || o < 0 || tb == 0) return (int)ncclInvalidArgument;
-    if (comm->nranks == 1) {
-      if (sendbuff != recvbuff)
+    if (comm && comm->nranks == 1) {  // a copy, before any argument check (nccl.cc:610-615)
+      if (sendbuff != recvbuff && count * tb)
         HIPCHECK(hipMemcpyAsync(recvbuff, sendbuff, count * tb, hipMemcpyDeviceToDevice, (hipStream_t)stream));
       return (int)ncclSuccess;
     }
+    if (!comm || !sendbuff || !recvbuff || count == 0) return (int)ncclInvalidArgument;
+    const int dt = reduceTypeFromNccl(ncclDtype, accumNcclDtype);
+    const int o = opFromNccl((ncclRedOp_t)ncclOp);
+    if (dt < 0 || o < 0 || tb == 0) return (int)ncclInvalidArgument;
     return comm->allReduce(sendbuff, recvbuff, count * tb, dt, o, algo, nblocks, nthreads, (hipStream_t)stream);
   });
 }

@@ -35,6 +35,7 @@ int launchBroadcast(const mscclppAmdRankView* views, int nviews, int nranks, siz
 size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype);
 size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype);
 size_t testLLScratchRequired(int nranks, size_t bytes);
+size_t testK2ScratchRequired(int nranks, size_t bytes);
 struct BulkGeom;
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks);
 }  // namespace mscclpp_amd
@@ -703,9 +704,10 @@ struct ncclComm {
       algo = MSCCLPP_AMD_ALGO_FULLMESH;
     mscclppAmdRankView v = baseView(in, out);
     if (algo == MSCCLPP_AMD_ALGO_PACKET || algo == MSCCLPP_AMD_ALGO_ALLPAIR || algo == MSCCLPP_AMD_ALGO_TEST_K6 ||
-        algo == MSCCLPP_AMD_ALGO_TEST_K7) {
+        algo == MSCCLPP_AMD_ALGO_TEST_K7 || algo == MSCCLPP_AMD_ALGO_TEST_K2) {
       const size_t need = algo == MSCCLPP_AMD_ALGO_PACKET    ? ll16ScratchRequired(nranks, bytes, dtype)
                           : algo == MSCCLPP_AMD_ALGO_ALLPAIR ? ll8ScratchRequired(nranks, bytes, dtype)
+                          : algo == MSCCLPP_AMD_ALGO_TEST_K2 ? testK2ScratchRequired(nranks, bytes)
                                                              : testLLScratchRequired(nranks, bytes);
       if (need == 0) return ncclInvalidUsage;
       ensure(llScratch, llBytes, peerLL, need, stream);

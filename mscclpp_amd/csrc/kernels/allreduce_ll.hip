@@ -43,6 +43,8 @@ struct LL8Geom {
   uint32_t units;   // 2-word units = ceil(W / 2)
   uint32_t pad;
   uint64_t* trace;  // phase stamps (mscclppAmdTraceSet) or null
+  uint64_t hbOdd;   // mscclpp-test allreduce2 layout only (V & 1024): scratch byte offset of the
+  uint64_t hbEven;  // packets when the flag is odd / even (allreduce_test.cu:861-863)
 };
 
 // ---- packet-major units ------------------------------------------------------------------------
@@ -99,6 +101,17 @@ __device__ __forceinline__ void poll_issue(const uint8_t* base, uint32_t stride,
     const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0,
                                                      ((peers >> p) & 1u) ? 0xFFFFFFFFu : 0u, 0x00020000);
     raw[p] = load16<kSystem>(r, (uint32_t)p * stride + pbyte);
+  }
+}
+// As poll_issue, for a scratch whose source regions are indexed by peer, not by rank: source p sits
+// in slot p < rank ? p : p - 1 (mscclpp-test allreduce2, allreduce_test.cu:876-880).
+__device__ __forceinline__ void poll_issue_peer_slots(const uint8_t* base, uint32_t stride, uint32_t pbyte,
+                                                      uint32_t peers, int rank, u32x4* raw) {
+#pragma unroll
+  for (int p = 0; p < kMaxRanks; ++p) {
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0,
+                                                     ((peers >> p) & 1u) ? 0xFFFFFFFFu : 0u, 0x00020000);
+    raw[p] = load16<kSystem>(r, (uint32_t)(p < rank ? p : p - 1) * stride + pbyte);
   }
 }
 __device__ __forceinline__ uint32_t poll_eval(const u32x4* raw, uint32_t flag, uint32_t peers, u32x2* w) {
@@ -339,7 +352,11 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
   bump_flags(v.flags, flag);
 }
 
-template <int DT, int OP, int NV, int V = 0>  // V: as allreduceLL16Kernel's (bits 4 and 8)
+// V: as allreduceLL16Kernel's (bits 4 and 8); 1024 = mscclpp-test allreduce2 on one node
+// (allreduce_test.cu:841-943): the same one hop with the harness's scratch -- source regions indexed
+// by peer (p < rank ? p : p - 1), odd flags at 0 and even ones after the n - 1 regions.  Its
+// LLPacket {x, flag, y, flag} is the 16-byte unit image below; int32, even nelems (the host checks).
+template <int DT, int OP, int NV, int V = 0>
 __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Geom g, int nranks, uint64_t budget) {
   const mscclppAmdRankView& v = views.v[NV == 1 ? 0 : blockIdx.y];
   const int rank = v.rank;
@@ -366,7 +383,10 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
     w0 = payload_ld(rin, in, (uint64_t)gtid * 8, clamp_valid(g.bytes, (uint64_t)gtid * 8, single ? 4 : 8));
   }
   const uint32_t flag = wave_uniform(flagv);
-  const uint64_t base = (flag & 1u) ? v.scratchBytes / 2 : 0;
+  constexpr bool kPeerSlots = (V & 1024) != 0;
+  const uint64_t base = kPeerSlots ? ((flag & 1u) ? g.hbOdd : g.hbEven) : ((flag & 1u) ? v.scratchBytes / 2 : 0);
+  // byte offset of source p's region in a scratch half
+  auto slotOff = [&](int p) -> uint32_t { return (uint32_t)((kPeerSlots && p > rank ? p - 1 : p) * region); };
 
   // put my whole buffer into every peer's scratch at rank*W packets (allreduce_allpair_packet.cu:39-42)
   for (uint32_t j = gtid; j < g.units; j += G * T) {
@@ -376,7 +396,8 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
 #pragma unroll 1
     for (int q = 0; q < nranks; ++q) {
       if (q == rank) continue;
-      const auto rq = make_rsrc((uint8_t*)v.peerScratch[q] + base + (uint64_t)rank * region);
+      const uint64_t mySlot = kPeerSlots && rank > q ? rank - 1 : rank;  // my region in q's scratch
+      const auto rq = make_rsrc((uint8_t*)v.peerScratch[q] + base + mySlot * region);
       unit_put<kSystem>(rq, j * 16u, w, flag, single);
     }
   }
@@ -400,21 +421,25 @@ __global__ void __launch_bounds__(512) allreduceLL8Kernel(Views<NV> views, LL8Ge
       bool ready = true;
 #pragma unroll
       for (int p = 0; p < kMaxRanks; ++p)
-        if (p < nranks && p != rank) ready &= unit_try(rscr, (uint32_t)(p * region) + j * 16u, flag, w[p], single);
+        if (p < nranks && p != rank) ready &= unit_try(rscr, slotOff(p) + j * 16u, flag, w[p], single);
       if (!ready) missing = peers;  // round 2: every peer read again
+    } else if (kPeerSlots) {
+      u32x4 raw[kMaxRanks];
+      poll_issue_peer_slots((const uint8_t*)v.scratch + base, (uint32_t)region, j * 16u, peers, rank, raw);
+      missing = poll_eval(raw, flag, peers, w);
     } else if (!waveSingle) {
       missing = poll_units((const uint8_t*)v.scratch + base, (uint32_t)region, j * 16u, flag, peers, w);
     } else {
 #pragma unroll
       for (int p = 0; p < kMaxRanks; ++p)
-        if (((peers >> p) & 1u) && !unit_try(rscr, (uint32_t)(p * region) + j * 16u, flag, w[p], single))
+        if (((peers >> p) & 1u) && !unit_try(rscr, slotOff(p) + j * 16u, flag, w[p], single))
           missing |= 1u << p;
     }
     count_misses<V>(v.err + 8, (uint32_t)__builtin_popcount(missing));
     if (missing) {
 #pragma unroll
       for (int p = 0; p < kMaxRanks; ++p)
-        if ((missing >> p) & 1u) w[p] = unit_wait(rscr, (uint32_t)(p * region) + j * 16u, flag, single, budget, v.err);
+        if ((missing >> p) & 1u) w[p] = unit_wait(rscr, slotOff(p) + j * 16u, flag, single, budget, v.err);
     }
 #pragma unroll
     for (int p = 0; p < kMaxRanks; ++p)
@@ -493,6 +518,27 @@ static bool testLLGeometry(int nranks, size_t bytes, LL16Geom* out) {
   return true;
 }
 
+// mscclpp-test allreduce2 on one node (allreduce_test.cu:841-943): int32 pairs, nelems even -> bytes
+// a multiple of 8; each half of the scratch holds n - 1 regions of nPkts = nelems / 2 LLPackets.
+static bool testK2Geometry(int nranks, size_t bytes, LL8Geom* out) {
+  if (bytes == 0 || bytes % 8) return false;
+  LL8Geom g{};
+  g.trace = g_mscclppAmdTrace;
+  g.bytes = bytes;
+  g.W = bytes / 4;
+  g.units = (uint32_t)(g.W / 2);
+  g.hbOdd = 0;
+  g.hbEven = (uint64_t)g.units * 16 * (uint64_t)(nranks - 1);  // scratchBaseIndex = nPkts * nPeers
+  *out = g;
+  return true;
+}
+
+size_t testK2ScratchRequired(int nranks, size_t bytes) {
+  LL8Geom g;
+  if (!testK2Geometry(nranks, bytes, &g)) return 0;
+  return 2 * g.hbEven;  // nPacket * max(nRanksPerNode - 1, 1) * 2 LLPackets (:1277-1283)
+}
+
 size_t testLLScratchRequired(int nranks, size_t bytes) {
   LL16Geom g;
   if (!testLLGeometry(nranks, bytes, &g)) return 0;
@@ -549,18 +595,23 @@ static void launchLL16(const mscclppAmdRankView* views, int nviews, const LL16Ge
     launchLL16T<DT, OP, kMaxRanks>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   }
 }
-template <int DT, int OP>
+template <int DT, int OP, int V = 0>
 static void launchLL8(const mscclppAmdRankView* views, int nviews, const LL8Geom& g, int nranks, int nblocks,
                       int nthreads, uint64_t budget, hipStream_t s) {
   if (nviews == 1) {
     Views<1> vw;
     vw.v[0] = views[0];
-    launchLL8T<DT, OP, 1>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+    launchLL8T<DT, OP, 1, V>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   } else {
     Views<kMaxRanks> vw{};
     for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
-    launchLL8T<DT, OP, kMaxRanks>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+    launchLL8T<DT, OP, kMaxRanks, V>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   }
+}
+template <int DT, int OP>
+static void launchTestK2(const mscclppAmdRankView* views, int nviews, const LL8Geom& g, int nranks, int nblocks,
+                         int nthreads, uint64_t budget, hipStream_t s) {
+  launchLL8<DT, OP, 1024>(views, nviews, g, nranks, nblocks, nthreads, budget, s);
 }
 
 // Default grids.  LL16: a multiple of the peer count (allreduce_packet.cu:164; its defaults, :180-212,
@@ -618,6 +669,18 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
     g.hbOdd = views[0].scratchBytes / 2;  // (flag % numScratchBuff) ? scratchBufferSize / 2 : 0 (:60)
     g.hbEven = 0;
     MSCCLPP_AMD_DISPATCH_ALL(dtype, op,launchLL16, views, nviews, g, nranks, nblocks, nthreads, budget, s);
+  } else if (algo == MSCCLPP_AMD_ALGO_TEST_K2) {
+    // harness default (allreduce_test.cu:1142-1145): (nRanksPerNode - 1) blocks of 1024 threads ->
+    // twice as many 512-lane workgroups here
+    if (nthreads <= 0) nthreads = 512;
+    if (nblocks <= 0) nblocks = 2 * (nranks - 1);
+    if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
+    if (dtype != kI32 && dtype != kU32) return 4;  // an int32 AllReduce
+    LL8Geom g;
+    if (!testK2Geometry(nranks, bytes, &g)) return 5;
+    for (int i = 0; i < nviews; ++i)
+      if (views[i].scratchBytes < testK2ScratchRequired(nranks, bytes)) return 5;
+    MSCCLPP_AMD_DISPATCH(dtype, op, launchTestK2, views, nviews, g, nranks, nblocks, nthreads, budget, s);
   } else if (algo == MSCCLPP_AMD_ALGO_TEST_K6 || algo == MSCCLPP_AMD_ALGO_TEST_K7) {
     // harness defaults (allreduce_test.cu:1134-1141): k6 21 x 512, k7 28 x 1024 -> 512-lane waves here
     if (nthreads <= 0) nthreads = 512;

@@ -594,6 +594,34 @@ void oracle_mscclpp_test_ll(int n, const uint32_t* const* in, uint64_t nelems, u
   free(acc);
 }
 
+/* mscclpp-test allreduce2, single node (test/mscclpp-test/allreduce_test.cu:841-943, worldSize ==
+ * nRanksPerNode), int32, nelems even.  One hop of LL16 packets (LLPacket = {x, flag, y, flag}):
+ * rank s puts its whole buffer into every peer q's scratch at packet
+ * scratchBaseIndex + (s < q ? s : s - 1) * nPkts, scratchBaseIndex = flag & 1 ? 0 : nPkts * (n - 1)
+ * (:861-863, :876-880); rank r sums the n - 1 packet streams in slot order from 0 and adds its own
+ * input last (:884-904), wrapping int32 adds; the result goes to the separate result buffer. */
+void oracle_mscclpp_test_k2(int n, const uint32_t* const* in, uint64_t nelems, uint32_t flag,
+                            uint32_t* const* scratch, uint32_t* const* out) {
+  const uint64_t nPkts = nelems / 2, nPeers = (uint64_t)(n - 1);
+  const uint64_t base = (flag & 1u) ? 0 : nPkts * nPeers;
+  for (int s = 0; s < n; s++)
+    for (int q = 0; q < n; q++)
+      if (q != s) {
+        const uint64_t slot = (uint64_t)(s < q ? s : s - 1);
+        oracle_ll16_pack(in[s], nPkts, flag, scratch[q] + (base + slot * nPkts) * 4);
+      }
+  uint32_t* tmp = (uint32_t*)malloc(nelems * 4 + 8);
+  for (int r = 0; r < n; r++) {
+    for (uint64_t i = 0; i < nelems; i++) out[r][i] = 0;
+    for (uint64_t slot = 0; slot < nPeers; slot++) {
+      oracle_ll16_unpack(scratch[r] + (base + slot * nPkts) * 4, nPkts, flag, tmp);
+      for (uint64_t i = 0; i < nelems; i++) out[r][i] += tmp[i];
+    }
+    for (uint64_t i = 0; i < nelems; i++) out[r][i] = in[r][i] + out[r][i];
+  }
+  free(tmp);
+}
+
 /* allreduceAllPairs (allreduce_allpair_packet.cu:15-69): one-hop LL8.  Rank s writes its
  * whole buffer (W words, W=(2c+2)/4 for 2-byte types) as LL8 packets into every peer's scratch
  * at s*W packets (:28, :40-41); rank r sums x_r then peers ascending (:49-61). */

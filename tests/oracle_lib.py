@@ -67,6 +67,7 @@ def L():
             ("oracle_allreduce_allpairs", [i32, i32, i32, vp, u64, u32, u64, vp, vp], None),
             ("oracle_allreduce_sliced", [i32, i32, i32, vp, u64, u64, i32, vp], None),
             ("oracle_mscclpp_test_ll", [i32, vp, u64, u32, vp, vp], None),
+            ("oracle_mscclpp_test_k2", [i32, vp, u64, u32, vp, vp], None),
             ("oracle_allreduce_owned", [i32, i32, i32, vp, u64, u64, u64, i32, vp], None),
             ("oracle_trigger_encode", [u64, u32, u64, u32, u64, u64, u32, vp], None),
             ("oracle_fifo_commit_bit", [u64, u32], u64),
@@ -160,6 +161,16 @@ def mscclpp_test_ll(inputs, nelems, flag, scratch_bytes):
     scr = [np.zeros(scratch_bytes // 4, np.uint32) for _ in range(n)]
     outs = [np.zeros(nelems, np.uint32) for _ in range(n)]
     L().oracle_mscclpp_test_ll(n, _ptr_array(ins), nelems, flag, _ptr_array(scr), _ptr_array(outs))
+    return outs, scr
+
+
+def mscclpp_test_k2(inputs, nelems, flag, scratch_bytes):
+    """mscclpp-test allreduce2 on one node: outputs and the full scratch images (harness layout)."""
+    n = len(inputs)
+    ins = [np.ascontiguousarray(a).view(np.uint32) for a in inputs]
+    scr = [np.zeros(scratch_bytes // 4, np.uint32) for _ in range(n)]
+    outs = [np.zeros(nelems, np.uint32) for _ in range(n)]
+    L().oracle_mscclpp_test_k2(n, _ptr_array(ins), nelems, flag, _ptr_array(scr), _ptr_array(outs))
     return outs, scr
 
 

@@ -1,7 +1,8 @@
 """GPU parity of the mscclpp-test AllReduce kernels restated for gfx950 (SURVEY §8a row a16:
-test/mscclpp-test/allreduce_test.cu allreduce5 / allreduce6 / allreduce7), n ranks in one process.
+test/mscclpp-test/allreduce_test.cu allreduce2 / allreduce5 / allreduce6 / allreduce7), n ranks in one
+process.
 
-k6 / k7: outputs and the whole packet scratch image (harness layout, flag parity double buffering)
+k2 / k6 / k7: outputs and the whole packet scratch image (harness layout, flag parity double buffering)
 bit-exact against the oracle's restatement; k5 (in place, remote reads + gets): exact int32 sums.
 Plus the harness's known answer (input = rank -> n(n-1)/2, allreduce_test.cu:1172-1183)."""
 import numpy as np
@@ -18,14 +19,16 @@ def _rand_i32(n, count, seed):
     return [rng.integers(-2 ** 31, 2 ** 31, count, dtype=np.int64).astype(np.int32) for _ in range(n)]
 
 
-@pytest.mark.parametrize("kernel", ["k6", "k7"])
+@pytest.mark.parametrize("kernel", ["k6", "k7", "k2"])
 @pytest.mark.parametrize("n,count", [(2, 4096), (4, 8192), (8, 6144), (8, 65536), (3, 1536), (8, 16)])
 def test_ll_test_kernels_bit_exact(built, kernel, n, count):
     import mscclpp_amd as m
 
     code = m.ALGO_NAMES[kernel]
     sb = m.scratch_required(code, n, count * 4, m.I32)
-    assert sb == 8 * count * 4
+    # k6/k7: nPacket * 2 * 2 LLPackets; k2: nPacket * (n - 1) * 2 (allreduce_test.cu:1277-1286)
+    assert sb == (8 * count * 4 if kernel != "k2" else 16 * count * (n - 1))
+    oracle = O.mscclpp_test_k2 if kernel == "k2" else O.mscclpp_test_ll
     ranks = m.InProcessRanks(n, sb)
     for call, flag in enumerate((1, 2, 3)):
         ins = _rand_i32(n, count, 10 * call + n)
@@ -34,7 +37,7 @@ def test_ll_test_kernels_bit_exact(built, kernel, n, count):
         ranks.all_reduce(dins, douts, code)
         torch.cuda.synchronize()
         assert ranks.errors() == [0] * n
-        exp, scr = O.mscclpp_test_ll([a.view(np.uint32) for a in ins], count, flag, sb)
+        exp, scr = oracle([a.view(np.uint32) for a in ins], count, flag, sb)
         want = np.sum(np.stack([a.astype(np.int64) for a in ins]), axis=0).astype(np.uint32)  # wrapping
         for r in range(n):
             got = douts[r].cpu().numpy().view(np.uint32)
@@ -112,7 +115,7 @@ def test_harness_kat(built):
 
     n, count = 8, 1 << 14
     _run_k5([(n, count, None, 0)])  # k5 (in place), default launch shape
-    for kernel in ("k6", "k7"):
+    for kernel in ("k6", "k7", "k2"):
         code = m.ALGO_NAMES[kernel]
         ranks = m.InProcessRanks(n, max(m.scratch_required(code, n, count * 4, m.I32), 1 << 16))
         ins = [torch.full((count,), r, dtype=torch.int32, device="cuda") for r in range(n)]
@@ -125,7 +128,7 @@ def test_harness_kat(built):
 
 
 def test_restrictions(built):
-    """k5 runs in place; k5/k6/k7 are int32 kernels; k6/k7 need bytes % (8 * n) == 0."""
+    """k5 runs in place; k2/k5/k6/k7 are int32 kernels; k6/k7 need bytes % (8 * n) == 0, k2 an even count."""
     import mscclpp_amd as m
 
     n = 4
@@ -140,9 +143,14 @@ def test_restrictions(built):
     odd = [torch.zeros(4 * n + 4, dtype=torch.int32, device="cuda") for _ in range(n)]
     with pytest.raises(m.MscclppError):
         ranks.all_reduce(odd, [torch.empty_like(t) for t in odd], m.ALGO_TEST_K6)
+    with pytest.raises(m.MscclppError):
+        ranks.all_reduce(f, [torch.empty_like(t) for t in f], m.ALGO_TEST_K2)
+    odd2 = [torch.zeros(1023, dtype=torch.int32, device="cuda") for _ in range(n)]
+    with pytest.raises(m.MscclppError):
+        ranks.all_reduce(odd2, [torch.empty_like(t) for t in odd2], m.ALGO_TEST_K2)
 
 
-@pytest.mark.parametrize("kernel", ["1", "5", "6", "7", "rsag_zc"])
+@pytest.mark.parametrize("kernel", ["1", "2", "5", "6", "7", "rsag_zc"])
 def test_harness_two_processes(built, tmp_path, kernel):
     """tools/allreduce_test_perf.py (the mscclpp-test runTest loop) with 2 ranks sharing cuda:0:
     graph-captured timing, the n(n-1)/2 data check and the JSONL perf rows."""
@@ -154,7 +162,7 @@ def test_harness_two_processes(built, tmp_path, kernel):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = tmp_path / "perf.jsonl"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str({"1": 29610, "5": 29611, "6": 29612, "7": 29613}.get(kernel, 29614)),
+           "--master-addr", "127.0.0.1", "--master-port", str({"1": 29610, "5": 29611, "6": 29612, "7": 29613, "2": 29616}.get(kernel, 29614)),
            os.path.join(root, "tools", "allreduce_test_perf.py"), "-b", "64K", "-e", "1M", "-f", "4", "-k", kernel,
            "-w", "2", "-n", "5", "-G", "2", "-o", str(out)]
     env = dict(os.environ, MSCCLPP_AMD_SPIN_TIMEOUT_MS="5000")

@@ -7,8 +7,8 @@ checkData :346-360) and allreduce_test.cu (runColl :1107-1170, initData :1172-11
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
         tools/allreduce_test_perf.py -b 24K -e 48M -f 2 -k 6 -o perf.jsonl
 
-Kernels (-k): 1, 5, 6, 7 -- the harness's own int32 kernels (allreduce1 ring through the host proxy,
-allreduce5 AMD branch, allreduce6 LL16, allreduce7 LL8); or a product algorithm name (packet, allpair, fullmesh,
+Kernels (-k): 1, 2, 5, 6, 7 -- the harness's own int32 kernels (allreduce1 ring through the host proxy,
+allreduce2 LL16 one-hop on one node, allreduce5 AMD branch, allreduce6 LL16, allreduce7 LL8); or a product algorithm name (packet, allpair, fullmesh,
 rsag, rsag_zc) run on the same int32 data.  Timing is the reference's: `iters` calls captured in one
 HIP graph, the graph launched `-G` times after a barrier, time / iters / launches, averaged over
 ranks (-a 1); data check = the known answer input = rank -> n(n-1)/2 on every element.  Rows are
@@ -27,7 +27,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-IN_PLACE = {"1": True, "5": True, "6": False, "7": False}  # isInPlace (allreduce_test.cu:1262-1264)
+IN_PLACE = {"1": True, "2": False, "5": True, "6": False, "7": False}  # isInPlace (allreduce_test.cu:1262-1264)
 
 
 def parse_size(v):
