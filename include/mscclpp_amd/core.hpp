@@ -25,6 +25,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <array>
 #include <cstdint>
 #include <future>
 #include <memory>
@@ -56,6 +57,8 @@ class Bootstrap {
   virtual int getRank() const = 0;
   virtual int getNranks() const = 0;
   virtual int getNranksPerNode() const = 0;
+  // Ranks sharing this rank's GPU IPC domain (bootstrap.cc:459): the whole node here.
+  virtual int getNranksPerIpcDomain() const { return getNranksPerNode(); }
   // Point-to-point, matched by (peer, tag); a send never waits for its receive.
   virtual void send(void* data, int size, int peer, int tag) = 0;
   virtual void recv(void* data, int size, int peer, int tag) = 0;
@@ -66,7 +69,42 @@ class Bootstrap {
   void recv(std::vector<char>& data, int peer, int tag);
 };
 
-// ---- transports (core.hpp:211-460) --------------------------------------------------------------
+// The 128-byte rendezvous id (core.hpp:20-24): the ncclUniqueId of this library.
+constexpr unsigned int UniqueIdBytes = 128;
+using UniqueId = std::array<uint8_t, UniqueIdBytes>;
+
+// TcpBootstrap (core.hpp:113-197).  Ranks meet at a root that the creator of the id runs (a thread
+// of createUniqueId()'s process) or, with initialize("ip:port"), that rank 0 runs at that address.
+// initialize() also builds this library's communicator for the rank on the current device (the
+// IPC-mapped scratch, flags and error word every channel of a Communicator uses), so
+// Communicator(bootstrap) shares it; the timeout is MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S's (default 600 s)
+// when timeoutSec is not positive, else timeoutSec.
+class TcpBootstrap : public Bootstrap {
+ public:
+  static UniqueId createUniqueId();
+  TcpBootstrap(int rank, int nRanks);
+  ~TcpBootstrap() override;
+  UniqueId getUniqueId() const;
+  void initialize(UniqueId uniqueId, int64_t timeoutSec = 30);
+  void initialize(const std::string& ifIpPortTrio, int64_t timeoutSec = 30);
+  int getRank() const override;
+  int getNranks() const override;
+  int getNranksPerNode() const override;
+  void send(void* data, int size, int peer, int tag) override;
+  void recv(void* data, int size, int peer, int tag) override;
+  void allGather(void* allData, int size) override;
+  void barrier() override;
+  using Bootstrap::recv;
+  using Bootstrap::send;
+  // The communicator initialize() built (null before).
+  ncclComm_t ncclComm() const;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> pimpl_;
+};
+
+// ---- transports and devices (core.hpp:211-466) ---------------------------------------------------
 enum class Transport { Unknown, CudaIpc, NumTransports };
 
 class TransportFlags {
@@ -86,11 +124,26 @@ class TransportFlags {
   unsigned bits_ = 0;
 };
 
+enum class DeviceType { Unknown, CPU, GPU };
+
+struct Device {
+  Device() = default;
+  Device(DeviceType type, int id = -1) : type(type), id(id) {}
+  DeviceType type = DeviceType::GPU;
+  int id = -1;  // -1: the communicator's GPU
+};
+
+// Deviation: the default transport is CudaIpc (the reference's is Unknown), the only one here.
 struct EndpointConfig {
   Transport transport = Transport::CudaIpc;
+  Device device{DeviceType::GPU};
+  int maxWriteQueueSize = -1;
   EndpointConfig() = default;
-  EndpointConfig(Transport t) : transport(t) {}
+  EndpointConfig(Transport transport, Device device = DeviceType::GPU, int maxWriteQueueSize = -1)
+      : transport(transport), device(device), maxWriteQueueSize(maxWriteQueueSize) {}
 };
+
+class Context;  // core.hpp:470: accepted by Communicator's constructor, no state of its own here
 
 // ---- registered memory (core.hpp:585-627) -------------------------------------------------------
 class RegisteredMemory {
@@ -175,6 +228,10 @@ class Communicator {
  public:
   // A handle over an existing communicator of this library (not owned).
   explicit Communicator(ncclComm_t comm);
+  // The reference's constructor (core.hpp:818).  A TcpBootstrap brings the communicator its
+  // initialize() built; any other Bootstrap is used to hand rank 0's fresh id to every rank, and the
+  // communicator is built here (collective) and owned.  `context` is accepted and ignored.
+  explicit Communicator(std::shared_ptr<Bootstrap> bootstrap, std::shared_ptr<Context> context = nullptr);
   ~Communicator();
   Communicator(const Communicator&) = delete;
   Communicator& operator=(const Communicator&) = delete;

@@ -212,12 +212,10 @@ void rootLoop(int lfd, uint64_t nonce) {
 
 }  // namespace
 
-BootstrapId bootstrapCreateRoot() {
+// Listen on (addr, port) -- port 0: any -- and run the root thread there; the id names it.
+static BootstrapId createRootOn(in_addr a, uint16_t portNet, uint64_t nonce) {
   BootstrapId id{};
   std::memcpy(id.magic, "MSCAMD1", 8);
-  const char* addrEnv = std::getenv("MSCCLPP_AMD_BOOTSTRAP_ADDR");
-  in_addr a{};
-  if (!addrEnv || inet_pton(AF_INET, addrEnv, &a) != 1) inet_pton(AF_INET, "127.0.0.1", &a);
   int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
   if (lfd < 0) throw std::runtime_error("bootstrap: socket() failed");
   int one = 1;
@@ -225,24 +223,58 @@ BootstrapId bootstrapCreateRoot() {
   sockaddr_in sa{};
   sa.sin_family = AF_INET;
   sa.sin_addr = a;
-  sa.sin_port = 0;
+  sa.sin_port = portNet;
   if (::bind(lfd, (sockaddr*)&sa, sizeof(sa)) != 0 || ::listen(lfd, 256) != 0) {
     ::close(lfd);
     throw std::runtime_error("bootstrap: bind/listen failed");
   }
   socklen_t sl = sizeof(sa);
   getsockname(lfd, (sockaddr*)&sa, &sl);
-  std::random_device rd;
-  id.nonce = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+  id.nonce = nonce;
   id.addr = sa.sin_addr.s_addr;
   id.port = sa.sin_port;
   std::thread(rootLoop, lfd, id.nonce).detach();
   return id;
 }
 
+BootstrapId bootstrapCreateRoot() {
+  const char* addrEnv = std::getenv("MSCCLPP_AMD_BOOTSTRAP_ADDR");
+  in_addr a{};
+  if (!addrEnv || inet_pton(AF_INET, addrEnv, &a) != 1) inet_pton(AF_INET, "127.0.0.1", &a);
+  std::random_device rd;
+  const uint64_t nonce =
+      ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+  return createRootOn(a, 0, nonce);
+}
+
+// "ip:port" or "interface:ip:port" (TcpBootstrap::initialize(ifIpPortTrio), bootstrap.cc:232-262):
+// every rank derives the same id from the string; rank 0 also runs the root there.  The nonce is
+// a hash of the string, so two jobs on different ports never join each other's root.
+BootstrapId bootstrapIdFromIpPort(const std::string& trio, bool createRoot) {
+  const size_t last = trio.rfind(':');
+  if (last == std::string::npos || last + 1 >= trio.size())
+    throw std::invalid_argument("bootstrap: expected \"ip:port\" or \"interface:ip:port\", got \"" + trio + "\"");
+  std::string ip = trio.substr(0, last);
+  const size_t first = ip.rfind(':');
+  if (first != std::string::npos) ip = ip.substr(first + 1);  // drop the interface name
+  const long port = std::strtol(trio.c_str() + last + 1, nullptr, 10);
+  in_addr a{};
+  if (port <= 0 || port > 65535 || inet_pton(AF_INET, ip.c_str(), &a) != 1)
+    throw std::invalid_argument("bootstrap: bad IPv4 address or port in \"" + trio + "\"");
+  uint64_t nonce = 1469598103934665603ull;
+  for (char ch : ip + ":" + std::to_string(port)) nonce = (nonce ^ (unsigned char)ch) * 1099511628211ull;
+  if (createRoot) return createRootOn(a, htons((uint16_t)port), nonce);
+  BootstrapId id{};
+  std::memcpy(id.magic, "MSCAMD1", 8);
+  id.addr = a.s_addr;
+  id.port = htons((uint16_t)port);
+  id.nonce = nonce;
+  return id;
+}
+
 bool bootstrapIdValid(const BootstrapId& id) { return std::memcmp(id.magic, "MSCAMD1", 8) == 0; }
 
-TcpBootstrap::TcpBootstrap(int rank, int nranks, const BootstrapId& id, int timeoutSec)
+StarBootstrap::StarBootstrap(int rank, int nranks, const BootstrapId& id, int timeoutSec)
     : rank_(rank), nranks_(nranks), fd_(-1) {
   sockaddr_in sa{};
   sa.sin_family = AF_INET;
@@ -262,11 +294,11 @@ TcpBootstrap::TcpBootstrap(int rank, int nranks, const BootstrapId& id, int time
   sendAll(fd_, &h, sizeof(h));
 }
 
-TcpBootstrap::~TcpBootstrap() {
+StarBootstrap::~StarBootstrap() {
   if (fd_ >= 0) ::close(fd_);
 }
 
-void TcpBootstrap::readOne() {
+void StarBootstrap::readOne() {
   MsgHeader h{};
   recvAll(fd_, &h, sizeof(h));
   std::vector<char> body(h.len);
@@ -279,7 +311,7 @@ void TcpBootstrap::readOne() {
 }
 
 template <typename Ready>
-void TcpBootstrap::waitFor(Ready ready) {
+void StarBootstrap::waitFor(Ready ready) {
   std::unique_lock<std::mutex> lk(mu_);
   for (;;) {
     if (ready()) return;
@@ -303,7 +335,7 @@ void TcpBootstrap::waitFor(Ready ready) {
   }
 }
 
-void TcpBootstrap::allGather(const void* send, void* recv, size_t bytes) {
+void StarBootstrap::allGather(const void* send, void* recv, size_t bytes) {
   std::lock_guard<std::mutex> round(agMu_);
   {
     std::lock_guard<std::mutex> lk(sendMu_);
@@ -322,7 +354,7 @@ void TcpBootstrap::allGather(const void* send, void* recv, size_t bytes) {
   if (!all.empty()) std::memcpy(recv, all.data(), all.size());
 }
 
-void TcpBootstrap::send(const void* data, size_t bytes, int peer, int tag) {
+void StarBootstrap::send(const void* data, size_t bytes, int peer, int tag) {
   if (peer < 0 || peer >= nranks_) throw std::invalid_argument("bootstrap send: bad peer");
   std::lock_guard<std::mutex> lk(sendMu_);
   MsgHeader h{kMsgP2P, peer, tag, (uint64_t)bytes};
@@ -330,7 +362,7 @@ void TcpBootstrap::send(const void* data, size_t bytes, int peer, int tag) {
   if (bytes) sendAll(fd_, data, bytes);
 }
 
-void TcpBootstrap::recv(void* data, size_t bytes, int peer, int tag) {
+void StarBootstrap::recv(void* data, size_t bytes, int peer, int tag) {
   if (peer < 0 || peer >= nranks_) throw std::invalid_argument("bootstrap recv: bad peer");
   const auto key = std::make_pair(peer, tag);
   std::vector<char> m;
@@ -348,13 +380,13 @@ void TcpBootstrap::recv(void* data, size_t bytes, int peer, int tag) {
   if (bytes) std::memcpy(data, m.data(), bytes);
 }
 
-void TcpBootstrap::barrier() {
+void StarBootstrap::barrier() {
   char dummy = 0;
   std::vector<char> all(nranks_);
   allGather(&dummy, all.data(), 1);
 }
 
-void TcpBootstrap::broadcast(void* buf, size_t bytes, int root) {
+void StarBootstrap::broadcast(void* buf, size_t bytes, int root) {
   std::vector<char> all(bytes * nranks_);
   allGather(buf, all.data(), bytes);
   std::memcpy(buf, all.data() + (size_t)root * bytes, bytes);

@@ -32,14 +32,16 @@ static_assert(sizeof(BootstrapId) == 128, "unique id must be 128 bytes (nccl.h:2
 
 // Creates a listening root (a detached thread in this process) and returns its id.
 BootstrapId bootstrapCreateRoot();
+// The id of "ip:port" / "interface:ip:port"; createRoot: also listen there (the caller is rank 0).
+BootstrapId bootstrapIdFromIpPort(const std::string& ifIpPortTrio, bool createRoot);
 bool bootstrapIdValid(const BootstrapId& id);
 
-class TcpBootstrap {
+class StarBootstrap {
  public:
-  TcpBootstrap(int rank, int nranks, const BootstrapId& id, int timeoutSec);
-  ~TcpBootstrap();
-  TcpBootstrap(const TcpBootstrap&) = delete;
-  TcpBootstrap& operator=(const TcpBootstrap&) = delete;
+  StarBootstrap(int rank, int nranks, const BootstrapId& id, int timeoutSec);
+  ~StarBootstrap();
+  StarBootstrap(const StarBootstrap&) = delete;
+  StarBootstrap& operator=(const StarBootstrap&) = delete;
 
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }

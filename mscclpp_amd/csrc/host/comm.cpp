@@ -215,23 +215,31 @@ ncclResult_t ncclGetUniqueId(ncclUniqueId* uniqueId) {
 }
 
 ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank) {
-  return (ncclResult_t)guarded([&] {
-    if (!comm) return (int)ncclInvalidArgument;
+  const char* to = std::getenv("MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S");
+  return (ncclResult_t)host::commInitRank(comm, nranks, &commId, rank, to ? std::atoi(to) : 600);
+}
+
+}  // extern "C"
+
+namespace mscclpp_amd {
+namespace host {
+int commInitRank(ncclComm_t* comm, int nranks, const void* commId, int rank, int timeoutSec) {
+  return guarded([&] {
+    if (!comm || !commId) return (int)ncclInvalidArgument;
     if (nranks <= 0 || rank < 0 || rank >= nranks) return (int)ncclInvalidArgument;
     if (nranks > MSCCLPP_AMD_MAX_RANKS) {
       warn("mscclpp_amd covers one MI355X node: at most 8 ranks");
       return (int)ncclInvalidUsage;
     }
     BootstrapId id;
-    std::memcpy(&id, &commId, sizeof(id));
+    std::memcpy(&id, commId, sizeof(id));
     if (!bootstrapIdValid(id)) return (int)ncclInvalidArgument;
     auto c = std::make_unique<ncclComm>();
     c->rank = rank;
     c->nranks = nranks;
     HIPCHECK(hipGetDevice(&c->device));
-    const char* to = std::getenv("MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S");
     info("rank " + std::to_string(rank) + ": bootstrap connect");
-    c->boot = std::make_unique<TcpBootstrap>(rank, nranks, id, to ? std::atoi(to) : 600);
+    c->boot = std::make_unique<StarBootstrap>(rank, nranks, id, timeoutSec > 0 ? timeoutSec : 600);
     info("rank " + std::to_string(rank) + ": bootstrap connected");
     const size_t tokBytes = sizeof(uint64_t) * MSCCLPP_AMD_MAX_RANKS * MSCCLPP_AMD_MAX_CHANNELS;
     c->tokens = (uint64_t*)allocUncached(tokBytes);
@@ -266,6 +274,10 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
     return (int)ncclSuccess;
   });
 }
+}  // namespace host
+}  // namespace mscclpp_amd
+
+extern "C" {
 
 ncclResult_t ncclCommInitRankConfig(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank, ncclConfig_t*) {
   return ncclCommInitRank(comm, nranks, commId, rank);
@@ -584,7 +596,7 @@ int mscclppAmdBootstrapCreate(int rank, int nranks, const void* uniqueId, void**
     BootstrapId id;
     std::memcpy(&id, uniqueId, sizeof(id));
     if (!bootstrapIdValid(id)) return (int)ncclInvalidArgument;
-    *handle = new TcpBootstrap(rank, nranks, id, 120);
+    *handle = new StarBootstrap(rank, nranks, id, 120);
     return (int)ncclSuccess;
   });
 }
@@ -592,7 +604,7 @@ int mscclppAmdBootstrapCreate(int rank, int nranks, const void* uniqueId, void**
 int mscclppAmdBootstrapAllGather(void* handle, const void* sendbuf, void* recvbuf, size_t bytes) {
   return guarded([&] {
     if (!handle) return (int)ncclInvalidArgument;
-    static_cast<TcpBootstrap*>(handle)->allGather(sendbuf, recvbuf, bytes);
+    static_cast<StarBootstrap*>(handle)->allGather(sendbuf, recvbuf, bytes);
     return (int)ncclSuccess;
   });
 }
@@ -600,13 +612,13 @@ int mscclppAmdBootstrapAllGather(void* handle, const void* sendbuf, void* recvbu
 int mscclppAmdBootstrapBarrier(void* handle) {
   return guarded([&] {
     if (!handle) return (int)ncclInvalidArgument;
-    static_cast<TcpBootstrap*>(handle)->barrier();
+    static_cast<StarBootstrap*>(handle)->barrier();
     return (int)ncclSuccess;
   });
 }
 
 int mscclppAmdBootstrapDestroy(void* handle) {
-  delete static_cast<TcpBootstrap*>(handle);
+  delete static_cast<StarBootstrap*>(handle);
   return ncclSuccess;
 }
 

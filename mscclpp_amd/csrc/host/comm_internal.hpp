@@ -288,7 +288,7 @@ inline std::shared_ptr<void> importBlob(const IpcBlob& b) {
 }
 
 struct ncclComm {
-  std::unique_ptr<TcpBootstrap> boot;
+  std::unique_ptr<StarBootstrap> boot;
   // the C++ plugin layer (algorithm.cpp): handle passed to Algorithm::execute, the collection the
   // NCCL entry points select from (nccl.cc:176, :308-314) and the executor for DSL algorithms,
   // created on the first DSL selection (collective: every rank selects the same algorithm)
@@ -873,6 +873,9 @@ const VendorNccl* vendorNccl();
 // MSCCLPP_AMD_FORCE_NCCL_FALLBACK_OPERATION ("all" or a comma list of allreduce, allgather,
 // reducescatter, broadcast) names `op`.
 bool forcedFallback(const char* op);
+// ncclCommInitRank with the bootstrap's connect / receive timeout given (ncclCommInitRank takes it
+// from MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S); commId is the 128-byte unique id.  Returns an ncclResult_t.
+int commInitRank(ncclComm_t* comm, int nranks, const void* commId, int rank, int timeoutSec);
 void initFallbackComm(ncclComm* c);                 // collective over c's bootstrap
 void destroyFallbackComm(ncclComm* c, bool abort);
 }  // namespace host

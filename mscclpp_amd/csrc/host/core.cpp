@@ -53,6 +53,7 @@ std::condition_variable gIpcClosed;
 std::shared_ptr<void> openIpcHandle(const hipIpcMemHandle_t& handle) {
   std::unique_lock<std::mutex> lk(gIpcMu);
   HandleKey key{handle};
+  bool warned = false;
   for (;;) {
     // An entry whose mapping has expired belongs to a deleter that has not reached its lock yet:
     // that is a close in progress too.  Only the deleter erases the entry.
@@ -62,7 +63,12 @@ std::shared_ptr<void> openIpcHandle(const hipIpcMemHandle_t& handle) {
     } else if (gIpcClosing.find(key) == gIpcClosing.end()) {
       break;
     }
-    gIpcClosed.wait(lk);  // rare: a buffer re-registered while its previous mapping is being closed
+    // rare: a buffer re-registered while its previous mapping is being closed (the close waits for
+    // the device to go idle, so a kernel that never ends keeps this waiting: say so once)
+    if (gIpcClosed.wait_for(lk, std::chrono::seconds(10)) == std::cv_status::timeout && !warned) {
+      warn("openIpcHandle: waiting for the previous mapping of this handle to close (the device is not idle)");
+      warned = true;
+    }
   }
   void* mapped = nullptr;
   HIPCHECK(hipIpcOpenMemHandle(&mapped, handle, hipIpcMemLazyEnablePeerAccess));
@@ -483,6 +489,113 @@ std::shared_ptr<Communicator> Communicator::create(int rank, int nranks, const n
   return p;
 }
 
+namespace {
+std::string initError(ncclResult_t r) {
+  return std::string(ncclGetErrorString(r)) + ": " + ncclGetLastError(nullptr);
+}
+}  // namespace
+
+// ---- TcpBootstrap (core.hpp:113-197) ----------------------------------------------------------------
+struct TcpBootstrap::Impl {
+  int rank = 0, nranks = 0;
+  UniqueId id{};
+  bool haveId = false;
+  ncclComm_t comm = nullptr;
+  std::shared_ptr<Bootstrap> link;  // the communicator's bootstrap (CommBootstrap)
+  Bootstrap& ready() const {
+    if (!link) throw Error("TcpBootstrap: call initialize() first", ErrorCode::InvalidUsage);
+    return *link;
+  }
+  void init(const void* id128, int64_t timeoutSec) {
+    if (comm) throw Error("TcpBootstrap: already initialized", ErrorCode::InvalidUsage);
+    const int r = host::commInitRank(&comm, nranks, id128, rank, (int)timeoutSec);
+    if (r != ncclSuccess) {
+      comm = nullptr;
+      throw Error("TcpBootstrap::initialize: " + initError((ncclResult_t)r), ErrorCode::SystemError);
+    }
+    link = std::make_shared<CommBootstrap>(comm);
+  }
+};
+
+UniqueId TcpBootstrap::createUniqueId() {
+  ncclUniqueId nid;
+  const ncclResult_t r = ncclGetUniqueId(&nid);
+  if (r != ncclSuccess) throw Error("TcpBootstrap::createUniqueId: " + initError(r), ErrorCode::SystemError);
+  UniqueId id;
+  static_assert(sizeof(nid) == UniqueIdBytes, "ncclUniqueId and UniqueId are both 128 bytes");
+  std::memcpy(id.data(), &nid, UniqueIdBytes);
+  return id;
+}
+
+TcpBootstrap::TcpBootstrap(int rank, int nRanks) : pimpl_(std::make_unique<Impl>()) {
+  if (nRanks <= 0 || rank < 0 || rank >= nRanks)
+    throw Error("TcpBootstrap: rank " + std::to_string(rank) + " of " + std::to_string(nRanks), ErrorCode::InvalidUsage);
+  pimpl_->rank = rank;
+  pimpl_->nranks = nRanks;
+}
+
+TcpBootstrap::~TcpBootstrap() {
+  if (pimpl_ && pimpl_->comm) (void)ncclCommDestroy(pimpl_->comm);
+}
+
+UniqueId TcpBootstrap::getUniqueId() const {
+  if (!pimpl_->haveId) throw Error("TcpBootstrap::getUniqueId: no id yet", ErrorCode::InvalidUsage);
+  return pimpl_->id;
+}
+
+void TcpBootstrap::initialize(UniqueId uniqueId, int64_t timeoutSec) {
+  pimpl_->id = uniqueId;
+  pimpl_->haveId = true;
+  pimpl_->init(uniqueId.data(), timeoutSec);
+}
+
+void TcpBootstrap::initialize(const std::string& ifIpPortTrio, int64_t timeoutSec) {
+  BootstrapId bid;
+  try {
+    bid = bootstrapIdFromIpPort(ifIpPortTrio, /*createRoot*/ pimpl_->rank == 0);
+  } catch (const std::invalid_argument& e) {
+    throw Error(std::string("TcpBootstrap::initialize: ") + e.what(), ErrorCode::InvalidUsage);
+  } catch (const std::exception& e) {
+    throw Error(std::string("TcpBootstrap::initialize: ") + e.what(), ErrorCode::SystemError);
+  }
+  std::memcpy(pimpl_->id.data(), &bid, UniqueIdBytes);
+  pimpl_->haveId = true;
+  pimpl_->init(&bid, timeoutSec);
+}
+
+int TcpBootstrap::getRank() const { return pimpl_->rank; }
+int TcpBootstrap::getNranks() const { return pimpl_->nranks; }
+int TcpBootstrap::getNranksPerNode() const { return pimpl_->nranks; }
+void TcpBootstrap::send(void* data, int size, int peer, int tag) { pimpl_->ready().send(data, size, peer, tag); }
+void TcpBootstrap::recv(void* data, int size, int peer, int tag) { pimpl_->ready().recv(data, size, peer, tag); }
+void TcpBootstrap::allGather(void* allData, int size) { pimpl_->ready().allGather(allData, size); }
+void TcpBootstrap::barrier() { pimpl_->ready().barrier(); }
+ncclComm_t TcpBootstrap::ncclComm() const { return pimpl_->comm; }
+
+Communicator::Communicator(std::shared_ptr<Bootstrap> bootstrap, std::shared_ptr<Context>) : comm_(nullptr) {
+  if (!bootstrap) throw Error("Communicator: null bootstrap", ErrorCode::InvalidUsage);
+  if (auto* tcp = dynamic_cast<TcpBootstrap*>(bootstrap.get())) {
+    comm_ = tcp->ncclComm();  // owned by the bootstrap, which this communicator keeps alive
+    if (!comm_) throw Error("Communicator: the TcpBootstrap is not initialized", ErrorCode::InvalidUsage);
+  } else {
+    // any other Bootstrap: rank 0's fresh id travels over it, then every rank builds the communicator
+    const int rank = bootstrap->getRank(), n = bootstrap->getNranks();
+    std::vector<ncclUniqueId> ids((size_t)n);
+    if (rank == 0) {
+      const ncclResult_t r = ncclGetUniqueId(&ids[0]);
+      if (r != ncclSuccess) throw Error("Communicator: ncclGetUniqueId: " + initError(r), ErrorCode::SystemError);
+    }
+    bootstrap->allGather(ids.data(), (int)sizeof(ncclUniqueId));
+    const ncclResult_t r = ncclCommInitRank(&comm_, n, ids[0], rank);
+    if (r != ncclSuccess) {
+      comm_ = nullptr;
+      throw Error("Communicator: ncclCommInitRank: " + initError(r), ErrorCode::SystemError);
+    }
+    owned_ = true;
+  }
+  bootstrap_ = std::move(bootstrap);
+}
+
 int Communicator::rank() const { return comm_->rank; }
 int Communicator::nRanks() const { return comm_->nranks; }
 int Communicator::nRanksPerNode() const { return comm_->nranks; }
@@ -559,6 +672,10 @@ struct EndpointWire {
 std::shared_future<Connection> Communicator::connect(const EndpointConfig& localConfig, int remoteRank, int tag) {
   if (localConfig.transport != Transport::CudaIpc)
     throw Error("connect: one MI355X node carries CudaIpc connections only", ErrorCode::InvalidUsage);
+  if (localConfig.device.type != DeviceType::GPU ||
+      (localConfig.device.id >= 0 && localConfig.device.id != comm_->device))
+    throw Error("connect: the local endpoint is this communicator's GPU (" + std::to_string(comm_->device) + ")",
+                ErrorCode::InvalidUsage);
   if (remoteRank < 0 || remoteRank >= comm_->nranks)
     throw Error("connect: bad remote rank", ErrorCode::InvalidUsage);
   EndpointWire mine{comm_->rank, (int32_t)getpid(), comm_->device, (int32_t)Transport::CudaIpc};

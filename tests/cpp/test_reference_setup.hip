@@ -1,0 +1,308 @@
+// The reference's user-level setup sequence, written only with its spellings (<mscclpp/...> headers,
+// namespace mscclpp, TcpBootstrap, Communicator(bootstrap), EndpointConfig{transport, {DeviceType,
+// id}}, GpuBuffer, DeviceSyncer), run on this library.  Three modes:
+//
+//   local       one rank: a PortChannel from one GpuBuffer to another over a connection to itself,
+//               one workgroup writes and puts with a signal, another waits and checks
+//               (the sequence of test/unit/local_channel_tests.cu:15-78)
+//   pair PORT   two processes meet at 127.0.0.1:PORT through TcpBootstrap::initialize("ip:port"),
+//               build a MemoryChannel and a packet MemoryChannel over GpuBuffers, and run a
+//               bidirectional put (+ signal / wait), get and putPackets / unpackPackets round, each
+//               checked word by word (the sequence of examples/tutorials/03-memory-channel)
+//   uid         the parent creates a UniqueId (TcpBootstrap::createUniqueId); two forked ranks
+//               initialize with it, and their Communicators exchange a buffer through a memory
+//               channel
+// Exit status 0 and "<mode> OK" on success.
+#include <hip/hip_runtime.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include <mscclpp/concurrency_device.hpp>
+#include <mscclpp/core.hpp>
+#include <mscclpp/gpu_utils.hpp>
+#include <mscclpp/memory_channel.hpp>
+#include <mscclpp/memory_channel_device.hpp>
+#include <mscclpp/port_channel.hpp>
+#include <mscclpp/port_channel_device.hpp>
+
+#define CHECK(cond)                                                               \
+  do {                                                                            \
+    if (!(cond)) {                                                                \
+      std::fprintf(stderr, "%s:%d check failed: %s\n", __FILE__, __LINE__, #cond); \
+      std::exit(1);                                                               \
+    }                                                                             \
+  } while (0)
+
+constexpr int kMagic = 777;
+
+// ---- local: PortChannel loopback -------------------------------------------------------------------
+__constant__ mscclpp::PortChannelDeviceHandle gPortChannel;
+
+__global__ void localPortChannelKernel(int* dst, int* src, size_t bytes, int* ret) {
+  if (blockIdx.x == 0) {
+    for (size_t i = threadIdx.x; i < bytes / sizeof(int); i += blockDim.x) src[i] = kMagic;
+    __syncthreads();
+    if (threadIdx.x == 0) gPortChannel.putWithSignal(0, bytes);
+  } else {
+    if (threadIdx.x == 0) gPortChannel.wait();
+    __syncthreads();
+    for (size_t i = threadIdx.x; i < bytes / sizeof(int); i += blockDim.x)
+      if (dst[i] != kMagic) *ret = 1;
+  }
+}
+
+static int runLocal() {
+  MSCCLPP_CUDATHROW(hipSetDevice(0));
+  auto bootstrap = std::make_shared<mscclpp::TcpBootstrap>(/*rank*/ 0, /*nRanks*/ 1);
+  bootstrap->initialize(mscclpp::TcpBootstrap::createUniqueId());
+  auto communicator = std::make_shared<mscclpp::Communicator>(bootstrap);
+  const mscclpp::Transport transport = mscclpp::Transport::CudaIpc;
+  auto connection = communicator->connect(transport, /*remoteRank*/ 0).get();
+
+  const size_t bytes = 4 << 20;
+  auto srcBuff = mscclpp::GpuBuffer(bytes).memory();
+  auto dstBuff = mscclpp::GpuBuffer(bytes).memory();
+  auto srcMem = communicator->registerMemory(srcBuff.get(), bytes, transport);
+  auto dstMem = communicator->registerMemory(dstBuff.get(), bytes, transport);
+
+  auto proxyService = std::make_shared<mscclpp::ProxyService>();
+  auto srcMemId = proxyService->addMemory(srcMem);
+  auto dstMemId = proxyService->addMemory(dstMem);
+  auto sid = proxyService->buildAndAddSemaphore(*communicator, connection);
+  auto portChannel = proxyService->portChannel(sid, dstMemId, srcMemId);
+  auto handle = portChannel.deviceHandle();
+  MSCCLPP_CUDATHROW(hipMemcpyToSymbol(HIP_SYMBOL(gPortChannel), &handle, sizeof(handle)));
+
+  std::shared_ptr<int> ret = mscclpp::detail::gpuCallocHostShared<int>();
+  proxyService->startProxy();
+  hipLaunchKernelGGL(localPortChannelKernel, dim3(2), dim3(1024), 0, 0, (int*)dstBuff.get(), (int*)srcBuff.get(),
+                     bytes, ret.get());
+  MSCCLPP_CUDATHROW(hipDeviceSynchronize());
+  proxyService->stopProxy();
+  CHECK(*ret == 0);
+  std::printf("local OK\n");
+  return 0;
+}
+
+// ---- pair: the memory-channel tutorial's three kernels ------------------------------------------
+__device__ mscclpp::DeviceSyncer devSyncer;
+
+__global__ void bidirPutKernel(mscclpp::MemoryChannelDeviceHandle* ch, size_t copyBytes, int myRank) {
+  const int tid = threadIdx.x + blockIdx.x * blockDim.x;
+  if (tid == 0) {
+    ch->relaxedSignal();
+    ch->relaxedWait();
+  }
+  devSyncer.sync(gridDim.x);
+  const uint64_t off = myRank * copyBytes;
+  ch->put(off, off, copyBytes, tid, blockDim.x * gridDim.x);
+  devSyncer.sync(gridDim.x);
+  if (tid == 0) {
+    ch->signal();
+    ch->wait();
+  }
+}
+
+__global__ void bidirGetKernel(mscclpp::MemoryChannelDeviceHandle* ch, size_t copyBytes, int myRank) {
+  const int tid = threadIdx.x + blockIdx.x * blockDim.x;
+  if (tid == 0) {
+    ch->relaxedSignal();
+    ch->relaxedWait();
+  }
+  devSyncer.sync(gridDim.x);
+  const uint64_t off = (myRank ^ 1) * copyBytes;
+  ch->get(off, off, copyBytes, tid, blockDim.x * gridDim.x);
+  devSyncer.sync(gridDim.x);
+  if (tid == 0) {  // the peer may not overwrite what this rank still reads
+    ch->signal();
+    ch->wait();
+  }
+}
+
+__global__ void bidirPutPacketKernel(mscclpp::MemoryChannelDeviceHandle* ch, size_t copyBytes, int myRank,
+                                     uint32_t flag) {
+  const int tid = threadIdx.x + blockIdx.x * blockDim.x;
+  if (tid == 0) {
+    ch->relaxedSignal();
+    ch->relaxedWait();
+  }
+  devSyncer.sync(gridDim.x);
+  const uint64_t off = myRank * copyBytes;
+  ch->putPackets(0, off, copyBytes, tid, blockDim.x * gridDim.x, flag);
+  ch->unpackPackets(0, off, copyBytes, tid, blockDim.x * gridDim.x, flag);
+}
+
+static std::vector<int> pattern(int rank, size_t n, int round) {
+  std::vector<int> v(n);
+  for (size_t i = 0; i < n; ++i) v[i] = (rank + 1) * 1000003 + (int)i * 7 + round * 31;
+  return v;
+}
+
+static int pairWorker(int myRank, const std::string& ipPort) {
+  MSCCLPP_CUDATHROW(hipSetDevice(0));
+  int gpuId = 0;
+  MSCCLPP_CUDATHROW(hipGetDevice(&gpuId));
+  const int remoteRank = myRank ^ 1, nRanks = 2;
+  const mscclpp::Transport transport = mscclpp::Transport::CudaIpc;
+  const size_t copyBytes = 1 << 20, n = copyBytes / sizeof(int);
+
+  auto bootstrap = std::make_shared<mscclpp::TcpBootstrap>(myRank, nRanks);
+  bootstrap->initialize(ipPort);
+  mscclpp::Communicator comm(bootstrap);
+  auto conn = comm.connect({transport, {mscclpp::DeviceType::GPU, gpuId}}, remoteRank).get();
+  auto sema = comm.buildSemaphore(conn, remoteRank).get();
+
+  mscclpp::GpuBuffer buffer(2 * copyBytes);
+  mscclpp::GpuBuffer pktBuffer(4 * copyBytes);
+  CHECK(buffer.bytes() == 2 * copyBytes && buffer.deviceId() == gpuId);
+  auto localRegMem = comm.registerMemory(buffer.data(), buffer.bytes(), transport);
+  auto localPktRegMem = comm.registerMemory(pktBuffer.data(), pktBuffer.bytes(), transport);
+  comm.sendMemory(localRegMem, remoteRank);
+  comm.sendMemory(localPktRegMem, remoteRank);
+  auto remoteRegMemFuture = comm.recvMemory(remoteRank);
+  auto remotePktRegMemFuture = comm.recvMemory(remoteRank);
+  mscclpp::RegisteredMemory remoteRegMem = remoteRegMemFuture.get();
+  mscclpp::RegisteredMemory remotePktRegMem = remotePktRegMemFuture.get();
+
+  mscclpp::MemoryChannel memChan(sema, /*dst*/ remoteRegMem, /*src*/ localRegMem);
+  mscclpp::MemoryChannel memPktChan(sema, /*dst*/ remotePktRegMem, /*src*/ localRegMem,
+                                    /*packetBuffer*/ localPktRegMem.data());
+  auto h = memChan.deviceHandle();
+  auto hp = memPktChan.deviceHandle();
+  auto dh = mscclpp::detail::gpuCallocShared<mscclpp::MemoryChannelDeviceHandle>();
+  auto dhp = mscclpp::detail::gpuCallocShared<mscclpp::MemoryChannelDeviceHandle>();
+  mscclpp::gpuMemcpy(dh.get(), &h, 1, hipMemcpyHostToDevice);
+  mscclpp::gpuMemcpy(dhp.get(), &hp, 1, hipMemcpyHostToDevice);
+  hipStream_t stream;
+  MSCCLPP_CUDATHROW(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  int* buf = (int*)buffer.data();
+  std::vector<int> got(2 * n);
+
+  auto fillMine = [&](int round) {
+    auto mine = pattern(myRank, n, round);
+    std::vector<int> zeros(n, 0);
+    mscclpp::gpuMemcpy(buf + myRank * n, mine.data(), n, hipMemcpyHostToDevice);
+    mscclpp::gpuMemcpy(buf + remoteRank * n, zeros.data(), n, hipMemcpyHostToDevice);
+    MSCCLPP_CUDATHROW(hipDeviceSynchronize());
+    bootstrap->barrier();
+  };
+  auto expectAt = [&](int region, int ofRank, int round, const char* what) {
+    mscclpp::gpuMemcpy(got.data(), buf, 2 * n, hipMemcpyDeviceToHost);
+    const auto want = pattern(ofRank, n, round);
+    size_t bad = 0;
+    for (size_t i = 0; i < n; ++i) bad += got[region * n + i] != want[i];
+    if (bad) std::fprintf(stderr, "rank %d %s: %zu of %zu words wrong\n", myRank, what, bad, n);
+    CHECK(bad == 0);
+  };
+
+  // put: my region goes to the peer's buffer at the same offset
+  fillMine(0);
+  hipLaunchKernelGGL(bidirPutKernel, dim3(32), dim3(1024), 0, stream, dh.get(), copyBytes, myRank);
+  MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+  bootstrap->barrier();
+  expectAt(remoteRank, remoteRank, 0, "put");
+  expectAt(myRank, myRank, 0, "put (own region)");
+
+  // get: the peer's region is read from the peer's buffer
+  fillMine(1);
+  hipLaunchKernelGGL(bidirGetKernel, dim3(32), dim3(1024), 0, stream, dh.get(), copyBytes, myRank);
+  MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+  bootstrap->barrier();
+  expectAt(remoteRank, remoteRank, 1, "get");
+
+  // packets: my region goes to the peer's packet buffer; I unpack the peer's into my own region
+  for (uint32_t flag = 1; flag <= 3; ++flag) {
+    fillMine(10 + (int)flag);
+    hipLaunchKernelGGL(bidirPutPacketKernel, dim3(32), dim3(1024), 0, stream, dhp.get(), copyBytes, myRank, flag);
+    MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+    bootstrap->barrier();
+    expectAt(myRank, remoteRank, 10 + (int)flag, "putPackets/unpackPackets");
+  }
+  MSCCLPP_CUDATHROW(hipStreamDestroy(stream));
+  bootstrap->barrier();
+  std::printf("rank %d pair OK\n", myRank);
+  std::fflush(stdout);
+  return 0;
+}
+
+// ---- uid: a UniqueId from the parent, Communicators in the children ------------------------------
+__global__ void putSignalKernel(mscclpp::MemoryChannelDeviceHandle ch, size_t bytes) {
+  ch.put(0, 0, bytes, threadIdx.x, blockDim.x);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ch.signal();
+    ch.wait();
+  }
+}
+
+static int uidWorker(int myRank, mscclpp::UniqueId id) {
+  MSCCLPP_CUDATHROW(hipSetDevice(0));
+  auto bootstrap = std::make_shared<mscclpp::TcpBootstrap>(myRank, 2);
+  bootstrap->initialize(id);
+  CHECK(bootstrap->getUniqueId() == id && bootstrap->getRank() == myRank && bootstrap->getNranks() == 2);
+  auto comm = std::make_shared<mscclpp::Communicator>(bootstrap);
+  const int remote = myRank ^ 1;
+  auto conn = comm->connect(mscclpp::Transport::CudaIpc, remote).get();
+  auto sema = comm->buildSemaphore(conn, remote).get();
+  const size_t n = 1 << 16;
+  mscclpp::GpuBuffer<int> src(n), dst(n);
+  auto srcMem = comm->registerMemory(src.data(), src.bytes(), mscclpp::Transport::CudaIpc);
+  auto dstMem = comm->registerMemory(dst.data(), dst.bytes(), mscclpp::Transport::CudaIpc);
+  comm->sendMemory(dstMem, remote);
+  auto peerDst = comm->recvMemory(remote).get();
+  auto mine = pattern(myRank, n, 5);
+  mscclpp::gpuMemcpy(src.data(), mine.data(), n, hipMemcpyHostToDevice);
+  bootstrap->barrier();
+  mscclpp::MemoryChannel ch(sema, peerDst, srcMem);
+  hipLaunchKernelGGL(putSignalKernel, dim3(1), dim3(1024), 0, 0, ch.deviceHandle(), n * sizeof(int));
+  MSCCLPP_CUDATHROW(hipDeviceSynchronize());
+  std::vector<int> got(n);
+  mscclpp::gpuMemcpy(got.data(), dst.data(), n, hipMemcpyDeviceToHost);
+  CHECK(got == pattern(remote, n, 5));
+  bootstrap->barrier();
+  std::printf("rank %d uid OK\n", myRank);
+  std::fflush(stdout);
+  return 0;
+}
+
+static int forkPair(const std::function<int(int)>& worker, const char* name) {
+  std::vector<pid_t> pids;
+  for (int r = 0; r < 2; ++r) {
+    const pid_t pid = fork();
+    CHECK(pid >= 0);
+    if (pid == 0) std::_Exit(worker(r));
+    pids.push_back(pid);
+  }
+  int bad = 0;
+  for (pid_t pid : pids) {
+    int st = 0;
+    waitpid(pid, &st, 0);
+    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) bad++;
+  }
+  std::printf(bad ? "%s FAILED\n" : "%s OK\n", name);
+  return bad ? 1 : 0;
+}
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "";
+  if (mode == "local") return runLocal();
+  if (mode == "pair" && argc > 2) {
+    const std::string ipPort = std::string("127.0.0.1:") + argv[2];
+    return forkPair([&](int r) { return pairWorker(r, ipPort); }, "pair");
+  }
+  if (mode == "uid") {
+    // the id is created here, before any child touches the GPU (the root thread lives in this
+    // process); no HIP call is made in the parent
+    const mscclpp::UniqueId id = mscclpp::TcpBootstrap::createUniqueId();
+    return forkPair([&](int r) { return uidWorker(r, id); }, "uid");
+  }
+  std::fprintf(stderr, "usage: %s local | pair PORT | uid\n", argv[0]);
+  return 2;
+}

@@ -12,11 +12,11 @@
 #include "bootstrap.hpp"
 
 using mscclpp_amd::BootstrapId;
-using mscclpp_amd::TcpBootstrap;
+using mscclpp_amd::StarBootstrap;
 
 static void rankMain(int rank, int n, BootstrapId id, int rounds, int* bad) {
   try {
-    TcpBootstrap b(rank, n, id, 60);
+    StarBootstrap b(rank, n, id, 60);
     std::vector<int> mine(16), all(16 * n);
     for (int it = 0; it < rounds; ++it) {
       for (int k = 0; k < 16; ++k) mine[k] = rank * 1000 + it * 16 + k;

@@ -1,0 +1,43 @@
+"""The reference's user-level setup written with its own spellings (tests/cpp/test_reference_setup.hip):
+TcpBootstrap + Communicator(bootstrap) + EndpointConfig{transport, {DeviceType, id}} + GpuBuffer +
+DeviceSyncer, on this library -- a PortChannel loopback on one rank (test/unit/local_channel_tests.cu),
+the memory-channel tutorial's put / get / packet round between two processes meeting at "ip:port"
+(examples/tutorials/03-memory-channel), and a UniqueId made in the parent."""
+import os
+import socket
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "bin", "test_reference_setup")
+
+
+def _run(args, timeout=120):
+    env = dict(os.environ, MSCCLPP_AMD_SPIN_TIMEOUT_MS="5000")
+    r = subprocess.run([EXE] + args, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout,
+                       env=env)
+    assert r.returncode == 0, r.stdout[-3000:]
+    return r.stdout
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_port_channel_loopback_one_rank(built):
+    assert "local OK" in _run(["local"])
+
+
+def test_memory_channel_tutorial_ip_port(built):
+    out = _run(["pair", str(_free_port())])
+    assert "rank 0 pair OK" in out and "rank 1 pair OK" in out and "pair OK" in out
+
+
+def test_unique_id_from_parent(built):
+    out = _run(["uid"])
+    assert "rank 0 uid OK" in out and "rank 1 uid OK" in out
