@@ -143,7 +143,30 @@ struct EndpointConfig {
       : transport(transport), device(device), maxWriteQueueSize(maxWriteQueueSize) {}
 };
 
-class Context;  // core.hpp:470: accepted by Communicator's constructor, no state of its own here
+class Context;
+class Connection;
+class RegisteredMemory;
+
+// ---- endpoints and contexts (core.hpp:473-545) ----------------------------------------------------
+// An endpoint names one side of a connection: a transport and a device of one process on one host.
+class Endpoint {
+ public:
+  Endpoint() = default;
+  const EndpointConfig& config() const;
+  Transport transport() const;
+  const Device& device() const;  // the id resolved to a GPU index
+  uint64_t hostHash() const;
+  uint64_t pidHash() const;      // the owning process (a random per-process value, not the PID)
+  int maxWriteQueueSize() const;
+  std::vector<char> serialize() const;
+  static Endpoint deserialize(const std::vector<char>& data);
+  struct Impl;
+  explicit Endpoint(std::shared_ptr<Impl> impl) : pimpl_(std::move(impl)) {}
+  bool valid() const { return (bool)pimpl_; }
+
+ private:
+  std::shared_ptr<Impl> pimpl_;
+};
 
 // ---- registered memory (core.hpp:585-627) -------------------------------------------------------
 class RegisteredMemory {
@@ -192,6 +215,9 @@ class Connection {
   void flush(int64_t timeoutUsec = -1);
   Transport transport() const;
   Transport remoteTransport() const;
+  std::shared_ptr<Context> context() const;  // the context the connection was made in
+  const Device& localDevice() const;
+  int getMaxWriteQueueSize() const;
   int remoteRank() const;
   int tag() const;
   hipStream_t stream() const;  // the communicator's shared copy stream
@@ -204,12 +230,48 @@ class Connection {
   std::shared_ptr<Impl> pimpl_;
 };
 
+// The process-local half of the channel layer (core.hpp:497-545): registrations and connections made
+// without a communicator, e.g. between two GPUs driven by one process.  connect() needs both
+// endpoints on this host; the remote one may come from another process (Endpoint::deserialize).
+// Endpoints of two different GPUs of this process get peer access enabled between them.
+class Context : public std::enable_shared_from_this<Context> {
+ public:
+  static std::shared_ptr<Context> create();
+  ~Context();
+  RegisteredMemory registerMemory(void* ptr, size_t size, TransportFlags transports);
+  Endpoint createEndpoint(EndpointConfig config);
+  Connection connect(const Endpoint& localEndpoint, const Endpoint& remoteEndpoint);
+  struct Impl;
+
+ private:
+  Context();
+  std::unique_ptr<Impl> pimpl_;
+};
+
 // ---- semaphore (core.hpp:691-745) ---------------------------------------------------------------
+// One side's token of a semaphore over a connection (core.hpp:667-690): 8 bytes of uncached device
+// memory on the connection's GPU, registered so that it can travel (serialize) to the peer.
+class SemaphoreStub {
+ public:
+  explicit SemaphoreStub(const Connection& connection);
+  const RegisteredMemory& memory() const;
+  std::vector<char> serialize() const;
+  static SemaphoreStub deserialize(const std::vector<char>& data);
+  struct Impl;
+  explicit SemaphoreStub(std::shared_ptr<Impl> impl) : pimpl_(std::move(impl)) {}
+  const std::shared_ptr<Impl>& pimpl() const { return pimpl_; }
+
+ private:
+  std::shared_ptr<Impl> pimpl_;
+};
+
 // One 64-bit token per side in uncached device memory (semaphore.cc:32-43): localMemory() is the
 // token this rank waits on, remoteMemory() the peer's token as mapped here.
 class Semaphore {
  public:
   Semaphore() = default;
+  // The local stub's token is the one this side waits on, the remote stub's the one it signals.
+  Semaphore(const SemaphoreStub& localStub, const SemaphoreStub& remoteStub);
   Connection& connection();
   const Connection& connection() const;
   const RegisteredMemory& localMemory() const;
@@ -249,6 +311,8 @@ class Communicator {
   void sendMemory(RegisteredMemory memory, int remoteRank, int tag = 0);
   std::shared_future<RegisteredMemory> recvMemory(int remoteRank, int tag = 0);
   std::shared_future<Connection> connect(const EndpointConfig& localConfig, int remoteRank, int tag = 0);
+  std::shared_future<Connection> connect(const Endpoint& localEndpoint, int remoteRank, int tag = 0);
+  std::shared_ptr<Context> context();  // the context this communicator's connections live in
   std::shared_future<Semaphore> buildSemaphore(const Connection& connection, int remoteRank, int tag = 0);
   int remoteRankOf(const Connection& connection);
   int tagOf(const Connection& connection);
@@ -271,6 +335,7 @@ class Communicator {
   ncclComm_t comm_;
   bool owned_ = false;
   std::shared_ptr<Bootstrap> bootstrap_;
+  std::shared_ptr<Context> context_;
 };
 
 // ---- device handles (core.hpp:960-975) ----------------------------------------------------------

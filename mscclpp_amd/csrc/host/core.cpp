@@ -236,6 +236,8 @@ uint64_t allocationId(const void* ptr) {
 
 }  // namespace host
 
+static RegisteredMemory registerLocal(void* ptr, size_t size, TransportFlags transports, int rank);
+
 // ---- Bootstrap ------------------------------------------------------------------------------------
 void Bootstrap::send(const std::vector<char>& data, int peer, int tag) {
   uint64_t n = data.size();
@@ -392,6 +394,9 @@ struct Connection::Impl {
   int remoteRank = -1;
   int tag = 0;
   int device = 0;
+  Device localDevice{DeviceType::GPU, 0};
+  int maxWriteQueueSize = -1;
+  std::shared_ptr<Context> context;
   std::shared_ptr<SharedCopyStream> copy;
   hipStream_t stream = nullptr;  // copy->stream
   uint64_t* slots = nullptr;
@@ -453,6 +458,12 @@ Transport Connection::remoteTransport() const { return Transport::CudaIpc; }
 int Connection::remoteRank() const { return pimpl_ ? pimpl_->remoteRank : -1; }
 int Connection::tag() const { return pimpl_ ? pimpl_->tag : -1; }
 hipStream_t Connection::stream() const { return pimpl_ ? pimpl_->stream : nullptr; }
+std::shared_ptr<Context> Connection::context() const { return pimpl_ ? pimpl_->context : nullptr; }
+const Device& Connection::localDevice() const {
+  static const Device none{DeviceType::Unknown, -1};
+  return pimpl_ ? pimpl_->localDevice : none;
+}
+int Connection::getMaxWriteQueueSize() const { return pimpl_ ? pimpl_->maxWriteQueueSize : -1; }
 
 // ---- Semaphore ---------------------------------------------------------------------------------------
 struct Semaphore::Impl {
@@ -609,13 +620,18 @@ std::shared_ptr<Bootstrap> Communicator::bootstrap() {
 }
 
 RegisteredMemory Communicator::registerMemory(void* ptr, size_t size, TransportFlags transports) {
+  return registerLocal(ptr, size, transports, comm_->rank);
+}
+
+// A registration of this process's buffer; `rank` is the owner's rank (-1: made by a Context).
+static RegisteredMemory registerLocal(void* ptr, size_t size, TransportFlags transports, int rank) {
   if (!ptr || size == 0) throw Error("registerMemory: null or empty buffer", ErrorCode::InvalidUsage);
   auto impl = std::make_shared<RegisteredMemory::Impl>();
   impl->data = ptr;
   impl->original = (uint64_t)ptr;
   impl->size = size;
   impl->transports = transports;
-  impl->rank = comm_->rank;
+  impl->rank = rank;
   impl->pid = (int32_t)getpid();
   impl->owner = host::processNonce();
   {
@@ -697,7 +713,9 @@ std::shared_future<Connection> Communicator::connect(const EndpointConfig& local
       comm_->ipcStream = copy;
     }
   }
-  return std::async(std::launch::deferred, [boot, remoteRank, tag, device, copy] {
+  auto ctx = context();
+  const int maxWq = localConfig.maxWriteQueueSize;
+  return std::async(std::launch::deferred, [boot, remoteRank, tag, device, copy, ctx, maxWq] {
            EndpointWire peer{};
            boot->recv(&peer, (int)sizeof(peer), remoteRank, connTag(tag));
            if (peer.transport != (int32_t)Transport::CudaIpc)
@@ -706,6 +724,9 @@ std::shared_future<Connection> Communicator::connect(const EndpointConfig& local
            impl->remoteRank = remoteRank;
            impl->tag = tag;
            impl->device = device;
+           impl->localDevice = Device(DeviceType::GPU, device);
+           impl->maxWriteQueueSize = maxWq;
+           impl->context = ctx;
            int cur = 0;
            gpuCheck(hipGetDevice(&cur), "hipGetDevice");
            gpuCheck(hipSetDevice(device), "hipSetDevice");
@@ -717,6 +738,18 @@ std::shared_future<Connection> Communicator::connect(const EndpointConfig& local
            gpuCheck(hipSetDevice(cur), "hipSetDevice");
            return Connection(impl);
          }).share();
+}
+
+std::shared_future<Connection> Communicator::connect(const Endpoint& localEndpoint, int remoteRank, int tag) {
+  if (!localEndpoint.valid()) throw Error("connect: empty endpoint", ErrorCode::InvalidUsage);
+  if (localEndpoint.pidHash() != host::processNonce())
+    throw Error("connect: the local endpoint belongs to another process", ErrorCode::InvalidUsage);
+  return connect(localEndpoint.config(), remoteRank, tag);
+}
+
+std::shared_ptr<Context> Communicator::context() {
+  if (!context_) context_ = Context::create();
+  return context_;
 }
 
 int Communicator::remoteRankOf(const Connection& connection) { return connection.remoteRank(); }
@@ -829,5 +862,188 @@ MemoryDevice2DeviceSemaphore::DeviceHandle MemoryDevice2DeviceSemaphore::deviceH
 
 BaseMemoryChannel::BaseMemoryChannel(const Semaphore& semaphore)
     : semaphore_(std::make_shared<MemoryDevice2DeviceSemaphore>(semaphore)) {}
+
+
+// ---- Endpoint / Context / SemaphoreStub (core.hpp:473-690) --------------------------------------------
+namespace {
+constexpr uint32_t kEndpointMagic = 0x50444e45;  // "ENDP"
+struct EndpointWireV2 {
+  uint32_t magic;
+  int32_t transport, devType, devId, maxWriteQueueSize, pad;
+  uint64_t hostHash, pidHash;
+};
+uint64_t thisHostHash() {
+  static const uint64_t h = [] {
+    char name[256] = {};
+    (void)gethostname(name, sizeof(name) - 1);
+    uint64_t x = 1469598103934665603ull;
+    for (const char* c = name; *c; ++c) x = (x ^ (unsigned char)*c) * 1099511628211ull;
+    return x;
+  }();
+  return h;
+}
+}  // namespace
+
+struct Endpoint::Impl {
+  EndpointConfig config;
+  uint64_t hostHash = 0, pidHash = 0;
+};
+
+const EndpointConfig& Endpoint::config() const {
+  if (!pimpl_) throw Error("Endpoint: empty", ErrorCode::InvalidUsage);
+  return pimpl_->config;
+}
+Transport Endpoint::transport() const { return config().transport; }
+const Device& Endpoint::device() const { return config().device; }
+uint64_t Endpoint::hostHash() const { return pimpl_ ? pimpl_->hostHash : 0; }
+uint64_t Endpoint::pidHash() const { return pimpl_ ? pimpl_->pidHash : 0; }
+int Endpoint::maxWriteQueueSize() const { return config().maxWriteQueueSize; }
+
+std::vector<char> Endpoint::serialize() const {
+  const EndpointConfig& c = config();
+  EndpointWireV2 w{kEndpointMagic, (int32_t)c.transport, (int32_t)c.device.type, c.device.id, c.maxWriteQueueSize, 0,
+                   pimpl_->hostHash, pimpl_->pidHash};
+  return std::vector<char>((const char*)&w, (const char*)&w + sizeof(w));
+}
+
+Endpoint Endpoint::deserialize(const std::vector<char>& data) {
+  EndpointWireV2 w{};
+  if (data.size() != sizeof(w)) throw Error("Endpoint::deserialize: bad size", ErrorCode::InvalidUsage);
+  std::memcpy(&w, data.data(), sizeof(w));
+  if (w.magic != kEndpointMagic) throw Error("Endpoint::deserialize: not an endpoint", ErrorCode::InvalidUsage);
+  auto impl = std::make_shared<Endpoint::Impl>();
+  impl->config = EndpointConfig((Transport)w.transport, Device((DeviceType)w.devType, w.devId), w.maxWriteQueueSize);
+  impl->hostHash = w.hostHash;
+  impl->pidHash = w.pidHash;
+  return Endpoint(impl);
+}
+
+struct Context::Impl {
+  std::mutex mu;
+  std::map<int, std::shared_ptr<SharedCopyStream>> copy;  // per local GPU: the connections' copy stream
+};
+
+Context::Context() : pimpl_(std::make_unique<Impl>()) {}
+Context::~Context() = default;
+std::shared_ptr<Context> Context::create() { return std::shared_ptr<Context>(new Context()); }
+
+RegisteredMemory Context::registerMemory(void* ptr, size_t size, TransportFlags transports) {
+  return registerLocal(ptr, size, transports, -1);
+}
+
+Endpoint Context::createEndpoint(EndpointConfig config) {
+  if (config.transport != Transport::CudaIpc)
+    throw Error("createEndpoint: one MI355X node carries CudaIpc connections only", ErrorCode::InvalidUsage);
+  if (config.device.type != DeviceType::GPU)
+    throw Error("createEndpoint: CudaIpc endpoints are GPUs", ErrorCode::InvalidUsage);
+  if (config.device.id < 0) gpuCheck(hipGetDevice(&config.device.id), "hipGetDevice");
+  int n = 0;
+  gpuCheck(hipGetDeviceCount(&n), "hipGetDeviceCount");
+  if (config.device.id >= n) throw Error("createEndpoint: no GPU " + std::to_string(config.device.id), ErrorCode::InvalidUsage);
+  auto impl = std::make_shared<Endpoint::Impl>();
+  impl->config = config;
+  impl->hostHash = thisHostHash();
+  impl->pidHash = host::processNonce();
+  return Endpoint(impl);
+}
+
+Connection Context::connect(const Endpoint& localEndpoint, const Endpoint& remoteEndpoint) {
+  if (!localEndpoint.valid() || !remoteEndpoint.valid()) throw Error("connect: empty endpoint", ErrorCode::InvalidUsage);
+  if (localEndpoint.pidHash() != host::processNonce())
+    throw Error("connect: the local endpoint belongs to another process", ErrorCode::InvalidUsage);
+  if (localEndpoint.transport() != Transport::CudaIpc || remoteEndpoint.transport() != Transport::CudaIpc)
+    throw Error("connect: CudaIpc endpoints only", ErrorCode::InvalidUsage);
+  if (remoteEndpoint.hostHash() != localEndpoint.hostHash())
+    throw Error("connect: the remote endpoint is on another host (one node here)", ErrorCode::InvalidUsage);
+  const int dev = localEndpoint.device().id;
+  int cur = 0;
+  gpuCheck(hipGetDevice(&cur), "hipGetDevice");
+  gpuCheck(hipSetDevice(dev), "hipSetDevice");
+  auto restore = [&] { (void)hipSetDevice(cur); };
+  try {
+    const int rdev = remoteEndpoint.device().id;
+    if (remoteEndpoint.pidHash() == localEndpoint.pidHash() && rdev != dev) {
+      // two GPUs of this process: this GPU stores into the other's memory directly
+      const hipError_t e = hipDeviceEnablePeerAccess(rdev, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        throw Error(std::string("connect: peer access GPU ") + std::to_string(dev) + " -> " + std::to_string(rdev) +
+                        ": " + hipGetErrorString(e),
+                    ErrorCode::SystemError);
+      (void)hipGetLastError();
+    }
+    std::shared_ptr<SharedCopyStream> copy;
+    {
+      std::lock_guard<std::mutex> lk(pimpl_->mu);
+      auto& slot = pimpl_->copy[dev];
+      if (!slot) {
+        slot = std::make_shared<SharedCopyStream>();
+        gpuCheck(hipStreamCreateWithFlags(&slot->stream, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+      }
+      copy = slot;
+    }
+    auto impl = std::make_shared<Connection::Impl>();
+    impl->device = dev;
+    impl->localDevice = Device(DeviceType::GPU, dev);
+    impl->maxWriteQueueSize = localEndpoint.maxWriteQueueSize();
+    impl->context = shared_from_this();
+    impl->copy = copy;
+    impl->stream = copy->stream;
+    gpuCheck(hipHostMalloc((void**)&impl->slots, Connection::Impl::kSlots * sizeof(uint64_t), hipHostMallocDefault),
+             "hipHostMalloc");
+    restore();
+    return Connection(impl);
+  } catch (...) {
+    restore();
+    throw;
+  }
+}
+
+struct SemaphoreStub::Impl {
+  Connection connection;               // empty for a stub received from elsewhere
+  RegisteredMemory memory;             // the token
+  std::shared_ptr<void> tokenAlloc;    // the token's allocation (local stubs)
+};
+
+SemaphoreStub::SemaphoreStub(const Connection& connection) : pimpl_(std::make_shared<Impl>()) {
+  if (!connection.valid()) throw Error("SemaphoreStub: empty connection", ErrorCode::InvalidUsage);
+  const int dev = connection.localDevice().id;
+  int cur = 0;
+  gpuCheck(hipGetDevice(&cur), "hipGetDevice");
+  gpuCheck(hipSetDevice(dev), "hipSetDevice");
+  void* tok = nullptr;
+  try {
+    tok = host::allocUncached(64);  // semaphore.cc:32-43: the token in uncached memory on AMD
+  } catch (...) {
+    (void)hipSetDevice(cur);
+    throw;
+  }
+  (void)hipSetDevice(cur);
+  pimpl_->tokenAlloc = std::shared_ptr<void>(tok, [](void* p) { host::freeDevice(p); });
+  pimpl_->connection = connection;
+  pimpl_->memory = registerLocal(tok, sizeof(uint64_t), Transport::CudaIpc, -1);
+}
+
+const RegisteredMemory& SemaphoreStub::memory() const { return pimpl_->memory; }
+std::vector<char> SemaphoreStub::serialize() const { return pimpl_->memory.serialize(); }
+SemaphoreStub SemaphoreStub::deserialize(const std::vector<char>& data) {
+  auto impl = std::make_shared<Impl>();
+  impl->memory = RegisteredMemory::deserialize(data);
+  return SemaphoreStub(impl);
+}
+
+Semaphore::Semaphore(const SemaphoreStub& localStub, const SemaphoreStub& remoteStub) {
+  const auto& l = localStub.pimpl();
+  const auto& r = remoteStub.pimpl();
+  if (!l || !r || !l->connection.valid())
+    throw Error("Semaphore: the local stub must be made from a connection of this process", ErrorCode::InvalidUsage);
+  auto impl = std::make_shared<Semaphore::Impl>();
+  impl->connection = l->connection;
+  impl->local = l->memory;
+  impl->remote = r->memory;
+  impl->tokenAlloc = l->tokenAlloc;
+  impl->budget = host::spinBudgetTicks();
+  impl->err = nullptr;
+  pimpl_ = impl;
+}
 
 }  // namespace mscclpp_amd

@@ -1,6 +1,6 @@
 // The reference's user-level setup sequence, written only with its spellings (<mscclpp/...> headers,
 // namespace mscclpp, TcpBootstrap, Communicator(bootstrap), EndpointConfig{transport, {DeviceType,
-// id}}, GpuBuffer, DeviceSyncer), run on this library.  Three modes:
+// id}}, GpuBuffer, DeviceSyncer), run on this library.  Four modes:
 //
 //   local       one rank: a PortChannel from one GpuBuffer to another over a connection to itself,
 //               one workgroup writes and puts with a signal, another waits and checks
@@ -12,6 +12,11 @@
 //   uid         the parent creates a UniqueId (TcpBootstrap::createUniqueId); two forked ranks
 //               initialize with it, and their Communicators exchange a buffer through a memory
 //               channel
+//   context     one process, no communicator: Context::create, two endpoints (GPU 0 and GPU 1, or
+//               GPU 0 twice on a one-GPU box), Context::connect both ways, SemaphoreStub per side,
+//               Semaphore(localStub, remoteStub), BaseMemoryChannel -- and the relaxedSignal /
+//               relaxedWait ping-pong of examples/tutorials/01-basic-concepts, which must take at
+//               least the spin the waiting side adds per round, and leave both tokens at `iter`
 // Exit status 0 and "<mode> OK" on success.
 #include <hip/hip_runtime.h>
 #include <sys/wait.h>
@@ -272,6 +277,99 @@ static int uidWorker(int myRank, mscclpp::UniqueId id) {
   return 0;
 }
 
+// ---- context: two endpoints of this process ----------------------------------------------------------
+__device__ void spinTicks(uint64_t ticks) {  // s_memrealtime: 100 MHz
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+  }
+}
+
+__global__ void pingKernel0(mscclpp::BaseMemoryChannelDeviceHandle* h, int iter) {
+  if (threadIdx.x + blockIdx.x * blockDim.x == 0) {
+    for (int i = 0; i < iter; ++i) {
+      h->relaxedWait();
+      spinTicks(10000);  // 100 us
+      h->relaxedSignal();
+    }
+  }
+}
+
+__global__ void pingKernel1(mscclpp::BaseMemoryChannelDeviceHandle* h, int iter) {
+  if (threadIdx.x + blockIdx.x * blockDim.x == 0) {
+    for (int i = 0; i < iter; ++i) {
+      h->relaxedSignal();
+      h->relaxedWait();
+    }
+  }
+}
+
+static int runContext() {
+  int ndev = 0;
+  MSCCLPP_CUDATHROW(hipGetDeviceCount(&ndev));
+  const int dev0 = 0, dev1 = ndev > 1 ? 1 : 0;
+  const int iter = 50;
+  const mscclpp::Transport transport = mscclpp::Transport::CudaIpc;
+  auto ctx = mscclpp::Context::create();
+  mscclpp::Endpoint ep0 = ctx->createEndpoint({transport, {mscclpp::DeviceType::GPU, dev0}});
+  mscclpp::Endpoint ep1 = ctx->createEndpoint({transport, {mscclpp::DeviceType::GPU, dev1}});
+  // an endpoint survives a round trip through its wire form
+  const mscclpp::Endpoint ep1b = mscclpp::Endpoint::deserialize(ep1.serialize());
+  CHECK(ep1b.device().id == dev1 && ep1b.pidHash() == ep1.pidHash() && ep1b.hostHash() == ep0.hostHash());
+
+  mscclpp::Connection conn0 = ctx->connect(/*localEndpoint*/ ep0, /*remoteEndpoint*/ ep1b);
+  mscclpp::SemaphoreStub semaStub0(conn0);
+  mscclpp::Connection conn1 = ctx->connect(/*localEndpoint*/ ep1, /*remoteEndpoint*/ ep0);
+  mscclpp::SemaphoreStub semaStub1(conn1);
+  CHECK(conn0.context() == ctx && conn0.localDevice().id == dev0 && conn1.localDevice().id == dev1);
+
+  MSCCLPP_CUDATHROW(hipSetDevice(dev0));
+  mscclpp::Semaphore sema0(/*localSemaphoreStub*/ semaStub0, /*remoteSemaphoreStub*/ semaStub1);
+  mscclpp::BaseMemoryChannel memChan0(sema0);
+  mscclpp::BaseMemoryChannelDeviceHandle h0 = memChan0.deviceHandle();
+  auto d0 = mscclpp::detail::gpuCallocShared<mscclpp::BaseMemoryChannelDeviceHandle>();
+  mscclpp::gpuMemcpy(d0.get(), &h0, 1, hipMemcpyHostToDevice);
+  hipStream_t s0;
+  MSCCLPP_CUDATHROW(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+
+  MSCCLPP_CUDATHROW(hipSetDevice(dev1));
+  // the remote stub travels as bytes, as it would between processes
+  mscclpp::Semaphore sema1(semaStub1, mscclpp::SemaphoreStub::deserialize(semaStub0.serialize()));
+  mscclpp::BaseMemoryChannel memChan1(sema1);
+  mscclpp::BaseMemoryChannelDeviceHandle h1 = memChan1.deviceHandle();
+  auto d1 = mscclpp::detail::gpuCallocShared<mscclpp::BaseMemoryChannelDeviceHandle>();
+  mscclpp::gpuMemcpy(d1.get(), &h1, 1, hipMemcpyHostToDevice);
+  hipStream_t s1;
+  MSCCLPP_CUDATHROW(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+
+  MSCCLPP_CUDATHROW(hipSetDevice(dev0));
+  hipLaunchKernelGGL(pingKernel0, dim3(1), dim3(1), 0, s0, d0.get(), iter);
+  MSCCLPP_CUDATHROW(hipGetLastError());
+  MSCCLPP_CUDATHROW(hipSetDevice(dev1));
+  hipEvent_t start, end;
+  MSCCLPP_CUDATHROW(hipEventCreate(&start));
+  MSCCLPP_CUDATHROW(hipEventCreate(&end));
+  MSCCLPP_CUDATHROW(hipEventRecord(start, s1));
+  hipLaunchKernelGGL(pingKernel1, dim3(1), dim3(1), 0, s1, d1.get(), iter);
+  MSCCLPP_CUDATHROW(hipGetLastError());
+  MSCCLPP_CUDATHROW(hipEventRecord(end, s1));
+  MSCCLPP_CUDATHROW(hipEventSynchronize(end));
+  float ms = 0;
+  MSCCLPP_CUDATHROW(hipEventElapsedTime(&ms, start, end));
+  MSCCLPP_CUDATHROW(hipSetDevice(dev0));
+  MSCCLPP_CUDATHROW(hipStreamSynchronize(s0));
+  // every signal landed: each side's token counts the other's iter signals
+  uint64_t tok0 = 0, tok1 = 0;
+  MSCCLPP_CUDATHROW(hipMemcpy(&tok0, sema0.localMemory().data(), 8, hipMemcpyDeviceToHost));
+  MSCCLPP_CUDATHROW(hipMemcpy(&tok1, sema1.localMemory().data(), 8, hipMemcpyDeviceToHost));
+  const float perIter = ms / iter;
+  std::printf("context: %d rounds, %.3f ms per round, tokens %llu %llu (GPUs %d, %d)\n", iter, perIter,
+              (unsigned long long)tok0, (unsigned long long)tok1, dev0, dev1);
+  CHECK(tok0 == (uint64_t)iter && tok1 == (uint64_t)iter);
+  CHECK(perIter >= 0.09f);  // each round waited for the other side's 100 us spin
+  std::printf("context OK\n");
+  return 0;
+}
+
 static int forkPair(const std::function<int(int)>& worker, const char* name) {
   std::vector<pid_t> pids;
   for (int r = 0; r < 2; ++r) {
@@ -293,6 +391,7 @@ static int forkPair(const std::function<int(int)>& worker, const char* name) {
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "";
   if (mode == "local") return runLocal();
+  if (mode == "context") return runContext();
   if (mode == "pair" && argc > 2) {
     const std::string ipPort = std::string("127.0.0.1:") + argv[2];
     return forkPair([&](int r) { return pairWorker(r, ipPort); }, "pair");
@@ -303,6 +402,6 @@ int main(int argc, char** argv) {
     const mscclpp::UniqueId id = mscclpp::TcpBootstrap::createUniqueId();
     return forkPair([&](int r) { return uidWorker(r, id); }, "uid");
   }
-  std::fprintf(stderr, "usage: %s local | pair PORT | uid\n", argv[0]);
+  std::fprintf(stderr, "usage: %s local | pair PORT | uid | context\n", argv[0]);
   return 2;
 }

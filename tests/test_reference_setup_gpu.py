@@ -2,7 +2,8 @@
 TcpBootstrap + Communicator(bootstrap) + EndpointConfig{transport, {DeviceType, id}} + GpuBuffer +
 DeviceSyncer, on this library -- a PortChannel loopback on one rank (test/unit/local_channel_tests.cu),
 the memory-channel tutorial's put / get / packet round between two processes meeting at "ip:port"
-(examples/tutorials/03-memory-channel), and a UniqueId made in the parent."""
+(examples/tutorials/03-memory-channel), a UniqueId made in the parent, and the Context / Endpoint /
+SemaphoreStub ping-pong of examples/tutorials/01-basic-concepts in one process."""
 import os
 import socket
 import subprocess
@@ -41,3 +42,8 @@ def test_memory_channel_tutorial_ip_port(built):
 def test_unique_id_from_parent(built):
     out = _run(["uid"])
     assert "rank 0 uid OK" in out and "rank 1 uid OK" in out
+
+
+def test_context_endpoints_ping_pong(built):
+    out = _run(["context"])
+    assert "context OK" in out, out
