@@ -74,6 +74,12 @@ DataType dataTypeFromNccl(ncclDataType_t t);
 // The communicator handed to algorithms (the reference passes std::shared_ptr<mscclpp::Communicator>)
 // is mscclpp_amd::Communicator of core.hpp.
 
+// executor.hpp:15-18
+enum class PacketType {
+  LL8,   // 8-byte low-latency packet
+  LL16,  // 16-byte low-latency packet
+};
+
 class ExecutionPlan {
  public:
   ExecutionPlan(const std::string& planPath, int rank);  // executor.hpp:30; throws on a bad plan
@@ -91,14 +97,16 @@ class ExecutionPlan {
   mscclppAmdExecutionPlan_t plan_ = nullptr;
 };
 
+// executor.hpp:58-85.  execute() throws mscclpp_amd::Error on failure (the reference's behaviour);
+// the scratch the plans use comes from the communicator (defaultScratchBuffer is accepted and unused).
 class Executor {
  public:
-  explicit Executor(std::shared_ptr<Communicator> comm);  // executor.hpp:63-66 (collective)
+  explicit Executor(std::shared_ptr<Communicator> comm, std::shared_ptr<char> defaultScratchBuffer = nullptr);
   ~Executor();
   Executor(const Executor&) = delete;
   Executor& operator=(const Executor&) = delete;
-  CommResult execute(int rank, void* sendbuff, void* recvbuff, size_t sendBuffSize, size_t recvBuffSize,
-                     DataType dataType, const ExecutionPlan& plan, hipStream_t stream, bool ll16 = true);
+  void execute(int rank, void* sendbuff, void* recvBuff, size_t sendBuffSize, size_t recvBuffSize, DataType dataType,
+               const ExecutionPlan& plan, hipStream_t stream, PacketType packetType = PacketType::LL16);
   void reset();
 
  private:

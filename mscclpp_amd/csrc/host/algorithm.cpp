@@ -76,18 +76,24 @@ size_t ExecutionPlan::minMessageSize() const { return mscclppAmdExecutionPlanMin
 size_t ExecutionPlan::maxMessageSize() const { return mscclppAmdExecutionPlanMaxMessageSize(plan_); }
 bool ExecutionPlan::isInPlace() const { return mscclppAmdExecutionPlanIsInPlace(plan_) != 0; }
 
-Executor::Executor(std::shared_ptr<Communicator> comm) {
-  if (!comm || mscclppAmdExecutorCreate(comm->ncclComm(), &ex_) != 0)
-    throw std::runtime_error(std::string("Executor: ") + ncclGetLastError(nullptr));
+Executor::Executor(std::shared_ptr<Communicator> comm, std::shared_ptr<char>) {
+  if (!comm) throw Error("Executor: null communicator", ErrorCode::InvalidUsage);
+  if (mscclppAmdExecutorCreate(comm->ncclComm(), &ex_) != 0)
+    throw Error(std::string("Executor: ") + ncclGetLastError(nullptr), ErrorCode::InternalError);
 }
 Executor::~Executor() {
   if (ex_) (void)mscclppAmdExecutorDestroy(ex_);
 }
-CommResult Executor::execute(int rank, void* sendbuff, void* recvbuff, size_t sendBuffSize, size_t recvBuffSize,
-                             DataType dataType, const ExecutionPlan& plan, hipStream_t stream, bool ll16) {
-  return asResult(mscclppAmdExecutorExecute(ex_, rank, sendbuff, recvbuff, sendBuffSize, recvBuffSize, (int)dataType,
-                                            plan.handle(), (void*)stream,
-                                            ll16 ? MSCCLPP_AMD_PACKET_LL16 : MSCCLPP_AMD_PACKET_LL8));
+void Executor::execute(int rank, void* sendbuff, void* recvbuff, size_t sendBuffSize, size_t recvBuffSize,
+                       DataType dataType, const ExecutionPlan& plan, hipStream_t stream, PacketType packetType) {
+  const int r = mscclppAmdExecutorExecute(ex_, rank, sendbuff, recvbuff, sendBuffSize, recvBuffSize, (int)dataType,
+                                          plan.handle(), (void*)stream,
+                                          packetType == PacketType::LL16 ? MSCCLPP_AMD_PACKET_LL16 : MSCCLPP_AMD_PACKET_LL8);
+  if (r == ncclSuccess) return;
+  const ErrorCode code = r == ncclInvalidArgument || r == ncclInvalidUsage ? ErrorCode::InvalidUsage
+                         : r == ncclUnhandledCudaError || r == ncclSystemError ? ErrorCode::SystemError
+                                                                               : ErrorCode::ExecutorError;
+  throw Error(std::string("Executor::execute: ") + ncclGetLastError(nullptr), code);
 }
 void Executor::reset() { (void)mscclppAmdExecutorReset(ex_); }
 
@@ -153,8 +159,12 @@ CommResult DslAlgorithm::execute(std::shared_ptr<Communicator> comm, const void*
                                  const std::unordered_map<std::string, uintptr_t>&, DataType) {
   if (!executor) throw std::logic_error("Executor is null in DslAlgorithm::execute");  // algorithm.cc:178-180
   if (dtype == DataType::AUTO) return CommResult::CommInvalidArgument;  // the executor checks the rest
-  return executor->execute(comm->rank(), const_cast<void*>(input), output, inputSize, outputSize, dtype, *plan_,
-                           stream);
+  try {
+    executor->execute(comm->rank(), const_cast<void*>(input), output, inputSize, outputSize, dtype, *plan_, stream);
+  } catch (const Error& e) {
+    return e.getErrorCode() == ErrorCode::InvalidUsage ? CommResult::CommInvalidArgument : CommResult::CommInternalError;
+  }
+  return CommResult::CommSuccess;
 }
 
 // ---- CollectiveRequest / AlgorithmCollection ---------------------------------------------------

@@ -1,6 +1,6 @@
 // The reference's user-level setup sequence, written only with its spellings (<mscclpp/...> headers,
 // namespace mscclpp, TcpBootstrap, Communicator(bootstrap), EndpointConfig{transport, {DeviceType,
-// id}}, GpuBuffer, DeviceSyncer), run on this library.  Four modes:
+// id}}, GpuBuffer, DeviceSyncer), run on this library.  Five modes:
 //
 //   local       one rank: a PortChannel from one GpuBuffer to another over a connection to itself,
 //               one workgroup writes and puts with a signal, another waits and checks
@@ -17,6 +17,10 @@
 //               Semaphore(localStub, remoteStub), BaseMemoryChannel -- and the relaxedSignal /
 //               relaxedWait ping-pong of examples/tutorials/01-basic-concepts, which must take at
 //               least the spin the waiting side adds per round, and leave both tokens at `iter`
+//   executor PLAN   the sequence of test/executor_test.cc: a UniqueId from the parent, two ranks with
+//               TcpBootstrap + Communicator + Executor + ExecutionPlan(PLAN, rank) + GpuBuffer, an
+//               in-place fp16 AllReduce through Executor::execute with PacketType::LL16 and ::LL8,
+//               three calls each on fresh inputs whose sums are exact
 // Exit status 0 and "<mode> OK" on success.
 #include <hip/hip_runtime.h>
 #include <sys/wait.h>
@@ -31,6 +35,7 @@
 
 #include <mscclpp/concurrency_device.hpp>
 #include <mscclpp/core.hpp>
+#include <mscclpp/executor.hpp>
 #include <mscclpp/gpu_utils.hpp>
 #include <mscclpp/memory_channel.hpp>
 #include <mscclpp/memory_channel_device.hpp>
@@ -370,6 +375,58 @@ static int runContext() {
   return 0;
 }
 
+// ---- executor: the reference's executor_test sequence -------------------------------------------
+static int executorWorker(int rank, mscclpp::UniqueId id, const std::string& planPath) {
+  MSCCLPP_CUDATHROW(hipSetDevice(0));
+  const int worldSize = 2;
+  auto bootstrap = std::make_shared<mscclpp::TcpBootstrap>(rank, worldSize);
+  bootstrap->initialize(id);
+  auto communicator = std::make_shared<mscclpp::Communicator>(bootstrap);
+  auto executor = std::make_shared<mscclpp::Executor>(communicator);
+  mscclpp::ExecutionPlan plan(planPath, rank);
+  CHECK(plan.collective() == "allreduce" && plan.isInPlace());
+  const size_t count = 1 << 16, bufferSize = count * sizeof(_Float16);
+  std::shared_ptr<char> sendbuff = mscclpp::GpuBuffer(bufferSize).memory();
+  hipStream_t stream;
+  MSCCLPP_CUDATHROW(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  std::vector<_Float16> h(count), got(count);
+  int call = 0;
+  for (mscclpp::PacketType pt : {mscclpp::PacketType::LL16, mscclpp::PacketType::LL8}) {
+    for (int it = 0; it < 3; ++it, ++call) {
+      // small integers: every partial sum is exact in fp16, so any reduction order gives the same bits
+      for (size_t i = 0; i < count; ++i) h[i] = (_Float16)(float)((i * 7 + call * 3 + rank * 5) % 61);
+      mscclpp::gpuMemcpy(sendbuff.get(), (const char*)h.data(), bufferSize, hipMemcpyHostToDevice);
+      bootstrap->barrier();
+      executor->execute(rank, sendbuff.get(), sendbuff.get(), bufferSize, bufferSize, mscclpp::DataType::FLOAT16, plan,
+                        stream, pt);
+      MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+      mscclpp::gpuMemcpy((char*)got.data(), sendbuff.get(), bufferSize, hipMemcpyDeviceToHost);
+      size_t bad = 0;
+      for (size_t i = 0; i < count; ++i) {
+        float want = 0;
+        for (int r = 0; r < worldSize; ++r) want += (float)((i * 7 + call * 3 + r * 5) % 61);
+        bad += (float)got[i] != want;
+      }
+      if (bad) std::fprintf(stderr, "rank %d call %d: %zu of %zu wrong\n", rank, call, bad, count);
+      CHECK(bad == 0);
+      bootstrap->barrier();
+    }
+  }
+  // a bad argument is an exception, as in the reference
+  bool threw = false;
+  try {
+    executor->execute(rank, nullptr, nullptr, bufferSize, bufferSize, mscclpp::DataType::FLOAT16, plan, stream);
+  } catch (const mscclpp::Error& e) {
+    threw = e.getErrorCode() == mscclpp::ErrorCode::InvalidUsage;
+  }
+  CHECK(threw);
+  MSCCLPP_CUDATHROW(hipStreamDestroy(stream));
+  bootstrap->barrier();
+  std::printf("rank %d executor OK\n", rank);
+  std::fflush(stdout);
+  return 0;
+}
+
 static int forkPair(const std::function<int(int)>& worker, const char* name) {
   std::vector<pid_t> pids;
   for (int r = 0; r < 2; ++r) {
@@ -402,6 +459,11 @@ int main(int argc, char** argv) {
     const mscclpp::UniqueId id = mscclpp::TcpBootstrap::createUniqueId();
     return forkPair([&](int r) { return uidWorker(r, id); }, "uid");
   }
-  std::fprintf(stderr, "usage: %s local | pair PORT | uid | context\n", argv[0]);
+  if (mode == "executor" && argc > 2) {
+    const std::string planPath = argv[2];
+    const mscclpp::UniqueId id = mscclpp::TcpBootstrap::createUniqueId();
+    return forkPair([&](int r) { return executorWorker(r, id, planPath); }, "executor");
+  }
+  std::fprintf(stderr, "usage: %s local | pair PORT | uid | context | executor PLAN\n", argv[0]);
   return 2;
 }

@@ -47,3 +47,10 @@ def test_unique_id_from_parent(built):
 def test_context_endpoints_ping_pong(built):
     out = _run(["context"])
     assert "context OK" in out, out
+
+
+@pytest.mark.parametrize("plan", ["allreduce_packet.json", "allreduce.json"])
+def test_executor_api_reference_plans(built, plan):
+    """test/executor_test.cc's sequence on the reference's own 2-rank plans (fixtures)."""
+    out = _run(["executor", os.path.join(ROOT, "tests", "golden", "plans", "ref", plan)])
+    assert "rank 0 executor OK" in out and "rank 1 executor OK" in out, out
