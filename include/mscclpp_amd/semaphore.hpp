@@ -39,6 +39,24 @@ class Host2DeviceSemaphore {
   uint32_t* err_ = nullptr;
 };
 
+// Host2HostSemaphore (semaphore.hpp, semaphore.cc:169-214) pairs two CPU endpoints over a network
+// transport; the reference refuses it on CudaIpc (:173-175), the only transport of one MI355X node,
+// so here every constructor refuses it the same way (Error, InvalidUsage).
+class Host2HostSemaphore {
+ public:
+  explicit Host2HostSemaphore(const Semaphore&) { refuse(); }
+  Host2HostSemaphore(Communicator&, const Connection&) { refuse(); }
+  Connection& connection() { refuse(); }
+  void signal() { refuse(); }
+  bool poll() { refuse(); }
+  void wait(int64_t = 10000000) { refuse(); }
+
+ private:
+  [[noreturn]] static void refuse() {
+    throw Error("Host2HostSemaphore cannot be used with CudaIpc transport", ErrorCode::InvalidUsage);
+  }
+};
+
 class MemoryDevice2DeviceSemaphore {
  public:
   MemoryDevice2DeviceSemaphore(const Semaphore& semaphore, uint64_t budget = 0, uint32_t* err = nullptr);
