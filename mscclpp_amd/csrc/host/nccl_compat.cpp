@@ -11,8 +11,8 @@
 //    ncclGroupSimulateEnd, group calls, and AllReduce / AllGather / ReduceScatter / Broadcast for
 //    data types and operations this path does not carry or that
 //    MSCCLPP_AMD_FORCE_NCCL_FALLBACK_OPERATION (reference: MSCCLPP_FORCE_NCCL_FALLBACK_OPERATION,
-//    "all" or a comma list) forces there.  Without a vendor library they return ncclInvalidUsage
-//    (the reference returns ncclInternalError / ncclInvalidUsage for the same cases).
+//    "all" or a comma list) forces there.  Without a vendor library they return ncclInternalError,
+//    as the reference does for the same cases.
 #include <dlfcn.h>
 #include <sys/stat.h>
 
@@ -108,7 +108,7 @@ void initFallbackComm(ncclComm* c) {
   if (r != ncclSuccess) {
     // e.g. several ranks on one device, which the vendor library refuses: run without fallback
     warn("vendor NCCL communicator unavailable (code " + std::to_string((int)r) +
-         "); operations outside this path will return ncclInvalidUsage");
+         "); operations outside this path will return ncclInternalError");
     return;
   }
   c->fallback = fb;
@@ -134,10 +134,12 @@ using mscclpp_amd::host::vendorNccl;
 // The vendor communicator of `comm`, or null (no vendor library, or it refused this communicator).
 static inline ncclComm_t vendorComm(ncclComm_t comm) { return comm ? (ncclComm_t)comm->fallback : nullptr; }
 
+// The reference's answer for an operation it does not carry and cannot forward: ncclInternalError
+// with a warning (nccl.cc:521-542, :774-821, :840-844).
 static ncclResult_t unavailable(const char* what) {
   warn(std::string(what) + " is not carried by this path and no vendor NCCL library is configured "
                            "(set MSCCLPP_AMD_NCCL_LIB_PATH)");
-  return ncclInvalidUsage;
+  return ncclInternalError;
 }
 
 extern "C" {
@@ -258,6 +260,16 @@ ncclResult_t ncclAllToAllv(const void* sendbuff, const size_t sendcounts[], cons
                            const size_t recvcounts[], const size_t rdispls[], ncclDataType_t datatype, ncclComm_t comm,
                            void* stream) {
   if (!comm) return ncclInvalidArgument;
+  if (comm->nranks == 1) {  // nccl.cc:812-818: block 0 to block 0
+    return (ncclResult_t)guarded([&] {
+      if (!recvcounts || !sdispls || !rdispls) return (int)ncclInvalidArgument;
+      const size_t tb = ncclTypeBytes(datatype), bytes = recvcounts[0] * tb;
+      if (bytes)
+        HIPCHECK(hipMemcpyAsync((char*)recvbuff + rdispls[0] * tb, (const char*)sendbuff + sdispls[0] * tb, bytes,
+                                hipMemcpyDeviceToDevice, (hipStream_t)stream));
+      return (int)ncclSuccess;
+    });
+  }
   if (vendorComm(comm) && vendorNccl()->AllToAllv)
     return vendorNccl()->AllToAllv(sendbuff, sendcounts, sdispls, recvbuff, recvcounts, rdispls, datatype,
                                    vendorComm(comm), stream);

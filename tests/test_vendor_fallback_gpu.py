@@ -29,6 +29,10 @@ L.ncclReduce.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_size_t, ctypes.c_int, 
 assert L.ncclReduce(x.data_ptr(), y.data_ptr(), 1000, 8, 0, 0, c.comm, m.stream_ptr()) == 0
 torch.cuda.synchronize()
 assert torch.equal(x, y)
+if not v.value:  # no vendor library: what the path does not carry is ncclInternalError (nccl.cc:774-782)
+    L.ncclSend.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                           ctypes.c_void_p]
+    assert L.ncclSend(x.data_ptr(), 10, 8, 0, c.comm, m.stream_ptr()) == 3
 c.destroy()
 print("VENDOR", bool(v.value))
 """
