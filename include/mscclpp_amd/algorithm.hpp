@@ -110,6 +110,7 @@ class Executor {
   void reset();
 
  private:
+  std::shared_ptr<Communicator> comm_;  // kept alive for the executor's lifetime, as the reference does
   mscclppAmdExecutor_t ex_ = nullptr;
 };
 

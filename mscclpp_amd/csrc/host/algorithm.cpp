@@ -76,7 +76,7 @@ size_t ExecutionPlan::minMessageSize() const { return mscclppAmdExecutionPlanMin
 size_t ExecutionPlan::maxMessageSize() const { return mscclppAmdExecutionPlanMaxMessageSize(plan_); }
 bool ExecutionPlan::isInPlace() const { return mscclppAmdExecutionPlanIsInPlace(plan_) != 0; }
 
-Executor::Executor(std::shared_ptr<Communicator> comm, std::shared_ptr<char>) {
+Executor::Executor(std::shared_ptr<Communicator> comm, std::shared_ptr<char>) : comm_(comm) {
   if (!comm) throw Error("Executor: null communicator", ErrorCode::InvalidUsage);
   if (mscclppAmdExecutorCreate(comm->ncclComm(), &ex_) != 0)
     throw Error(std::string("Executor: ") + ncclGetLastError(nullptr), ErrorCode::InternalError);
