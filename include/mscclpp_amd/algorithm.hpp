@@ -275,6 +275,7 @@ class AlgorithmCollection {
   std::vector<std::shared_ptr<Algorithm>> getAllAlgorithms() const;
   void extend(const AlgorithmCollection& other);
   void setSelectors(AlgoSelectFunc algoSelector, AlgoSelectFunc fallbackAlgoSelector);
+  bool hasAlgorithmSelector() const { return (bool)algoSelector_; }  // a user's primary selector is set
 
  private:
   AlgoMapByCollective algoMapByCollective_;

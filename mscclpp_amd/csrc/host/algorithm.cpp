@@ -235,7 +235,9 @@ std::shared_ptr<Algorithm> builtin(ncclComm* comm, const std::string& name, cons
                                                const std::unordered_map<std::string, uintptr_t>&,
                                                DataType accum) -> CommResult {
     ncclComm* c = std::static_pointer_cast<BuiltinCtx>(ctx)->comm;
-    if (nBlocks <= 0 && nThreads <= 0) {  // the tuned launch shape of this algorithm, if any
+    if (nBlocks == kTunedShapeResolved) {  // the caller looked the tuned shape up already: defaults
+      nBlocks = 0;
+    } else if (nBlocks <= 0 && nThreads <= 0) {  // the tuned launch shape of this algorithm, if any
       std::string tuned;
       int nb = 0, nt = 0;
       const size_t msg = inSize;  // the request's messageSize for all three (nccl.cc:586, :697, :748)
@@ -271,17 +273,21 @@ std::shared_ptr<Algorithm> builtin(ncclComm* comm, const std::string& name, cons
                                            Algorithm::Constraint{comm->nranks, comm->nranks});
 }
 
+// MSCCLPP_AMD_ALGO, read once (the reference reads its environment once, env.cpp).
 const char* envAlgoName() {
-  const char* e = std::getenv("MSCCLPP_AMD_ALGO");
-  if (!e || !*e) return nullptr;
-  const std::string s(e);
-  if (s == "packet") return "default_allreduce_packet";
-  if (s == "allpair" || s == "allpair_packet") return "default_allreduce_allpair_packet";
-  if (s == "fullmesh") return "default_allreduce_fullmesh";
-  if (s == "rsag") return "default_allreduce_rsag";
-  if (s == "rsag_zc" || s == "rsag_zero_copy") return "default_allreduce_rsag_zero_copy";
-  if (s == "rsag_pipeline") return "default_allreduce_rsag_pipeline";
-  return nullptr;
+  static const char* const name = []() -> const char* {
+    const char* e = std::getenv("MSCCLPP_AMD_ALGO");
+    if (!e || !*e) return nullptr;
+    const std::string s(e);
+    if (s == "packet") return "default_allreduce_packet";
+    if (s == "allpair" || s == "allpair_packet") return "default_allreduce_allpair_packet";
+    if (s == "fullmesh") return "default_allreduce_fullmesh";
+    if (s == "rsag") return "default_allreduce_rsag";
+    if (s == "rsag_zc" || s == "rsag_zero_copy") return "default_allreduce_rsag_zero_copy";
+    if (s == "rsag_pipeline") return "default_allreduce_rsag_pipeline";
+    return nullptr;
+  }();
+  return name;
 }
 
 std::shared_ptr<Algorithm> lookup(const AlgoMapByCollective& m, const std::string& coll, const char* name) {

@@ -393,11 +393,48 @@ static int selectAndExecute(ncclComm_t comm, const char* collective, const void*
                             ncclRedOp_t op, void* stream) {
   using namespace mscclpp_amd;
   static const std::unordered_map<std::string, std::vector<uint64_t>> kNoHints;
-  const std::string coll(collective);
   const DataType dtype = dataTypeFromNccl(datatype);
-  CollectiveRequest req{comm->nranks, comm->nranks, comm->rank, sendbuff, recvbuff, messageSize,
-                        (hipStream_t)stream, coll, dtype, kNoHints};
-  auto algo = comm->algos->selectAlgorithm(req);
+  // With only the built-in selector the choice is a function of (collective, size, dtype) and the
+  // tuned store: memoise it, and the tuned shape with it (one store lookup per new key instead of
+  // two per call).  `collective` is one of this file's literals, so its address names it.
+  const bool memoOk = !comm->algos->hasAlgorithmSelector();
+  std::shared_ptr<Algorithm> algo;
+  int nb = 0, nt = 0;
+  if (memoOk) {
+    const uint64_t gen = tunedGeneration();
+    const size_t h = (messageSize * 0x9E3779B97F4A7C15ull) ^ ((size_t)collective >> 3) ^ (size_t)datatype;
+    std::lock_guard<std::mutex> lk(comm->selMu);
+    ncclComm::SelMemo& m = comm->selMemo[(h >> 7) % comm->selMemo.size()];
+    if (m.coll == collective && m.size == messageSize && m.dtype == (int)datatype && m.gen == gen && m.algo) {
+      algo = m.algo;
+      nb = m.nb;
+      nt = m.nt;
+    } else {
+      CollectiveRequest req{comm->nranks, comm->nranks, comm->rank, sendbuff, recvbuff, messageSize,
+                            (hipStream_t)stream, std::string(collective), dtype, kNoHints};
+      algo = comm->algos->selectAlgorithm(req);
+      if (algo) {
+        const auto& tags = algo->tags();
+        if (tags.find("default") != tags.end()) {  // a built-in: its tuned shape, resolved once here
+          std::string name;
+          int tb = 0, tt = 0;
+          if (tunedConfig(collective, comm->nranks, messageSize, name, tb, tt) && name == algo->name()) {
+            nb = tb;
+            nt = tt;
+          }
+          if (nb <= 0 && nt <= 0) {
+            nb = kTunedShapeResolved;
+            nt = 0;
+          }
+        }
+        m = ncclComm::SelMemo{collective, messageSize, (int)datatype, gen, algo, nb, nt};
+      }
+    }
+  } else {
+    CollectiveRequest req{comm->nranks, comm->nranks, comm->rank, sendbuff, recvbuff, messageSize,
+                          (hipStream_t)stream, std::string(collective), dtype, kNoHints};
+    algo = comm->algos->selectAlgorithm(req);
+  }
   if (!algo) {
     warn(std::string("no algorithm selected for ") + collective + " of " + std::to_string(messageSize) + " bytes");
     return ncclInvalidUsage;
@@ -405,7 +442,7 @@ static int selectAndExecute(ncclComm_t comm, const char* collective, const void*
   if (algo->type() == AlgorithmType::DSL && !comm->executor) comm->executor = std::make_shared<Executor>(comm->cxx);
   const ReduceOp rop = op == ncclSum ? SUM : op == ncclMin ? MIN : NOP;
   const int rc = (int)algo->execute(comm->cxx, sendbuff, recvbuff, inBytes, outBytes, dtype, rop, (hipStream_t)stream,
-                                    comm->executor);
+                                    comm->executor, nb, nt);
   if (rc != ncclSuccess)
     warn(std::string(collective) + " via " + algo->name() + " of " + std::to_string(messageSize) +
          " bytes failed with code " + std::to_string(rc) + " (HIP: " + hipGetErrorString(hipPeekAtLastError()) + ")");

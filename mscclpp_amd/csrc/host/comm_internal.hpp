@@ -201,17 +201,20 @@ inline size_t envMaxUserRegs() {
   return v > 0 ? (size_t)v : 1024;
 }
 
-inline int envAlgo() {
-  const char* e = std::getenv("MSCCLPP_AMD_ALGO");
-  if (!e) return MSCCLPP_AMD_ALGO_AUTO;
-  std::string s(e);
-  if (s == "packet") return MSCCLPP_AMD_ALGO_PACKET;
-  if (s == "allpair" || s == "allpair_packet") return MSCCLPP_AMD_ALGO_ALLPAIR;
-  if (s == "fullmesh") return MSCCLPP_AMD_ALGO_FULLMESH;
-  if (s == "rsag") return MSCCLPP_AMD_ALGO_RSAG;
-  if (s == "rsag_zc" || s == "rsag_zero_copy") return MSCCLPP_AMD_ALGO_RSAG_ZC;
-  if (s == "rsag_pipeline") return MSCCLPP_AMD_ALGO_RSAG_PIPELINE;
-  return MSCCLPP_AMD_ALGO_AUTO;
+inline int envAlgo() {  // MSCCLPP_AMD_ALGO, read once
+  static const int algo = [] {
+    const char* e = std::getenv("MSCCLPP_AMD_ALGO");
+    if (!e) return (int)MSCCLPP_AMD_ALGO_AUTO;
+    const std::string s(e);
+    if (s == "packet") return (int)MSCCLPP_AMD_ALGO_PACKET;
+    if (s == "allpair" || s == "allpair_packet") return (int)MSCCLPP_AMD_ALGO_ALLPAIR;
+    if (s == "fullmesh") return (int)MSCCLPP_AMD_ALGO_FULLMESH;
+    if (s == "rsag") return (int)MSCCLPP_AMD_ALGO_RSAG;
+    if (s == "rsag_zc" || s == "rsag_zero_copy") return (int)MSCCLPP_AMD_ALGO_RSAG_ZC;
+    if (s == "rsag_pipeline") return (int)MSCCLPP_AMD_ALGO_RSAG_PIPELINE;
+    return (int)MSCCLPP_AMD_ALGO_AUTO;
+  }();
+  return algo;
 }
 
 }  // namespace host
@@ -243,6 +246,11 @@ size_t pendingMappingReleases();
 uint64_t allocationId(const void* ptr);  // HIP_POINTER_ATTRIBUTE_BUFFER_ID (0 if unknown)
 // Tuned configuration (tuning.cpp) for a collective of `bytes` on `nranks` ranks of this device's
 // SKU: the algorithm name and launch shape (0 = the algorithm's default); false if none.
+// nBlocks value a built-in algorithm's caller passes when it has looked the tuned launch shape up
+// itself and found none: use the defaults without looking again.
+constexpr int kTunedShapeResolved = -2147483647;
+// Generation of the tuned-config store (changes whenever a file is loaded into it).
+uint64_t tunedGeneration();
 bool tunedConfig(const std::string& collective, int nranks, uint64_t bytes, std::string& algorithm, int& nblocks,
                  int& nthreads, std::string* source = nullptr);
 int algoCodeOf(const std::string& name);  // MSCCLPP_AMD_ALGO_* of a default_allreduce_* name, or -1
@@ -306,6 +314,20 @@ struct ncclComm {
   uint64_t* pipeSems = nullptr;      // rsag_pipeline's intra-launch counters (3 x 256 + done count)
   std::shared_ptr<mscclpp_amd::Executor> executor;
   void buildAlgorithms();
+  // Selection memo of the NCCL entry points (comm.cpp selectAndExecute): the built-in selector's
+  // choice and the tuned launch shape per (collective, message size, dtype), valid for one
+  // tuned-store generation.  Used only while no user selector is set: a user's selector is asked on
+  // every call, as the reference does.
+  struct SelMemo {
+    const char* coll = nullptr;
+    size_t size = 0;
+    int dtype = -1;
+    uint64_t gen = 0;
+    std::shared_ptr<mscclpp_amd::Algorithm> algo;
+    int nb = 0, nt = 0;
+  };
+  std::array<SelMemo, 16> selMemo{};
+  std::mutex selMu;
   int rank = 0, nranks = 1, device = 0;
   // LL scratch (two halves, packets), bulk scratch, semaphores, flags, error word
   void* llScratch = nullptr;
@@ -806,6 +828,7 @@ struct ncclComm {
 
   void destroy() {
     (void)hipDeviceSynchronize();
+    for (auto& m : selMemo) m = SelMemo();
     algos.reset();
     executor.reset();
     if (boot) {

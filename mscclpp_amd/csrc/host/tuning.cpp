@@ -17,6 +17,7 @@
 // 2 ranks in one launch, fabric-free).  MSCCLPP_AMD_TUNED_CONFIG names a file
 // whose profiles are consulted first (e.g. the `tuned_config` that bench.py prints after tuning on
 // the node); mscclppAmdTunedConfigLoad does the same at run time.
+#include <atomic>
 #include <fstream>
 #include <sstream>
 
@@ -114,6 +115,10 @@ const Entry* selectIn(const std::vector<Entry>& es, uint64_t size) {
   return &es[i - 1];
 }
 
+// Bumped whenever the store's contents change, so callers that memoise a decision taken from it
+// (comm.cpp's selection memo) know to take it again.
+std::atomic<uint64_t> gTunedGen{1};
+
 struct Store {
   std::mutex mu;
   std::vector<Profile> user, builtin;
@@ -140,6 +145,7 @@ Store& store() {
         std::stringstream ss;
         ss << f.rdbuf();
         s.user = parseStore(ss.str(), "tuned");
+        gTunedGen.fetch_add(1);
       } catch (const std::exception& e) {
         warn(std::string("MSCCLPP_AMD_TUNED_CONFIG ignored: ") + e.what());
       }
@@ -174,6 +180,11 @@ const Entry* selectProfiles(const std::vector<Profile>& ps, const std::string& s
 }
 
 }  // namespace
+
+uint64_t tunedGeneration() {
+  (void)store();  // the built-in table and MSCCLPP_AMD_TUNED_CONFIG are read on first use
+  return gTunedGen.load(std::memory_order_relaxed);
+}
 
 bool tunedConfig(const std::string& collective, int nranks, uint64_t bytes, std::string& algorithm, int& nblocks,
                  int& nthreads, std::string* source) {
@@ -213,6 +224,7 @@ extern "C" int mscclppAmdTunedConfigLoad(const char* path) {
     Store& s = store();
     std::lock_guard<std::mutex> lk(s.mu);
     s.user = std::move(parsed);
+    gTunedGen.fetch_add(1);
     return (int)ncclSuccess;
   });
 }

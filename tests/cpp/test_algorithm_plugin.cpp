@@ -112,8 +112,16 @@ static int runCpu() {
     auto s = c.selectAlgorithm(r);
     return s ? s->name() : std::string("null");
   };
+  // MSCCLPP_AMD_ALGO is read once per process (the reference reads its environment once): the test
+  // runs this program with it unset and with MSCCLPP_AMD_ALGO=packet
+  const char* forced = std::getenv("MSCCLPP_AMD_ALGO");
+  if (forced && std::string(forced) == "packet") {
+    CHECK(pick(1024, ar) == "default_allreduce_packet");
+    CHECK(pick(48 << 20, ar) == "default_allreduce_packet");
+    std::printf("forced OK\n");
+    return 0;
+  }
   // algorithm_selector.cc:107-131 (AMD): <=16 KiB allpair, <=1 MiB packet, larger fullmesh
-  unsetenv("MSCCLPP_AMD_ALGO");
   CHECK(pick(1024, ar) == "default_allreduce_allpair_packet");
   CHECK(pick(1 << 14, ar) == "default_allreduce_allpair_packet");
   CHECK(pick((1 << 14) + 2, ar) == "default_allreduce_packet");
@@ -121,9 +129,6 @@ static int runCpu() {
   CHECK(pick(48 << 20, ar) == "default_allreduce_fullmesh");
   CHECK(pick(1 << 20, ag) == "default_allgather_fullmesh2");
   CHECK(pick(1 << 20, "broadcast") == "null");
-  setenv("MSCCLPP_AMD_ALGO", "packet", 1);
-  CHECK(pick(48 << 20, ar) == "default_allreduce_packet");
-  unsetenv("MSCCLPP_AMD_ALGO");
   Probe u;
   c.registerAlgorithm("allreduce", "mine", probeAlgo("mine", "allreduce", &u));
   c.setSelectors(
