@@ -1,6 +1,6 @@
 // The reference's user-level setup sequence, written only with its spellings (<mscclpp/...> headers,
 // namespace mscclpp, TcpBootstrap, Communicator(bootstrap), EndpointConfig{transport, {DeviceType,
-// id}}, GpuBuffer, DeviceSyncer), run on this library.  Five modes:
+// id}}, GpuBuffer, DeviceSyncer), run on this library.  Six modes:
 //
 //   local       one rank: a PortChannel from one GpuBuffer to another over a connection to itself,
 //               one workgroup writes and puts with a signal, another waits and checks
@@ -17,6 +17,11 @@
 //               Semaphore(localStub, remoteStub), BaseMemoryChannel -- and the relaxedSignal /
 //               relaxedWait ping-pong of examples/tutorials/01-basic-concepts, which must take at
 //               least the spin the waiting side adds per round, and leave both tokens at `iter`
+//   port PORT   the port-channel tutorial (examples/tutorials/04-port-channel): ProxyService::addSemaphore
+//               of a Communicator-built semaphore, portChannel(semaId, remote, local), a one-thread
+//               kernel doing signal / wait / putWithSignal / wait captured 20 times into a HIP graph
+//               per size (1 KiB, 1 MiB, 16 MiB) with the proxy stopped during capture and restarted
+//               for the replays, the peer's half checked after each size
 //   executor PLAN   the sequence of test/executor_test.cc: a UniqueId from the parent, two ranks with
 //               TcpBootstrap + Communicator + Executor + ExecutionPlan(PLAN, rank) + GpuBuffer, an
 //               in-place fp16 AllReduce through Executor::execute with PacketType::LL16 and ::LL8,
@@ -375,6 +380,86 @@ static int runContext() {
   return 0;
 }
 
+// ---- port: the port-channel tutorial ----------------------------------------------------------------
+__global__ void bidirPortPutKernel(mscclpp::PortChannelDeviceHandle* h, size_t copyBytes, int myRank) {
+  if (threadIdx.x + blockIdx.x * blockDim.x == 0) {
+    h->signal();
+    h->wait();
+    const uint64_t off = myRank * copyBytes;
+    h->putWithSignal(off, off, copyBytes);
+    h->wait();
+  }
+}
+
+static int portWorker(int myRank, const std::string& ipPort) {
+  MSCCLPP_CUDATHROW(hipSetDevice(0));
+  int gpuId = 0;
+  MSCCLPP_CUDATHROW(hipGetDevice(&gpuId));
+  const int remoteRank = myRank ^ 1, nRanks = 2, iter = 20;
+  const mscclpp::Transport transport = mscclpp::Transport::CudaIpc;
+  const size_t maxBytes = 16 << 20;
+  auto bootstrap = std::make_shared<mscclpp::TcpBootstrap>(myRank, nRanks);
+  bootstrap->initialize(ipPort);
+  mscclpp::Communicator comm(bootstrap);
+  auto conn = comm.connect({transport, {mscclpp::DeviceType::GPU, gpuId}}, remoteRank).get();
+  auto sema = comm.buildSemaphore(conn, remoteRank).get();
+  mscclpp::GpuBuffer buffer(2 * maxBytes);
+  auto localRegMem = comm.registerMemory(buffer.data(), buffer.bytes(), transport);
+  comm.sendMemory(localRegMem, remoteRank);
+  auto remoteRegMem = comm.recvMemory(remoteRank).get();
+
+  mscclpp::ProxyService proxyService;
+  mscclpp::SemaphoreId semaId = proxyService.addSemaphore(sema);
+  mscclpp::MemoryId localMemId = proxyService.addMemory(localRegMem);
+  mscclpp::MemoryId remoteMemId = proxyService.addMemory(remoteRegMem);
+  mscclpp::PortChannel portChan = proxyService.portChannel(semaId, remoteMemId, localMemId);
+  auto handle = portChan.deviceHandle();
+  auto dev = mscclpp::detail::gpuCallocShared<mscclpp::PortChannelDeviceHandle>();
+  mscclpp::gpuMemcpy(dev.get(), &handle, 1, hipMemcpyHostToDevice);
+  hipStream_t stream;
+  MSCCLPP_CUDATHROW(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  int* buf = (int*)buffer.data();
+  int round = 0;
+  for (size_t copyBytes : {(size_t)1024, (size_t)1 << 20, maxBytes}) {
+    const size_t n = copyBytes / sizeof(int);
+    auto mine = pattern(myRank, n, 20 + round);
+    mscclpp::gpuMemcpy(buf + myRank * n, mine.data(), n, hipMemcpyHostToDevice);  // at myRank * copyBytes
+    MSCCLPP_CUDATHROW(hipDeviceSynchronize());
+    // the tutorial's sequence: capture with the proxy stopped, replay with it running
+    proxyService.startProxy();
+    hipGraph_t graph;
+    hipGraphExec_t graphExec;
+    MSCCLPP_CUDATHROW(hipStreamBeginCapture(stream, hipStreamCaptureModeGlobal));
+    for (int i = 0; i < iter; ++i)
+      hipLaunchKernelGGL(bidirPortPutKernel, dim3(1), dim3(1), 0, stream, dev.get(), copyBytes, myRank);
+    MSCCLPP_CUDATHROW(hipStreamEndCapture(stream, &graph));
+    MSCCLPP_CUDATHROW(hipGraphInstantiate(&graphExec, graph, nullptr, nullptr, 0));
+    proxyService.stopProxy();
+    MSCCLPP_CUDATHROW(hipDeviceSynchronize());
+    proxyService.startProxy();
+    bootstrap->barrier();
+    MSCCLPP_CUDATHROW(hipGraphLaunch(graphExec, stream));
+    MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+    proxyService.stopProxy();
+    bootstrap->barrier();
+    std::vector<int> got(n);
+    mscclpp::gpuMemcpy(got.data(), buf + remoteRank * n, n, hipMemcpyDeviceToHost);
+    const auto want = pattern(remoteRank, n, 20 + round);
+    size_t bad = 0;
+    for (size_t i = 0; i < n; ++i) bad += got[i] != want[i];
+    if (bad) std::fprintf(stderr, "rank %d port %zu bytes: %zu of %zu words wrong\n", myRank, copyBytes, bad, n);
+    CHECK(bad == 0);
+    MSCCLPP_CUDATHROW(hipGraphExecDestroy(graphExec));
+    MSCCLPP_CUDATHROW(hipGraphDestroy(graph));
+    ++round;
+  }
+  MSCCLPP_CUDATHROW(hipStreamDestroy(stream));
+  bootstrap->barrier();
+  std::printf("rank %d port OK\n", myRank);
+  std::fflush(stdout);
+  return 0;
+}
+
 // ---- executor: the reference's executor_test sequence -------------------------------------------
 static int executorWorker(int rank, mscclpp::UniqueId id, const std::string& planPath) {
   MSCCLPP_CUDATHROW(hipSetDevice(0));
@@ -459,11 +544,15 @@ int main(int argc, char** argv) {
     const mscclpp::UniqueId id = mscclpp::TcpBootstrap::createUniqueId();
     return forkPair([&](int r) { return uidWorker(r, id); }, "uid");
   }
+  if (mode == "port" && argc > 2) {
+    const std::string ipPort = std::string("127.0.0.1:") + argv[2];
+    return forkPair([&](int r) { return portWorker(r, ipPort); }, "port");
+  }
   if (mode == "executor" && argc > 2) {
     const std::string planPath = argv[2];
     const mscclpp::UniqueId id = mscclpp::TcpBootstrap::createUniqueId();
     return forkPair([&](int r) { return executorWorker(r, id, planPath); }, "executor");
   }
-  std::fprintf(stderr, "usage: %s local | pair PORT | uid | context | executor PLAN\n", argv[0]);
+  std::fprintf(stderr, "usage: %s local | pair PORT | uid | context | port PORT | executor PLAN\n", argv[0]);
   return 2;
 }

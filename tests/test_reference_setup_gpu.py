@@ -39,6 +39,11 @@ def test_memory_channel_tutorial_ip_port(built):
     assert "rank 0 pair OK" in out and "rank 1 pair OK" in out and "pair OK" in out
 
 
+def test_port_channel_tutorial_graph_replays(built):
+    out = _run(["port", str(_free_port())])
+    assert "rank 0 port OK" in out and "rank 1 port OK" in out, out
+
+
 def test_unique_id_from_parent(built):
     out = _run(["uid"])
     assert "rank 0 uid OK" in out and "rank 1 uid OK" in out
