@@ -11,8 +11,13 @@
 // Built by oracle/build_ref.sh into oracle/_ref/libref.so; used only by tests/.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstring>
+#include <vector>
+
 #include <mscclpp/copy_device.hpp>
 #include <mscclpp/gpu_data_types.hpp>
+#include <mscclpp/memory_channel_device.hpp>
 #include <mscclpp/packet_device.hpp>
 
 using namespace mscclpp;
@@ -208,6 +213,114 @@ int refB15Convert(const float* in, size_t n, uint8_t* enc, uint8_t* encX4, float
   hipLaunchKernelGGL(refB15ConvertKernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream, in, n, enc,
                      encX4, dec, decX4);
   return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// ---- the reference's own LL16 two-hop AllReduce kernel, run as n ranks on one GPU ------------------
+// python/mscclpp_benchmark/allreduce.cu:223-289 (allreduce2; the same algorithm and scratch layout as
+// test/mscclpp-test/allreduce_test.cu:972-1034 allreduce6), compiled where it lies by build_ref.sh into
+// oracle/_ref/bench_allreduce_int.hsaco with TYPE=int.  Each rank loads its own copy of the code object,
+// so each has its own `globalFlag` (initially 1, bumped once per call, as in one process per GPU).  The
+// kernel spins on packets from the other ranks, so all n launches must be resident together: one stream
+// per rank, and the caller runs with GPU_MAX_HW_QUEUES > n so no two streams share a hardware queue.
+struct RefBench2 {
+  int n = 0;
+  std::vector<hipModule_t> mod;
+  std::vector<hipFunction_t> fn;
+  std::vector<hipStream_t> stream;
+  std::vector<MemoryChannelDeviceHandle*> chans;  // device, n - 1 per rank
+};
+
+void* refBench2Open(const char* hsaco, int n) {
+  if (n < 2 || n > 8) return nullptr;
+  auto* h = new RefBench2;
+  h->n = n;
+  h->mod.resize(n);
+  h->fn.resize(n);
+  h->stream.resize(n);
+  h->chans.resize(n);
+  for (int r = 0; r < n; ++r) {
+    if (hipModuleLoad(&h->mod[r], hsaco) != hipSuccess ||
+        hipModuleGetFunction(&h->fn[r], h->mod[r], "allreduce2") != hipSuccess ||
+        hipStreamCreateWithFlags(&h->stream[r], hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&h->chans[r], sizeof(MemoryChannelDeviceHandle) * (n - 1)) != hipSuccess)
+      return nullptr;
+  }
+  return h;
+}
+
+// Packet scratch the way the reference allocates it on AMD (GpuBuffer -> hipExtMallocWithFlags with
+// hipDeviceMallocUncached, src/core/gpu_utils.cc): the ranks' kernels run on different XCDs, whose
+// L2s do not see each other's writes to ordinary (coarse-grained) device memory.  Zero-filled.
+void* refMallocUncached(uint64_t bytes) {
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  return p;
+}
+
+void refFree(void* p) { (void)hipFree(p); }
+
+void refBench2Close(void* handle) {
+  auto* h = static_cast<RefBench2*>(handle);
+  if (!h) return;
+  for (int r = 0; r < h->n; ++r) {
+    if (h->chans[r]) (void)hipFree(h->chans[r]);
+    if (h->stream[r]) (void)hipStreamDestroy(h->stream[r]);
+    if (h->mod[r]) (void)hipModuleUnload(h->mod[r]);
+  }
+  delete h;
+}
+
+// One AllReduce call on every rank.  bufs/scratch/results: n device pointers each (scratch zeroed by
+// the caller before the first call, 4 * nelems / 2 LL16 packets); nelems ints per rank.  Returns 0,
+// 4 on a shape the kernel cannot take (it would index past its channel array or split a packet), 1 on
+// a HIP error, 2 if the ranks have not finished after timeoutMs.
+int refBench2Run(void* handle, void* const* bufs, void* const* scratch, void* const* results, uint64_t nelems,
+                 int blocksPerPeer, int threads, int timeoutMs) {
+  auto* h = static_cast<RefBench2*>(handle);
+  if (!h) return 1;
+  const int n = h->n, nPeers = n - 1;
+  if (nelems == 0 || nelems % (2 * (uint64_t)n) != 0 || nelems > (1ull << 30) || blocksPerPeer < 1 ||
+      blocksPerPeer * nPeers > 64 || threads < 64 || threads > 1024 || threads % 64 != 0)
+    return 4;
+  for (int r = 0; r < n; ++r) {
+    std::vector<MemoryChannelDeviceHandle> hc(nPeers);
+    for (int p = 0; p < nPeers; ++p) {
+      const int remote = p < r ? p : p + 1;
+      std::memset(static_cast<void*>(&hc[p]), 0, sizeof(hc[p]));
+      hc[p].dst_ = scratch[remote];
+      hc[p].src_ = bufs[r];
+      hc[p].packetBuffer_ = scratch[r];
+    }
+    if (hipMemcpy(h->chans[r], hc.data(), sizeof(hc[0]) * nPeers, hipMemcpyHostToDevice) != hipSuccess) return 1;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  for (int r = 0; r < n; ++r) {
+    MemoryChannelDeviceHandle* c = h->chans[r];
+    void* buff = bufs[r];
+    void* scr = scratch[r];
+    void* res = results[r];
+    int rank = r, world = n;
+    size_t ne = nelems;
+    void* args[] = {&c, &buff, &scr, &res, &rank, &world, &ne};
+    if (hipModuleLaunchKernel(h->fn[r], blocksPerPeer * nPeers, 1, 1, threads, 1, 1, 0, h->stream[r], args,
+                              nullptr) != hipSuccess)
+      return 1;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int r = 0; r < n;) {
+    const hipError_t e = hipStreamQuery(h->stream[r]);
+    if (e == hipSuccess) {
+      ++r;
+      continue;
+    }
+    if (e != hipErrorNotReady) return 1;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) return 2;
+  }
+  return 0;
 }
 
 }  // extern "C"

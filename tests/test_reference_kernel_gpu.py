@@ -1,0 +1,43 @@
+"""Kernel-level reference pin: the reference's OWN LL16 two-hop AllReduce kernel
+-- python/mscclpp_benchmark/allreduce.cu:223-289 allreduce2, the algorithm and scratch layout of
+test/mscclpp-test/allreduce_test.cu:972-1034 allreduce6 -- compiled from the reference source where it
+lies (oracle/build_ref.sh -> oracle/_ref/bench_allreduce_int.hsaco, TYPE=int) and run as n ranks on one
+GPU (one code object and one stream per rank, channels holding the peers' plain scratch pointers).
+
+On the same inputs, for three calls (flag 1, 2, 3: both double-buffer halves and a wrap back), the
+reference kernel's outputs equal this library's k6 and the CPU oracle's restatement bit for bit, and
+after the first call every rank's whole packet scratch image (input packets, reduced-result packets,
+flag words) is identical across all three.  This pins the oracle (tests/oracle_lib.py
+mscclpp_test_ll) on the reference's own device code, not only on its host-side fixtures.
+
+The worker runs in its own process because the ranks spin on each other's packets: it sets
+GPU_MAX_HW_QUEUES above n before HIP starts, so no two rank streams share a hardware queue."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+HSACO = os.path.join(ROOT, "oracle", "_ref", "bench_allreduce_int.hsaco")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref.so")
+
+# (ranks, int32 elements per rank, blocks per peer, threads per block); count % (2 n) == 0
+CASES = [(2, 4096, 2, 1024), (3, 1536, 4, 256), (4, 8192, 2, 512), (8, 6144, 1, 1024), (8, 65536, 4, 1024),
+         (8, 16, 1, 64)]
+
+
+def test_reference_allreduce2_matches_k6_and_oracle(built):
+    if not (os.path.exists(HSACO) and os.path.exists(REF_SO)):
+        pytest.skip("oracle/_ref not built (needs /root/reference at build time)")
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "ref_kernel_worker.py"), json.dumps(CASES)],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=150, env=env, cwd=ROOT)
+    assert r.returncode == 0 and "WORKER OK" in r.stdout, r.stdout[-4000:]
+    recs = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert [(x["n"], x["count"]) for x in recs] == [(c[0], c[1]) for c in CASES]
+    assert all(x["calls"] == 3 and x["scratch_words_compared"] == x["n"] * 8 * x["count"] for x in recs)
