@@ -221,31 +221,87 @@ int refB15Convert(const float* in, size_t n, uint8_t* enc, uint8_t* encX4, float
 // oracle/_ref/bench_allreduce_int.hsaco with TYPE=int.  Each rank loads its own copy of the code object,
 // so each has its own `globalFlag` (initially 1, bumped once per call, as in one process per GPU).  The
 // kernel spins on packets from the other ranks, so all n launches must be resident together: one stream
-// per rank, and the caller runs with GPU_MAX_HW_QUEUES > n so no two streams share a hardware queue.
+// per rank, and the caller runs with GPU_MAX_HW_QUEUES > 8 so no two streams share a hardware queue.
 struct RefBench2 {
   int n = 0;
   std::vector<hipModule_t> mod;
   std::vector<hipFunction_t> fn;
-  std::vector<hipStream_t> stream;
   std::vector<MemoryChannelDeviceHandle*> chans;  // device, n - 1 per rank
 };
 
+// One stream per rank for the process's life (so cases do not churn hardware queues), each made to
+// own its queue before the first real launch (a queue is created at a stream's first submission);
+// plus a stream for diagnostics that never waits behind a spinning rank.
+static hipStream_t gRankStream[8];
+static hipStream_t gDiagStream;
+
+static bool rankStreams() {
+  if (gDiagStream) return true;
+  for (auto& s : gRankStream) {
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return false;
+    hipLaunchKernelGGL((refReduceKernel<3, 0>), dim3(1), dim3(64), 0, s, nullptr, nullptr, (size_t)0);
+    if (hipGetLastError() != hipSuccess) return false;
+  }
+  if (hipStreamCreateWithFlags(&gDiagStream, hipStreamNonBlocking) != hipSuccess) return false;
+  return hipDeviceSynchronize() == hipSuccess;
+}
+
 void* refBench2Open(const char* hsaco, int n) {
-  if (n < 2 || n > 8) return nullptr;
+  if (n < 2 || n > 8 || !rankStreams()) return nullptr;
   auto* h = new RefBench2;
   h->n = n;
   h->mod.resize(n);
   h->fn.resize(n);
-  h->stream.resize(n);
   h->chans.resize(n);
   for (int r = 0; r < n; ++r) {
     if (hipModuleLoad(&h->mod[r], hsaco) != hipSuccess ||
         hipModuleGetFunction(&h->fn[r], h->mod[r], "allreduce2") != hipSuccess ||
-        hipStreamCreateWithFlags(&h->stream[r], hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&h->chans[r], sizeof(MemoryChannelDeviceHandle) * (n - 1)) != hipSuccess)
       return nullptr;
   }
+  // distinct modules must hold distinct globalFlag words (one per rank, as one per process)
+  std::vector<void*> flags(n);
+  for (int r = 0; r < n; ++r) {
+    size_t bytes = 0;
+    if (hipModuleGetGlobal(reinterpret_cast<hipDeviceptr_t*>(&flags[r]), &bytes, h->mod[r], "globalFlag") !=
+            hipSuccess ||
+        bytes != sizeof(uint64_t))
+      return nullptr;
+    for (int q = 0; q < r; ++q)
+      if (flags[q] == flags[r]) return nullptr;
+  }
   return h;
+}
+
+// After a timeout: which ranks' launches finished (done[r]) and each rank's globalFlag (flags[r]),
+// read on the diagnostic stream while the others may still spin.  0 on success.
+int refBench2Diag(void* handle, int* done, uint64_t* flags) {
+  auto* h = static_cast<RefBench2*>(handle);
+  if (!h) return 1;
+  uint64_t* pinned = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&pinned), sizeof(uint64_t) * h->n, hipHostMallocDefault) != hipSuccess)
+    return 1;
+  int rc = 0;
+  for (int r = 0; r < h->n && rc == 0; ++r) {
+    done[r] = hipStreamQuery(gRankStream[r]) == hipSuccess;
+    void* g = nullptr;
+    size_t bytes = 0;
+    if (hipModuleGetGlobal(reinterpret_cast<hipDeviceptr_t*>(&g), &bytes, h->mod[r], "globalFlag") != hipSuccess ||
+        hipMemcpyAsync(pinned + r, g, sizeof(uint64_t), hipMemcpyDeviceToHost, gDiagStream) != hipSuccess)
+      rc = 1;
+  }
+  if (rc == 0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hipStreamQuery(gDiagStream) == hipErrorNotReady)
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        rc = 2;
+        break;
+      }
+  }
+  if (rc == 0)
+    for (int r = 0; r < h->n; ++r) flags[r] = pinned[r];
+  if (rc != 2) (void)hipHostFree(pinned);  // a copy still in flight keeps its target
+  return rc;
 }
 
 // Packet scratch the way the reference allocates it on AMD (GpuBuffer -> hipExtMallocWithFlags with
@@ -268,7 +324,6 @@ void refBench2Close(void* handle) {
   if (!h) return;
   for (int r = 0; r < h->n; ++r) {
     if (h->chans[r]) (void)hipFree(h->chans[r]);
-    if (h->stream[r]) (void)hipStreamDestroy(h->stream[r]);
     if (h->mod[r]) (void)hipModuleUnload(h->mod[r]);
   }
   delete h;
@@ -306,13 +361,13 @@ int refBench2Run(void* handle, void* const* bufs, void* const* scratch, void* co
     int rank = r, world = n;
     size_t ne = nelems;
     void* args[] = {&c, &buff, &scr, &res, &rank, &world, &ne};
-    if (hipModuleLaunchKernel(h->fn[r], blocksPerPeer * nPeers, 1, 1, threads, 1, 1, 0, h->stream[r], args,
+    if (hipModuleLaunchKernel(h->fn[r], blocksPerPeer * nPeers, 1, 1, threads, 1, 1, 0, gRankStream[r], args,
                               nullptr) != hipSuccess)
       return 1;
   }
   const auto t0 = std::chrono::steady_clock::now();
   for (int r = 0; r < n;) {
-    const hipError_t e = hipStreamQuery(h->stream[r]);
+    const hipError_t e = hipStreamQuery(gRankStream[r]);
     if (e == hipSuccess) {
       ++r;
       continue;

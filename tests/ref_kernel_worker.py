@@ -29,6 +29,7 @@ def _lib():
     L.refBench2Open.argtypes = [ctypes.c_char_p, ctypes.c_int]
     L.refBench2Open.restype = vp
     L.refBench2Close.argtypes = [vp]
+    L.refBench2Diag.argtypes = [vp, vp, vp]
     L.refBench2Run.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.refBench2Run.restype = ctypes.c_int
     L.refMallocUncached.argtypes = [ctypes.c_uint64]
@@ -61,6 +62,15 @@ def run_case(L, m, n, count, blocks_per_peer, threads):
             rout = [torch.zeros_like(d) for d in dins]
             torch.cuda.synchronize()
             rc = L.refBench2Run(h, _ptrs(dins), _ptrs(rscr), _ptrs(rout), count, blocks_per_peer, threads, 20000)
+            if rc == 2:  # ranks still spinning: say which and with what flag, then leave without waiting
+                done, flags = (ctypes.c_int * n)(), (ctypes.c_uint64 * n)()
+                drc = L.refBench2Diag(h, done, flags)
+                print(json.dumps({"timeout": rec, "call": call, "diag_rc": drc, "done": list(done),
+                                  "globalFlag": list(flags)}), flush=True)
+                import subprocess
+                ps = subprocess.run(["ps", "-eo", "pid,ppid,etimes,stat,cmd"], stdout=subprocess.PIPE, text=True)
+                print("\n".join(x[:200] for x in ps.stdout.splitlines() if "python" in x or "PID" in x), flush=True)
+                os._exit(3)
             assert rc == 0, f"refBench2Run returned {rc}"
             douts = [torch.zeros_like(d) for d in dins]
             ours.all_reduce(dins, douts, m.ALGO_TEST_K6)

@@ -11,7 +11,7 @@ flag words) is identical across all three.  This pins the oracle (tests/oracle_l
 mscclpp_test_ll) on the reference's own device code, not only on its host-side fixtures.
 
 The worker runs in its own process because the ranks spin on each other's packets: it sets
-GPU_MAX_HW_QUEUES above n before HIP starts, so no two rank streams share a hardware queue."""
+GPU_MAX_HW_QUEUES above 8 before HIP starts, so no two rank streams share a hardware queue."""
 import json
 import os
 import subprocess
