@@ -43,6 +43,26 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0xFFFFFFFF, 0x00020000);
 }
 
+// A lane's strided walk over n units of Unit bytes (i = tid, tid + nthreads, ...) through buffer
+// resources, whose offsets are 32 bits: f(i, w0, off) with off = (i - w0) * Unit, the byte offset
+// of unit i from unit w0, where the caller's resources start.  Up to 4 GiB (every bucket in
+// practice) w0 is 0 throughout and the caller's resources are loop-invariant; beyond, the walk goes
+// window by window of 2 GiB with w0 the window's first unit (uniform across the wave), so a buffer
+// of any size is addressed exactly as the reference's 64-bit pointer arithmetic addresses it.
+template <uint32_t Unit, typename F>
+__device__ __forceinline__ void for_each_strided(uint64_t n, uint64_t tid, uint64_t nthreads, F&& f) {
+  if (n * Unit <= 0xFFFFFFFFull) {
+    for (uint64_t i = tid; i < n; i += nthreads) f(i, (uint64_t)0, (uint32_t)(i * Unit));
+    return;
+  }
+  constexpr uint64_t kWindowUnits = (1ull << 31) / Unit;
+  for (uint64_t w0 = 0; w0 < n; w0 += kWindowUnits) {
+    const uint64_t w1 = n - w0 < kWindowUnits ? n : w0 + kWindowUnits;
+    uint64_t i = tid >= w0 ? tid : tid + (w0 - tid + nthreads - 1) / nthreads * nthreads;
+    for (; i < w1; i += nthreads) f(i, w0, (uint32_t)((i - w0) * Unit));
+  }
+}
+
 template <int Policy>
 __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, Policy);

@@ -92,13 +92,14 @@ struct MemoryChannelDeviceHandle : public BaseMemoryChannelDeviceHandle {
     static_assert(sizeof(PacketType) == 16 || sizeof(PacketType) == 8, "Unsupported packet type");
     char* dst = reinterpret_cast<char*>(dst_) + targetOffset;
     const uint32_t* s = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(src_) + originOffset);
-    const auto r = make_rsrc(dst);
     if constexpr (sizeof(PacketType) == 16) {
-      for (uint64_t i = threadId; i < originBytes / 8; i += numThreads)
-        store16<kSystem>(r, (uint32_t)(i * 16), LL16Packet::make(s[2 * i], s[2 * i + 1], flag));
+      for_each_strided<16>(originBytes / 8, threadId, numThreads, [&](uint64_t i, uint64_t w0, uint32_t off) {
+        store16<kSystem>(make_rsrc(dst + w0 * 16), off, LL16Packet::make(s[2 * i], s[2 * i + 1], flag));
+      });
     } else {
-      for (uint64_t i = threadId; i < originBytes / 4; i += numThreads)
-        store8<kSystem>(r, (uint32_t)(i * 8), u32x2{s[i], flag});
+      for_each_strided<8>(originBytes / 4, threadId, numThreads, [&](uint64_t i, uint64_t w0, uint32_t off) {
+        store8<kSystem>(make_rsrc(dst + w0 * 8), off, u32x2{s[i], flag});
+      });
     }
   }
   template <typename PacketType = LL16Packet>
@@ -124,15 +125,15 @@ struct MemoryChannelDeviceHandle : public BaseMemoryChannelDeviceHandle {
     (void)maxSpinCount;
     uint32_t* d = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(src_) + originOffset);
     const char* pk = reinterpret_cast<const char*>(packetBuffer_) + targetOffset;
-    const auto r = make_rsrc(pk);
     const uint64_t budget = semaphore_.budget ? semaphore_.budget : kDefaultSpinTicks;
     if constexpr (sizeof(PacketType) == 16) {
-      for (uint64_t i = threadId; i < originBytes / 8; i += numThreads) {
-        u32x4 v = load16<kSystem>(r, (uint32_t)(i * 16));
+      for_each_strided<16>(originBytes / 8, threadId, numThreads, [&](uint64_t i, uint64_t w0, uint32_t off) {
+        const auto r = make_rsrc(pk + w0 * 16);
+        u32x4 v = load16<kSystem>(r, off);
         if (!LL16Packet::ready(v, flag)) {
           SpinGuard g(budget);
           do {
-            v = load16<kSystem>(r, (uint32_t)(i * 16));
+            v = load16<kSystem>(r, off);
             if (g.expired()) {
               report_error(semaphore_.err, kErrPacketTimeout);
               break;
@@ -141,14 +142,15 @@ struct MemoryChannelDeviceHandle : public BaseMemoryChannelDeviceHandle {
         }
         d[2 * i] = v.x;
         d[2 * i + 1] = v.z;
-      }
+      });
     } else {
-      for (uint64_t i = threadId; i < originBytes / 4; i += numThreads) {
-        u32x2 v = load8<kSystem>(r, (uint32_t)(i * 8));
+      for_each_strided<8>(originBytes / 4, threadId, numThreads, [&](uint64_t i, uint64_t w0, uint32_t off) {
+        const auto r = make_rsrc(pk + w0 * 8);
+        u32x2 v = load8<kSystem>(r, off);
         if (v.y != flag) {
           SpinGuard g(budget);
           do {
-            v = load8<kSystem>(r, (uint32_t)(i * 8));
+            v = load8<kSystem>(r, off);
             if (g.expired()) {
               report_error(semaphore_.err, kErrPacketTimeout);
               break;
@@ -156,7 +158,7 @@ struct MemoryChannelDeviceHandle : public BaseMemoryChannelDeviceHandle {
           } while (v.y != flag);
         }
         d[i] = v.x;
-      }
+      });
     }
   }
   template <typename PacketType = LL16Packet>
@@ -178,23 +180,22 @@ struct MemoryChannelDeviceHandle : public BaseMemoryChannelDeviceHandle {
     uint64_t head = ((d + Alignment - 1) / Alignment * Alignment - d) / 4;
     if (head > numInt) head = numInt;
     auto copy4 = [&](uint64_t from, uint64_t n) {
-      const auto rd = make_rsrc(dst + from * 4);
-      const auto rs = make_rsrc(src + from * 4);
-      for (uint64_t i = tid; i < n; i += nthreads) {
-        const uint32_t v = RemoteDst ? load4<kLocal>(rs, (uint32_t)(i * 4)) : load4<kRemote>(rs, (uint32_t)(i * 4));
+      for_each_strided<4>(n, tid, nthreads, [&](uint64_t, uint64_t w0, uint32_t off) {
+        const auto rd = make_rsrc(dst + (from + w0) * 4);
+        const auto rs = make_rsrc(src + (from + w0) * 4);
+        const uint32_t v = RemoteDst ? load4<kLocal>(rs, off) : load4<kRemote>(rs, off);
         if (RemoteDst)
-          store4<kRemote>(rd, (uint32_t)(i * 4), v);
+          store4<kRemote>(rd, off, v);
         else
-          store4<kLocal>(rd, (uint32_t)(i * 4), v);
-      }
+          store4<kLocal>(rd, off, v);
+      });
     };
     if (CopyRemainder) copy4(0, head);
     constexpr uint64_t kIntPer = Alignment / 4;
     const uint64_t nElem = (numInt - head) / kIntPer;
-    const auto rd = make_rsrc(dst + head * 4);
-    const auto rs = make_rsrc(src + head * 4);
-    for (uint64_t i = tid; i < nElem; i += nthreads) {
-      const uint32_t off = (uint32_t)(i * Alignment);
+    for_each_strided<Alignment>(nElem, tid, nthreads, [&](uint64_t, uint64_t w0, uint32_t off) {
+      const auto rd = make_rsrc(dst + head * 4 + w0 * Alignment);
+      const auto rs = make_rsrc(src + head * 4 + w0 * Alignment);
       if constexpr (Alignment == 16) {
         const u32x4 v = RemoteDst ? load16<kLocal>(rs, off) : load16<kRemote>(rs, off);
         if (RemoteDst)
@@ -214,7 +215,7 @@ struct MemoryChannelDeviceHandle : public BaseMemoryChannelDeviceHandle {
         else
           store4<kLocal>(rd, off, v);
       }
-    }
+    });
     if (CopyRemainder && kIntPer > 1) copy4(head + nElem * kIntPer, numInt - head - nElem * kIntPer);
     // this lane's copies are complete when it returns, so a workgroup barrier followed by one
     // lane's signal() publishes the whole workgroup's put (or its get's data to the other waves)

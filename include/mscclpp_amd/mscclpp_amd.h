@@ -272,6 +272,10 @@ int mscclppAmdLaunchPortChannelPut(void* chans, int nchans, const uint64_t* dstO
 /* MemoryChannel device-surface self-test on one GPU (two in-process ranks): mode 0 LL16 packet
  * ping-pong, 1 LL8 ping-pong, 2 put + signal/wait round trip.  *failures = mismatching words. */
 int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int* failures, uint32_t* devErr);
+/* put, get and putPackets + unpackPackets (LL16, LL8) of `bytes` (multiple of 16, meant to exceed
+ * 4 GiB) on one GPU, nblocks x 256 lanes as one thread group; bad[0..3] = words that differ from the
+ * source pattern after each of the four (memory_channel_device.hpp:101-215 take 64-bit offsets). */
+int mscclppAmdMemChannelBigTest(uint64_t bytes, int nblocks, unsigned long long* bad, uint32_t* devErr);
 
 /* ---- bootstrap (TcpBootstrap, src/core/bootstrap/bootstrap.cc:169-611) -------------------------
  * Host-only setup plane; uniqueId is the 128-byte ncclUniqueId from ncclGetUniqueId. */

@@ -537,15 +537,23 @@ __global__ void __launch_bounds__(512) allreduceRsAgPipelineKernel(Views<NV> vie
 
 static thread_local int g_launch_status = 0;
 
+// Each workgroup addresses its sub-range of a buffer from one buffer resource (32-bit offsets): a
+// launch whose per-workgroup range would exceed that is refused (ncclInvalidUsage) -- more
+// workgroups carry it (every default shape does up to hundreds of GiB).
+constexpr uint64_t kBlkOffsetLimit = 0xFFFFFFFFull - 64;
+
 size_t bulkScratchRequired(int nranks, size_t bytes, size_t maxScratch, BulkGeom* out, int nblocks) {
   BulkGeom g{};
   g.trace = g_mscclppAmdTrace;
   g.bytes = bytes;
   const uint64_t per = (bytes + nranks - 1) / nranks;
   g.slice = (per + 15) & ~15ull;
-  // largest pass whose n regions fit the scratch budget
+  // largest pass whose n regions fit the scratch budget, and the 32-bit offsets of the one buffer
+  // resource the reduce step reads all n regions through (source q at q * pass)
   uint64_t pass = g.slice;
-  const uint64_t cap = maxScratch / (uint64_t)nranks;
+  uint64_t cap = maxScratch / (uint64_t)nranks;
+  const uint64_t cap32 = (0xFFFFFFFFull - 64) / (uint64_t)nranks;
+  if (cap > cap32) cap = cap32;
   if (pass > cap) pass = cap / ((uint64_t)16 * nblocks) * ((uint64_t)16 * nblocks);
   if (pass == 0) return 0;
   g.pass = pass;
@@ -638,6 +646,7 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
     g.pass = g.slice;
     g.npasses = 1;
     g.blk = ((g.slice + nblocks - 1) / nblocks + 15) & ~15ull;
+    if (g.blk > kBlkOffsetLimit) return 5;  // more workgroups needed: one workgroup's range is one descriptor
     g_launch_status = 0;
     auto go = [&](auto kern) {
       if (!grid_coresident(kern, nthreads, (long)nblocks * nviews)) {
@@ -679,6 +688,7 @@ int launchCollectiveBulk(int mode, int algo, const mscclppAmdRankView* views, in
     g.pass = g.slice;
     g.npasses = 1;
     g.blk = ((g.slice + nblocks - 1) / nblocks + 15) & ~15ull;
+    if (g.blk > kBlkOffsetLimit) return 5;
     g_launch_status = 0;
     MSCCLPP_AMD_DISPATCH_ALL(dtype, op, launchZeroCopy, views, nviews, g, nranks, nblocks, nthreads, budget, s);
     if (g_launch_status) return g_launch_status;
@@ -714,6 +724,7 @@ int launchBroadcast(const mscclppAmdRankView* views, int nviews, int nranks, siz
   if (nblocks > kMaxChannels || nthreads > 512 || nthreads % 64 || nthreads < 64) return 4;
   if (root < 0 || root >= nranks || bytes == 0) return 4;
   const uint64_t blk = ((bytes + nblocks - 1) / nblocks + 15) & ~15ull;
+  if (blk > kBlkOffsetLimit) return 5;
   auto go = [&](auto kern, auto vw) {
     if (!grid_coresident(kern, nthreads, (long)nblocks * nviews)) return 5;
     hipLaunchKernelGGL(kern, dim3(nblocks, nviews), dim3(nthreads), 0, s, vw, (uint64_t)bytes, blk, nranks, root,

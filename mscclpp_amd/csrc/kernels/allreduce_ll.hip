@@ -533,21 +533,36 @@ static bool testK2Geometry(int nranks, size_t bytes, LL8Geom* out) {
   return true;
 }
 
+// The LL kernels address a buffer, and all source regions of a scratch half, from one buffer
+// resource each (32-bit offsets: the whole packet exchange of a bucket stays in one descriptor, no
+// per-unit rebasing on the latency path).  So an LL bucket is bounded: its bytes, and the n regions
+// of a scratch half, must lie within 4 GiB of their base -- LL16 to just under 2 GiB per rank,
+// LL8 to 2 GiB / n; beyond, the call is refused (ncclInvalidUsage) rather than wrapped.  The
+// reference runs these protocols below 1 MiB (algorithm_selector.cc:107-117); larger buckets take the
+// bulk paths, which rebase per workgroup and per pass.
+constexpr uint64_t kLLOffsetLimit = 0xFFFFFFFFull - 64;
+static bool ll16Fits(int nranks, const LL16Geom& g) {
+  return g.bytes <= kLLOffsetLimit && (uint64_t)nranks * g.ppr * 16 <= kLLOffsetLimit;
+}
+static bool ll8Fits(int nranks, const LL8Geom& g) {
+  return g.bytes <= kLLOffsetLimit && (uint64_t)nranks * g.W * 8 + 16 <= kLLOffsetLimit;
+}
+
 size_t testK2ScratchRequired(int nranks, size_t bytes) {
   LL8Geom g;
-  if (!testK2Geometry(nranks, bytes, &g)) return 0;
+  if (!testK2Geometry(nranks, bytes, &g) || !ll8Fits(nranks, g)) return 0;
   return 2 * g.hbEven;  // nPacket * max(nRanksPerNode - 1, 1) * 2 LLPackets (:1277-1283)
 }
 
 size_t testLLScratchRequired(int nranks, size_t bytes) {
   LL16Geom g;
-  if (!testLLGeometry(nranks, bytes, &g)) return 0;
+  if (!testLLGeometry(nranks, bytes, &g) || !ll16Fits(nranks, g)) return 0;
   return 4 * (g.W / 2) * 16;  // nPacket * 2 (data, result) * 2 (double buffering), :1282-1286
 }
 
 size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype) {
   LL16Geom g = ll16Geometry(nranks, bytes, dtype);
-  if (g.W == 0) return 0;
+  if (g.W == 0 || !ll16Fits(nranks, g)) return 0;
   uint64_t half = g.roff + (uint64_t)nranks * g.ppr * 16;
   const uint64_t inRegion = (uint64_t)nranks * g.ppr * 16;
   if (inRegion > half) half = inRegion;
@@ -557,6 +572,7 @@ size_t ll16ScratchRequired(int nranks, size_t bytes, int dtype) {
 
 size_t ll8ScratchRequired(int nranks, size_t bytes, int dtype) {
   LL8Geom g = ll8Geometry(bytes, dtype);
+  if (g.W == 0 || !ll8Fits(nranks, g)) return 0;
   uint64_t half = ((uint64_t)nranks * g.W * 8 + 255) & ~255ull;
   return 2 * half;
 }
@@ -663,6 +679,7 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
     LL16Geom g = ll16Geometry(nranks, bytes, dtype);
     if (g.W == 0) return 4;
+    if (!ll16Fits(nranks, g)) return 5;
     for (int i = 0; i < nviews; ++i)
       if (views[i].scratchBytes != views[0].scratchBytes || views[i].scratchBytes < ll16ScratchRequired(nranks, bytes, dtype))
         return 5;
@@ -677,7 +694,7 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
     if (dtype != kI32 && dtype != kU32) return 4;  // an int32 AllReduce
     LL8Geom g;
-    if (!testK2Geometry(nranks, bytes, &g)) return 5;
+    if (!testK2Geometry(nranks, bytes, &g) || !ll8Fits(nranks, g)) return 5;
     for (int i = 0; i < nviews; ++i)
       if (views[i].scratchBytes < testK2ScratchRequired(nranks, bytes)) return 5;
     MSCCLPP_AMD_DISPATCH(dtype, op, launchTestK2, views, nviews, g, nranks, nblocks, nthreads, budget, s);
@@ -690,7 +707,7 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
     if (dtype != kI32 && dtype != kU32) return 4;  // the mscclpp-test kernels are int32 AllReduces
     LL16Geom g;
-    if (!testLLGeometry(nranks, bytes, &g)) return 5;
+    if (!testLLGeometry(nranks, bytes, &g) || !ll16Fits(nranks, g)) return 5;
     for (int i = 0; i < nviews; ++i)
       if (views[i].scratchBytes < testLLScratchRequired(nranks, bytes)) return 5;
     MSCCLPP_AMD_DISPATCH(dtype, op, launchLL16, views, nviews, g, nranks, nblocks, nthreads, budget, s);
@@ -699,6 +716,7 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
     const LL8Geom g = ll8Geometry(bytes, dtype);
     if (g.W == 0) return 4;
+    if (!ll8Fits(nranks, g)) return 5;
     for (int i = 0; i < nviews; ++i)
       if (views[i].scratchBytes < ll8ScratchRequired(nranks, bytes, dtype)) return 5;
     MSCCLPP_AMD_DISPATCH_ALL(dtype, op,launchLL8, views, nviews, g, nranks, nblocks, nthreads, budget, s);

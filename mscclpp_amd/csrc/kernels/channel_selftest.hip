@@ -66,9 +66,103 @@ __global__ void memChanSelfTestKernel(MemoryChannelDeviceHandle* chans, int* b0,
   }
 }
 
+// ---- buffers beyond 4 GiB (the primitives' buffer resources are rebased window by window) -------
+// word i of the pattern: distinct for words 2^30 apart, so a copy that wrapped at 4 GiB shows
+__device__ __forceinline__ uint32_t bigPattern(uint64_t i) {
+  return (uint32_t)(i * 2654435761ull) ^ (uint32_t)(i >> 30) * 0x9E3779B9u ^ 0x5bd1e995u;
+}
+__global__ void bigFillKernel(uint32_t* p, uint64_t words) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = bigPattern(i);
+}
+__global__ void bigCountKernel(const uint32_t* p, uint64_t words, unsigned long long* bad) {
+  unsigned long long n = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x)
+    n += p[i] != bigPattern(i);
+  if (n) atomicAdd(bad, n);
+}
+// op 0 put, 1 get, 2 putPackets<LL16>, 3 unpackPackets<LL16>, 4 putPackets<LL8>, 5 unpackPackets<LL8>;
+// the whole grid is one "thread group" of the primitive (threadId = flat id, numThreads = grid size)
+__global__ void bigChannelKernel(MemoryChannelDeviceHandle ch, uint64_t bytes, int op) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+  switch (op) {
+    case 0: ch.put(0, bytes, tid, nt); break;
+    case 1: ch.get(0, bytes, tid, nt); break;
+    case 2: ch.putPackets<LL16Packet>(0, 0, bytes, tid, nt, 1u); break;
+    case 3: ch.unpackPackets<LL16Packet>(0, 0, bytes, tid, nt, 1u); break;
+    case 4: ch.putPackets<LL8Packet>(0, 0, bytes, tid, nt, 2u); break;
+    default: ch.unpackPackets<LL8Packet>(0, 0, bytes, tid, nt, 2u); break;
+  }
+}
+
 }  // namespace mscclpp_amd
 
 using namespace mscclpp_amd;
+
+// put / get / putPackets + unpackPackets (LL16, LL8) of `bytes` (a multiple of 16; > 4 GiB is the
+// point) on one GPU: a patterned source, a "peer" buffer and a packet buffer.  bad[0..3]: words that
+// differ from the pattern after put (peer), get (back into a cleared local), LL16 and LL8 round trips.
+extern "C" int mscclppAmdMemChannelBigTest(uint64_t bytes, int nblocks, unsigned long long* bad, uint32_t* devErr) {
+  if (!bad || !devErr || bytes == 0 || bytes % 16 || nblocks <= 0 || nblocks > 4096) return 4;
+  const uint64_t words = bytes / 4;
+  uint32_t *src = nullptr, *peer = nullptr, *local = nullptr, *err = nullptr;
+  void* pk = nullptr;
+  unsigned long long* dbad = nullptr;
+  int rc = 0;
+  const dim3 grid(nblocks), block(256);
+  auto count = [&](const uint32_t* p, int k) {
+    if (hipMemset(dbad + k, 0, 8) != hipSuccess) return false;
+    hipLaunchKernelGGL(bigCountKernel, dim3(1024), block, 0, 0, p, words, dbad + k);
+    return hipGetLastError() == hipSuccess;
+  };
+  auto run = [&](void* dst, void* srcp, void* pkt, int op) {
+    MemoryChannelDeviceHandle h{};
+    h.semaphore_ = {nullptr, nullptr, nullptr, 200000000ull /* 2 s */, err};
+    h.dst_ = dst;
+    h.src_ = srcp;
+    h.packetBuffer_ = pkt;
+    hipLaunchKernelGGL(bigChannelKernel, grid, block, 0, 0, h, bytes, op);
+    return hipGetLastError() == hipSuccess;
+  };
+#define CK(x)              \
+  if (!(x)) {              \
+    rc = 1;                \
+    goto done;             \
+  }
+  CK(hipMalloc((void**)&src, bytes) == hipSuccess);
+  CK(hipMalloc((void**)&peer, bytes) == hipSuccess);
+  CK(hipMalloc((void**)&local, bytes) == hipSuccess);
+  CK(hipMalloc(&pk, 2 * bytes) == hipSuccess);
+  CK(hipMalloc((void**)&dbad, 4 * 8) == hipSuccess);
+  CK(hipMalloc((void**)&err, 16) == hipSuccess);
+  CK(hipMemset(err, 0, 16) == hipSuccess);
+  CK(hipMemset(peer, 0, bytes) == hipSuccess);
+  hipLaunchKernelGGL(bigFillKernel, dim3(1024), block, 0, 0, src, words);
+  CK(hipGetLastError() == hipSuccess);
+  CK(run(peer, src, nullptr, 0));  // put: src -> peer
+  CK(count(peer, 0));
+  CK(hipMemset(local, 0, bytes) == hipSuccess);
+  CK(run(peer, local, nullptr, 1));  // get: peer -> local
+  CK(count(local, 1));
+  CK(hipMemset(pk, 0, 2 * bytes) == hipSuccess);
+  CK(hipMemset(local, 0, bytes) == hipSuccess);
+  CK(run(pk, src, nullptr, 2));   // putPackets<LL16>: src -> packets
+  CK(run(nullptr, local, pk, 3));  // unpackPackets<LL16>: packets -> local
+  CK(count(local, 2));
+  CK(hipMemset(local, 0, bytes) == hipSuccess);
+  CK(run(pk, src, nullptr, 4));
+  CK(run(nullptr, local, pk, 5));
+  CK(count(local, 3));
+  CK(hipDeviceSynchronize() == hipSuccess);
+  CK(hipMemcpy(bad, dbad, 4 * 8, hipMemcpyDeviceToHost) == hipSuccess);
+  CK(hipMemcpy(devErr, err, 4, hipMemcpyDeviceToHost) == hipSuccess);
+done:
+#undef CK
+  (void)hipDeviceSynchronize();
+  for (void* p : {(void*)src, (void*)peer, (void*)local, pk, (void*)dbad, (void*)err})
+    if (p) (void)hipFree(p);
+  return rc;
+}
 
 // Returns 0 on success, the mismatch count in *failures, any device error code in *devErr.
 extern "C" int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int* failures, uint32_t* devErr) {

@@ -55,13 +55,13 @@ __device__ void copyBytes(uint8_t* dst, const uint8_t* src, uint64_t bytes, uint
   uint64_t done = 0;
   if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
     const uint64_t n16 = bytes / 16;
-    const auto rs = make_rsrc(src);
-    const auto rd = make_rsrc(dst);
-    for (uint64_t i = tid; i < n16; i += nthreads) {
-      u32x4 v = RemoteSrc ? load16<kSystem>(rs, (uint32_t)(i * 16)) : load16<kPlain>(rs, (uint32_t)(i * 16));
-      if (RemoteDst) store16<kSystem>(rd, (uint32_t)(i * 16), v);
-      else store16<kPlain>(rd, (uint32_t)(i * 16), v);
-    }
+    for_each_strided<16>(n16, tid, nthreads, [&](uint64_t, uint64_t w0, uint32_t off) {
+      const auto rs = make_rsrc(src + w0 * 16);
+      const auto rd = make_rsrc(dst + w0 * 16);
+      u32x4 v = RemoteSrc ? load16<kSystem>(rs, off) : load16<kPlain>(rs, off);
+      if (RemoteDst) store16<kSystem>(rd, off, v);
+      else store16<kPlain>(rd, off, v);
+    });
     done = n16 * 16;
   }
   if ((((uintptr_t)(dst + done) | (uintptr_t)(src + done)) & 3) == 0) {

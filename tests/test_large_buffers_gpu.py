@@ -1,0 +1,79 @@
+"""Buffers beyond 4 GiB (an MI355X holds 288 GB of HBM).  The kernels address memory through buffer
+descriptors, whose offsets are 32 bits; the reference's kernels use 64-bit pointer arithmetic and
+take any size.  Here:
+
+* the MemoryChannel primitives (put, get, putPackets / unpackPackets in LL16 and LL8) walk a range of
+  any size, rebasing their descriptor every 2 GiB (device.hpp for_each_strided): a 4 GiB + 3 MiB
+  range comes back equal to its source pattern, which differs between words 4 GiB apart;
+* the bulk AllReduce kernels stay within 4 GiB per descriptor: fullmesh / rsag cap a pass so the
+  reduce step's n scratch regions fit (here a 2-rank 9 GiB bucket with 9 GiB of scratch runs in
+  three passes instead of wrapping at 4 GiB), zero-copy and the pipeline address per workgroup;
+  every int32 element of the result is checked against the sum of the inputs.
+* the LL protocols refuse buckets whose packet regions would pass 4 GiB (tests/test_library.py).
+"""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GiB, MiB = 1 << 30, 1 << 20
+
+
+def _need(nbytes):
+    free, _ = torch.cuda.mem_get_info()
+    if free < nbytes:
+        pytest.skip(f"needs {nbytes / GiB:.0f} GiB of free device memory")
+
+
+def test_channel_primitives_beyond_4GiB(built):
+    import mscclpp_amd as m
+
+    nbytes = 4 * GiB + 3 * MiB + 48
+    _need(5 * nbytes + 2 * GiB)
+    L = m.lib()
+    L.mscclppAmdMemChannelBigTest.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    bad = (ctypes.c_ulonglong * 4)()
+    err = ctypes.c_uint32(0)
+    rc = L.mscclppAmdMemChannelBigTest(nbytes, 1024, bad, ctypes.byref(err))
+    assert rc == 0
+    assert err.value == 0
+    assert list(bad) == [0, 0, 0, 0], "words off after put, get, LL16 and LL8 round trips: %s" % list(bad)
+
+
+@pytest.fixture(scope="module")
+def big_ranks(built):
+    import mscclpp_amd as m
+
+    n, count = 2, (9 * GiB) // 4 + 4096  # int32 elements per rank: 9 GiB + 16 KiB
+    nbytes = count * 4
+    _need(5 * n * nbytes + 4 * GiB)
+    ranks = m.InProcessRanks(n, 1 * MiB, nbytes)  # bulk scratch = the bucket: without the cap, one 4.5 GiB pass
+    dev = torch.device("cuda", 0)
+    ins = []
+    for r in range(n):
+        t = torch.empty(count, dtype=torch.int32, device=dev)
+        for c in t.split(1 << 28):
+            c.random_(0, 1 << 20)
+        ins.append(t)
+    outs = [torch.empty_like(t) for t in ins]
+    yield m, ranks, ins, outs
+    del ins, outs
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("algo", ["fullmesh", "rsag", "rsag_zc", "rsag_pipeline"])
+def test_bulk_allreduce_beyond_4GiB(big_ranks, algo):
+    m, ranks, ins, outs = big_ranks
+    for o in outs:
+        o.fill_(-1)
+    torch.cuda.synchronize()
+    ranks.all_reduce(ins, outs, m.ALGO_NAMES[algo], budget_ticks=3_000_000_000)
+    torch.cuda.synchronize()
+    assert ranks.errors() == [0] * ranks.n
+    for r, o in enumerate(outs):
+        wrong = 0
+        for a, b, c in zip(ins[0].split(1 << 28), ins[1].split(1 << 28), o.split(1 << 28)):
+            wrong += int((c != a + b).sum())
+        assert wrong == 0, f"{algo}: rank {r} has {wrong} wrong int32 elements of {o.numel()}"

@@ -51,6 +51,28 @@ def test_loads_and_host_logic(built):
     assert m.scratch_required(m.ALGO_ALLPAIR, 8, 16 << 10, m.F16) == 2 * 8 * (16 << 10) * 2
 
 
+def test_buffer_resource_offset_limits(built):
+    """Buckets whose LL offsets would pass 4 GiB from one descriptor are refused (0 = ncclInvalidUsage
+    at the call); the bulk pass is capped so the reduce step's n regions stay within 4 GiB."""
+    import mscclpp_amd as m
+
+    MiB, GiB = 1 << 20, 1 << 30
+    # LL16: the n input regions of a scratch half span 2 * bytes
+    assert m.scratch_required(m.ALGO_PACKET, 8, 2 * GiB - MiB, m.F16) > 0
+    assert m.scratch_required(m.ALGO_PACKET, 8, 2 * GiB + MiB, m.F16) == 0
+    assert m.scratch_required(m.ALGO_TEST_K6, 2, GiB, m.I32) > 0
+    assert m.scratch_required(m.ALGO_TEST_K6, 2, 2 * GiB + 16 * MiB, m.I32) == 0
+    # LL8: every rank's whole buffer in one half: 2 * n * bytes
+    assert m.scratch_required(m.ALGO_ALLPAIR, 8, 255 * MiB, m.F16) > 0
+    assert m.scratch_required(m.ALGO_ALLPAIR, 8, 257 * MiB, m.F16) == 0
+    assert m.scratch_required(m.ALGO_TEST_K2, 8, 257 * MiB, m.I32) == 0
+    # bulk: n regions of one pass within 4 GiB of the reduce step's descriptor
+    for n in (2, 8):
+        s = m.scratch_required(m.ALGO_FULLMESH, n, 48 * GiB, m.F16)
+        assert 0 < s <= 4 * GiB - 64
+    assert m.scratch_required(m.ALGO_FULLMESH, 8, 48 * MiB, m.F16) == 48 * MiB  # one pass, as before
+
+
 def test_invalid_arguments_rejected_without_gpu(built):
     import mscclpp_amd as m
 
