@@ -45,8 +45,18 @@ struct BasePortChannelDeviceHandle {
       : semaphoreId_(semaphoreId), semaphore_(semaphore), fifo_(fifo), flushDonePos_(flushDonePos) {}
 
 #if defined(__HIP__)
+  // A trigger carries 32-bit offsets and size (fifo_device.hpp:71-77; the reference asserts this in
+  // debug builds and truncates in release ones).  A put that does not fit is not pushed at all --
+  // no truncated copy, no signal for data that was not sent -- and kErrBadGeometry is recorded in
+  // the FIFO's error word; larger transfers are split by the caller, as with the reference.
+  __device__ __forceinline__ bool triggerFits(uint64_t dstOffset, uint64_t srcOffset, uint64_t size) {
+    if (((dstOffset | srcOffset | size) >> TriggerBitsOffset) == 0) return true;
+    report_error(fifo_.err, kErrBadGeometry);
+    return false;
+  }
   __device__ __forceinline__ void put(MemoryId dstId, uint64_t dstOffset, MemoryId srcId, uint64_t srcOffset,
                                      uint64_t size) {
+    if (!triggerFits(dstOffset, srcOffset, size)) return;
     fifo_.push(ProxyTrigger(TriggerData, dstId, dstOffset, srcId, srcOffset, size, semaphoreId_));
   }
   __device__ __forceinline__ void put(MemoryId dstId, MemoryId srcId, uint64_t offset, uint64_t size) {
@@ -55,6 +65,7 @@ struct BasePortChannelDeviceHandle {
   __device__ __forceinline__ void signal() { fifo_.push(ProxyTrigger(TriggerFlag, 0, 0, 0, 0, 0, semaphoreId_)); }
   __device__ __forceinline__ void putWithSignal(MemoryId dstId, uint64_t dstOffset, MemoryId srcId, uint64_t srcOffset,
                                                uint64_t size) {
+    if (!triggerFits(dstOffset, srcOffset, size)) return;
     fifo_.push(ProxyTrigger(TriggerData | TriggerFlag, dstId, dstOffset, srcId, srcOffset, size, semaphoreId_));
   }
   __device__ __forceinline__ void putWithSignal(MemoryId dstId, MemoryId srcId, uint64_t offset, uint64_t size) {
@@ -64,6 +75,7 @@ struct BasePortChannelDeviceHandle {
                                                        uint64_t srcOffset, uint64_t size,
                                                        int64_t maxSpinCount = 1000000) {
     (void)maxSpinCount;
+    if (!triggerFits(dstOffset, srcOffset, size)) return;
     const uint64_t pos = fifo_.push(
         ProxyTrigger(TriggerData | TriggerFlag | TriggerSync, dstId, dstOffset, srcId, srcOffset, size, semaphoreId_));
     detail::waitFlush(flushDonePos_, pos, fifo_.budget, fifo_.err);

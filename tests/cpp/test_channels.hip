@@ -254,6 +254,17 @@ __global__ void kernelPortPutPingPong(int* buff, int rank, int nElem, int* ret, 
   }
 }
 
+// A trigger carries 32-bit offsets and size (fifo_device.hpp:71-77): oversize puts are refused on the
+// device -- nothing pushed, kErrBadGeometry in the error word -- instead of being truncated.
+__global__ void kernelPortOversizePut() {
+  if (threadIdx.x == 0) {
+    DeviceHandle<mscclpp::PortChannel>& c = gChannelOneToOneTestConstPortChans;
+    c.put(0, 0, 1ull << 32);
+    c.putWithSignal(1ull << 32, 0, 16);
+    c.putWithSignalAndFlush(0, 1ull << 32, 16);
+  }
+}
+
 static int worker(int rank, ncclUniqueId id, int nElemMax) {
   gRank = rank;
   int ndev = 0;
@@ -392,6 +403,15 @@ static int worker(int rank, ncclUniqueId id, int nElemMax) {
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(gChannelOneToOneTestConstPortChans), &h, sizeof(h)));
       for (int n : {2, 1024 + 6, 1024 * 1024})
         if (n <= nElemMax) run("port put ping-pong", kernelPortPutPingPong, n, 50);
+      const uint64_t handled = proxy.triggersHandled();
+      hipLaunchKernelGGL(kernelPortOversizePut, dim3(1), dim3(64), 0, 0);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipDeviceSynchronize());
+      uint32_t code = 0;
+      CHECK(mscclppAmdCommGetDeviceError(comm->ncclComm(), &code, 1) == 0);
+      CHECK(code == 4 /* kErrBadGeometry */);
+      CHECK(proxy.triggersHandled() == handled);
+      comm->bootstrap()->barrier();
     }
     CHECK(proxy.triggersHandled() > 0);
     proxy.stopProxy();
