@@ -9,6 +9,7 @@ take any size.  Here:
   reduce step's n scratch regions fit (here a 2-rank 9 GiB bucket with 9 GiB of scratch runs in
   three passes instead of wrapping at 4 GiB), zero-copy and the pipeline address per workgroup;
   every int32 element of the result is checked against the sum of the inputs.
+* the 1-GPU LL16 self-reduce (config 2) runs a 4.5 GiB bucket exactly;
 * the LL protocols refuse buckets whose packet regions would pass 4 GiB (tests/test_library.py).
 """
 import ctypes
@@ -77,3 +78,59 @@ def test_bulk_allreduce_beyond_4GiB(big_ranks, algo):
         for a, b, c in zip(ins[0].split(1 << 28), ins[1].split(1 << 28), o.split(1 << 28)):
             wrong += int((c != a + b).sum())
         assert wrong == 0, f"{algo}: rank {r} has {wrong} wrong int32 elements of {o.numel()}"
+
+
+def test_self_reduce_beyond_4GiB(built):
+    """The 1-GPU LL16 hot path (BASELINE config 2) on a 4.5 GiB int32 bucket: out = x + unpack(pack(y))
+    for every element (the kernel rebases its descriptors per 1 KiB chunk)."""
+    import mscclpp_amd as m
+
+    count = (9 * GiB // 2) // 4 + 1024
+    nbytes = count * 4
+    _need(6 * nbytes + 2 * GiB)
+    dev = torch.device("cuda", 0)
+    x, y = (torch.empty(count, dtype=torch.int32, device=dev) for _ in range(2))
+    for t in (x, y):
+        for c in t.split(1 << 28):
+            c.random_(0, 1 << 20)
+    out = torch.full_like(x, -1)
+    pk = m.DeviceBuffer(2 * nbytes)
+    flags = torch.ones(m.FLAG_SLOTS, dtype=torch.int32, device=dev)
+    err = torch.zeros(16, dtype=torch.int32, device=dev)
+    m.self_reduce_ll16(x, y, pk.ptr, out, flags, err, budget_ticks=3_000_000_000)
+    torch.cuda.synchronize()
+    assert int(err[0]) == 0
+    wrong = sum(int((c != a + b).sum()) for a, b, c in zip(x.split(1 << 28), y.split(1 << 28), out.split(1 << 28)))
+    assert wrong == 0, f"{wrong} wrong int32 elements of {count}"
+    pk.free()
+
+
+@pytest.mark.parametrize("algo,nbytes", [("packet", 2 * GiB - MiB), ("allpair", GiB - MiB)])
+def test_ll_at_largest_accepted_bucket(built, algo, nbytes):
+    """LL16 / LL8 at 2 ranks just under their 4 GiB descriptor bound (packet regions reaching ~4 GiB
+    from their base): every element right; one step above, the call is refused (ncclInvalidUsage)."""
+    import mscclpp_amd as m
+
+    n, code = 2, m.ALGO_NAMES[algo]
+    sb = m.scratch_required(code, n, nbytes, m.I32)
+    assert sb > 0 and m.scratch_required(code, n, nbytes + 2 * MiB, m.I32) == 0
+    _need(n * (sb + 3 * nbytes) + 2 * GiB)
+    dev = torch.device("cuda", 0)
+    ranks = m.InProcessRanks(n, sb)
+    ins = []
+    for r in range(n):
+        t = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
+        for c in t.split(1 << 28):
+            c.random_(0, 1 << 20)
+        ins.append(t)
+    outs = [torch.full_like(t, -1) for t in ins]
+    ranks.all_reduce(ins, outs, code, budget_ticks=3_000_000_000)
+    torch.cuda.synchronize()
+    assert ranks.errors() == [0] * n
+    for r, o in enumerate(outs):
+        wrong = sum(int((c != a + b).sum()) for a, b, c in zip(ins[0].split(1 << 28), ins[1].split(1 << 28), o.split(1 << 28)))
+        assert wrong == 0, f"{algo}: rank {r} has {wrong} wrong elements"
+    del outs
+    big = [torch.empty(nbytes // 4 + (2 * MiB) // 4, dtype=torch.int32, device=dev) for _ in range(n)]
+    with pytest.raises(m.MscclppError):
+        ranks.all_reduce(big, big, code)
