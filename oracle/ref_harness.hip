@@ -246,6 +246,8 @@ static bool rankStreams() {
   return hipDeviceSynchronize() == hipSuccess;
 }
 
+void refBench2Close(void* handle);
+
 void* refBench2Open(const char* hsaco, int n) {
   if (n < 2 || n > 8 || !rankStreams()) return nullptr;
   auto* h = new RefBench2;
@@ -256,8 +258,10 @@ void* refBench2Open(const char* hsaco, int n) {
   for (int r = 0; r < n; ++r) {
     if (hipModuleLoad(&h->mod[r], hsaco) != hipSuccess ||
         hipModuleGetFunction(&h->fn[r], h->mod[r], "allreduce2") != hipSuccess ||
-        hipMalloc(&h->chans[r], sizeof(MemoryChannelDeviceHandle) * (n - 1)) != hipSuccess)
+        hipMalloc(&h->chans[r], sizeof(MemoryChannelDeviceHandle) * (n - 1)) != hipSuccess) {
+      refBench2Close(h);
       return nullptr;
+    }
   }
   // distinct modules must hold distinct globalFlag words (one per rank, as one per process)
   std::vector<void*> flags(n);
@@ -265,10 +269,15 @@ void* refBench2Open(const char* hsaco, int n) {
     size_t bytes = 0;
     if (hipModuleGetGlobal(reinterpret_cast<hipDeviceptr_t*>(&flags[r]), &bytes, h->mod[r], "globalFlag") !=
             hipSuccess ||
-        bytes != sizeof(uint64_t))
+        bytes != sizeof(uint64_t)) {
+      refBench2Close(h);
       return nullptr;
+    }
     for (int q = 0; q < r; ++q)
-      if (flags[q] == flags[r]) return nullptr;
+      if (flags[q] == flags[r]) {
+        refBench2Close(h);
+        return nullptr;
+      }
   }
   return h;
 }
