@@ -134,3 +134,43 @@ def test_ll_at_largest_accepted_bucket(built, algo, nbytes):
     big = [torch.empty(nbytes // 4 + (2 * MiB) // 4, dtype=torch.int32, device=dev) for _ in range(n)]
     with pytest.raises(m.MscclppError):
         ranks.all_reduce(big, big, code)
+
+
+@pytest.mark.parametrize("algo", ["fullmesh", "rsag"])
+def test_reduce_scatter_and_all_gather_beyond_4GiB(big_ranks, algo):
+    """ncclReduceScatter / ncclAllGather through the bulk kernel (modes 1 and 2) with 4.5 GiB blocks:
+    9 GiB gathered or reduced per rank, in capped passes, every element checked."""
+    m, ranks, ins, outs = big_ranks
+    n = ranks.n
+    block = (ins[0].numel() // n) // 4 * 4  # int32 elements per rank block (16-byte multiple)
+    chunk = 1 << 28
+    # ReduceScatter: rank r gets sum over q of ins[q][r*block : (r+1)*block]
+    rs_in = [t[: n * block] for t in ins]
+    rs_out = [o[:block] for o in outs]
+    for o in rs_out:
+        o.fill_(-1)
+    ranks.collective(1, rs_in, rs_out, algo=m.ALGO_NAMES[algo], budget_ticks=3_000_000_000)
+    torch.cuda.synchronize()
+    assert ranks.errors() == [0] * n
+    for r in range(n):
+        lo = r * block
+        wrong = 0
+        for s in range(0, block, chunk):
+            e = min(block, s + chunk)
+            wrong += int((rs_out[r][s:e] != ins[0][lo + s:lo + e] + ins[1][lo + s:lo + e]).sum())
+        assert wrong == 0, f"ReduceScatter {algo}: rank {r} has {wrong} wrong elements"
+    # AllGather: outs[r] = ins[0][:block] ++ ins[1][:block]
+    ag_in = [t[:block] for t in ins]
+    ag_out = [o[: n * block] for o in outs]
+    for o in ag_out:
+        o.fill_(-1)
+    ranks.collective(2, ag_in, ag_out, algo=m.ALGO_NAMES[algo], budget_ticks=3_000_000_000)
+    torch.cuda.synchronize()
+    assert ranks.errors() == [0] * n
+    for r in range(n):
+        wrong = 0
+        for q in range(n):
+            for s in range(0, block, chunk):
+                e = min(block, s + chunk)
+                wrong += int((ag_out[r][q * block + s:q * block + e] != ins[q][s:e]).sum())
+        assert wrong == 0, f"AllGather {algo}: rank {r} has {wrong} wrong elements"
