@@ -9,7 +9,8 @@ take any size.  Here:
   reduce step's n scratch regions fit (here a 2-rank 9 GiB bucket with 9 GiB of scratch runs in
   three passes instead of wrapping at 4 GiB), zero-copy and the pipeline address per workgroup;
   every int32 element of the result is checked against the sum of the inputs.
-* the 1-GPU LL16 self-reduce (config 2) runs a 4.5 GiB bucket exactly;
+* the 1-GPU LL16 self-reduce (config 2) runs a 4.5 GiB bucket exactly; ReduceScatter, AllGather
+  (4.5 GiB blocks) and Broadcast (9 GiB) likewise;
 * the LL protocols refuse buckets whose packet regions would pass 4 GiB (tests/test_library.py).
 """
 import ctypes
@@ -174,3 +175,16 @@ def test_reduce_scatter_and_all_gather_beyond_4GiB(big_ranks, algo):
                 e = min(block, s + chunk)
                 wrong += int((ag_out[r][q * block + s:q * block + e] != ins[q][s:e]).sum())
         assert wrong == 0, f"AllGather {algo}: rank {r} has {wrong} wrong elements"
+
+
+def test_broadcast_beyond_4GiB(big_ranks):
+    """ncclBroadcast's zero-copy pull of a 9 GiB buffer from root 1 (default shape: 128 workgroups)."""
+    m, ranks, ins, outs = big_ranks
+    for o in outs:
+        o.fill_(-1)
+    ranks.broadcast(ins, outs, 1, budget_ticks=3_000_000_000)
+    torch.cuda.synchronize()
+    assert ranks.errors() == [0] * ranks.n
+    for r, o in enumerate(outs):
+        wrong = sum(int((c != a).sum()) for a, c in zip(ins[1].split(1 << 28), o.split(1 << 28)))
+        assert wrong == 0, f"rank {r} has {wrong} wrong elements"
