@@ -11,9 +11,13 @@ take any size.  Here:
   every int32 element of the result is checked against the sum of the inputs.
 * the 1-GPU LL16 self-reduce (config 2) runs a 4.5 GiB bucket exactly; ReduceScatter, AllGather
   (4.5 GiB blocks) and Broadcast (9 GiB) likewise;
+* ncclAllReduce between two processes (IPC-mapped 9 GiB buffers; default selector and rsag_zc);
 * the LL protocols refuse buckets whose packet regions would pass 4 GiB (tests/test_library.py).
 """
 import ctypes
+import multiprocessing as mp
+import os
+import traceback
 
 import pytest
 import torch
@@ -188,3 +192,63 @@ def test_broadcast_beyond_4GiB(big_ranks):
     for r, o in enumerate(outs):
         wrong = sum(int((c != a).sum()) for a, c in zip(ins[1].split(1 << 28), o.split(1 << 28)))
         assert wrong == 0, f"rank {r} has {wrong} wrong elements"
+
+
+def _pattern(rank, lo, hi, device):
+    """int32 elements [lo, hi) of rank's input: distinct 4 GiB apart, small enough that sums stay exact."""
+    i = torch.arange(lo, hi, dtype=torch.int64, device=device)
+    return ((i * 2654435761 + (i >> 30) * 97 + rank * 12345) & 0xFFFFF).to(torch.int32)
+
+
+def _nccl_worker(rank, n, uid, count, q):
+    try:
+        os.environ.setdefault("MSCCLPP_AMD_SPIN_TIMEOUT_MS", "20000")
+        import mp_util
+
+        mp_util.place_rank(rank, n)
+        import mscclpp_amd as m
+
+        dev = torch.device("cuda", torch.cuda.current_device())
+        comm = m.Communicator(rank, n, uid)
+        chunk = 1 << 28
+        x = torch.empty(count, dtype=torch.int32, device=dev)
+        for s in range(0, count, chunk):
+            x[s:s + chunk] = _pattern(rank, s, min(count, s + chunk), dev)
+        out = torch.empty_like(x)
+        res = []
+        for algo in (None, "rsag_zc"):  # the selector's choice at 9 GiB (fullmesh, many 128 MiB-scratch passes), zero-copy
+            out.fill_(-1)
+            comm.all_reduce(x, out, algo=algo)
+            torch.cuda.synchronize()
+            wrong = 0
+            for s in range(0, count, chunk):
+                e = min(count, s + chunk)
+                want = sum(_pattern(r, s, e, dev) for r in range(n))
+                wrong += int((out[s:e] != want).sum())
+            res.append((algo or "auto", comm.device_error(), wrong))
+        comm.barrier()
+        comm.destroy()
+        q.put((rank, res, None))
+    except Exception:
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_nccl_allreduce_two_processes_beyond_4GiB(built):
+    """The drop-in path end to end: ncclAllReduce between two processes (IPC-mapped 9 GiB outputs
+    and inputs) -- the default selector (fullmesh through the communicator's 128 MiB scratch) and
+    zero-copy rsag -- every element equal to the sum of both ranks' inputs."""
+    import mp_util
+    import mscclpp_amd as m
+
+    n, count = 2, (9 * GiB) // 4 + 4096
+    _need(n * (2 * count * 4 + 3 * GiB))
+    uid = m.Communicator.unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_nccl_worker, args=(r, n, uid, count, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = mp_util.collect(procs, q, n, 240)
+    for rank in range(n):
+        for algo, errc, wrong in got[rank]:
+            assert errc == 0 and wrong == 0, (rank, algo, errc, wrong)
