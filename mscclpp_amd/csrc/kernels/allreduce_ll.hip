@@ -675,6 +675,8 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
                       int op, int nblocks, int nthreads, uint64_t budget, hipStream_t s) {
   g_ll_launch_status = 0;
   if (algo == MSCCLPP_AMD_ALGO_PACKET) {
+    // an explicit grid narrower than the peer count is an invalid argument (allreduce_packet.cu:238-241)
+    if (nblocks > 0 && nblocks < nranks - 1) return 4;
     ll16Defaults(nranks, bytes, nblocks, nthreads);
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
     LL16Geom g = ll16Geometry(nranks, bytes, dtype);
@@ -742,6 +744,8 @@ extern "C" int mscclppAmdDiagAllReduceLL(int algo, const mscclppAmdRankView* vie
   for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
   g_ll_launch_status = 0;
   if (algo == MSCCLPP_AMD_ALGO_PACKET) {
+    // an explicit grid narrower than the peer count is an invalid argument (allreduce_packet.cu:238-241)
+    if (nblocks > 0 && nblocks < nranks - 1) return 4;
     ll16Defaults(nranks, bytes, nblocks, nthreads);
     LL16Geom g = ll16Geometry(nranks, bytes, kF16);
     if (views[0].scratchBytes < ll16ScratchRequired(nranks, bytes, kF16)) return 5;

@@ -312,3 +312,20 @@ def test_rsag_pipeline_min(built):
     exp = _pipeline_expected(dt, O.MIN, ins, count * 2, n, R, T)
     for r in range(n):
         _cmp(_bytes(douts[r]), exp.view(np.uint8)[: count * 2], dt)
+
+
+def test_packet_grid_narrower_than_peers_is_invalid(built):
+    """allreduce_packet.cu:238-241: an explicit LL16 grid with fewer workgroups than peers is an
+    invalid argument (ncclInvalidArgument / CommInvalidArgument), not silently widened."""
+    import mscclpp_amd as m
+
+    n, count = 4, 4096
+    ranks = m.InProcessRanks(n, m.scratch_required(m.ALGO_PACKET, n, count * 2, O.F16))
+    ins = [torch.ones(count, dtype=torch.float16, device="cuda") for _ in range(n)]
+    outs = [torch.empty_like(t) for t in ins]
+    with pytest.raises(m.MscclppError) as e:
+        ranks.all_reduce(ins, outs, m.ALGO_PACKET, nblocks=2, nthreads=256)
+    assert e.value.code == 4
+    ranks.all_reduce(ins, outs, m.ALGO_PACKET, nblocks=3, nthreads=256)  # = peers: accepted
+    torch.cuda.synchronize()
+    assert ranks.errors() == [0] * n and all(bool(torch.all(o == n)) for o in outs)
