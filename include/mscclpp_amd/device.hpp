@@ -50,7 +50,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p) {
 // window by window of 2 GiB with w0 the window's first unit (uniform across the wave), so a buffer
 // of any size is addressed exactly as the reference's 64-bit pointer arithmetic addresses it.
 template <uint32_t Unit, typename F>
-__device__ __forceinline__ void for_each_strided(uint64_t n, uint64_t tid, uint64_t nthreads, F&& f) {
+__host__ __device__ __forceinline__ void for_each_strided(uint64_t n, uint64_t tid, uint64_t nthreads, F&& f) {
   if (n * Unit <= 0xFFFFFFFFull) {
     for (uint64_t i = tid; i < n; i += nthreads) f(i, (uint64_t)0, (uint32_t)(i * Unit));
     return;
