@@ -1,0 +1,11 @@
+// <mscclpp/atomic_device.hpp> on this library (include/mscclpp_amd/atomic_device.hpp).
+// A caller written against the reference's include/mscclpp/atomic_device.hpp compiles unchanged with
+// `-I include`; namespace mscclpp names the declarations through a using-directive
+// (include/mscclpp/namespace.hpp).
+#ifndef MSCCLPP_AMD_FWD_ATOMIC_DEVICE_HPP_
+#define MSCCLPP_AMD_FWD_ATOMIC_DEVICE_HPP_
+
+#include "mscclpp_amd/atomic_device.hpp"
+#include "mscclpp/namespace.hpp"
+
+#endif  // MSCCLPP_AMD_FWD_ATOMIC_DEVICE_HPP_

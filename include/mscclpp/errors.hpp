@@ -1,0 +1,11 @@
+// <mscclpp/errors.hpp> on this library (include/mscclpp_amd/errors.hpp).
+// A caller written against the reference's include/mscclpp/errors.hpp compiles unchanged with
+// `-I include`; namespace mscclpp names the declarations through a using-directive
+// (include/mscclpp/namespace.hpp).
+#ifndef MSCCLPP_AMD_FWD_ERRORS_HPP_
+#define MSCCLPP_AMD_FWD_ERRORS_HPP_
+
+#include "mscclpp_amd/errors.hpp"
+#include "mscclpp/namespace.hpp"
+
+#endif  // MSCCLPP_AMD_FWD_ERRORS_HPP_

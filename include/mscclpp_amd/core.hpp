@@ -34,21 +34,11 @@
 #include <type_traits>
 #include <vector>
 
+#include "mscclpp_amd/errors.hpp"
 #include "mscclpp_amd/nccl.h"
 
 namespace mscclpp_amd {
 
-// errors.hpp: ErrorCode and Error (the code says what kind of failure it is)
-enum class ErrorCode { SystemError, InternalError, RemoteError, InvalidUsage, Timeout, Aborted, ExecutorError };
-
-class Error : public std::runtime_error {
- public:
-  Error(const std::string& message, ErrorCode errorCode) : std::runtime_error(message), errorCode_(errorCode) {}
-  ErrorCode getErrorCode() const { return errorCode_; }
-
- private:
-  ErrorCode errorCode_;
-};
 
 // ---- bootstrap (core.hpp:29-110) ----------------------------------------------------------------
 class Bootstrap {

@@ -17,8 +17,9 @@
 
 namespace mscclpp_amd {
 
+// a failed runtime call throws CudaError carrying the hipError_t (gpu_utils.hpp MSCCLPP_CUDATHROW)
 inline void gpuCheck(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw Error(std::string(what) + ": " + hipGetErrorString(e), ErrorCode::SystemError);
+  if (e != hipSuccess) throw CudaError(std::string("Call to ") + what + " failed", static_cast<int>(e));
 }
 
 // MSCCLPP_CUDATHROW (gpu_utils.hpp / errors.hpp): throw on a failed runtime call.  The calls are

@@ -88,6 +88,9 @@ int guarded(F&& f) {
   } catch (const HipError& e) {
     warn(e.what());
     return ncclUnhandledCudaError;
+  } catch (const mscclpp_amd::CudaError& e) {  // a failed HIP runtime call (MSCCLPP_CUDATHROW, gpu_utils.hpp)
+    warn(e.what());
+    return ncclUnhandledCudaError;
   } catch (const mscclpp_amd::Error& e) {  // the host channel API's errors (core.hpp)
     warn(e.what());
     switch (e.getErrorCode()) {

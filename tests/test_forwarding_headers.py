@@ -41,7 +41,27 @@ using T = mscclpp::Host2HostSemaphore;
 static const mscclpp::PacketType kPt = mscclpp::PacketType::LL8;
 static const mscclpp::DataType kDt = mscclpp::DataType::FLOAT8_E4M3B15;
 __global__ void k(mscclpp::MemoryChannelDeviceHandle* h) { h->putPackets<mscclpp::LL16Packet>(0, 0, 64, threadIdx.x, blockDim.x, 1); }
-int main() { return 0; }
+// atomic_device.hpp / poll_device.hpp / assert_device.hpp spellings, as port_channel_device.hpp:28 and
+// concurrency_device.hpp:54 use them
+__global__ void k2(uint64_t* flushDonePos, uint64_t fifoPos, unsigned int* count) {
+  POLL_MAYBE_JAILBREAK((mscclpp::atomicLoad<uint64_t, mscclpp::scopeSystem>(flushDonePos, mscclpp::memoryOrderAcquire) <= fifoPos), 1000000);
+  OR_POLL_MAYBE_JAILBREAK(*count == 0, *count == 1, -1);
+  mscclpp::atomicStore(count, 1u, mscclpp::memoryOrderRelaxed);
+  (void)mscclpp::atomicFetchAdd<unsigned int, mscclpp::scopeDevice>(count, 1u, mscclpp::memoryOrderAcqRel);
+  MSCCLPP_ASSERT_DEVICE(*count > 0, "count");
+}
+int main() {
+  try {
+    throw mscclpp::Error("x", mscclpp::ErrorCode::InvalidUsage);
+  } catch (const mscclpp::BaseError& e) {
+    if (e.getErrorCode() != (int)mscclpp::ErrorCode::InvalidUsage) return 1;
+  }
+  try {
+    throw mscclpp::CudaError("y", 1);
+  } catch (const mscclpp::BaseError&) {
+  }
+  return mscclpp::errorToString(mscclpp::ErrorCode::Timeout) == "Timeout" ? 0 : 1;
+}
 """
 
 
