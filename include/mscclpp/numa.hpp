@@ -1,0 +1,11 @@
+// <mscclpp/numa.hpp> on this library (include/mscclpp_amd/numa.hpp).
+// A caller written against the reference's include/mscclpp/numa.hpp compiles unchanged with
+// `-I include`; namespace mscclpp names the declarations through a using-directive
+// (include/mscclpp/namespace.hpp).
+#ifndef MSCCLPP_AMD_FWD_NUMA_HPP_
+#define MSCCLPP_AMD_FWD_NUMA_HPP_
+
+#include "mscclpp_amd/numa.hpp"
+#include "mscclpp/namespace.hpp"
+
+#endif  // MSCCLPP_AMD_FWD_NUMA_HPP_

@@ -1,0 +1,11 @@
+// <mscclpp/utils.hpp> on this library (include/mscclpp_amd/utils.hpp).
+// A caller written against the reference's include/mscclpp/utils.hpp compiles unchanged with
+// `-I include`; namespace mscclpp names the declarations through a using-directive
+// (include/mscclpp/namespace.hpp).
+#ifndef MSCCLPP_AMD_FWD_UTILS_HPP_
+#define MSCCLPP_AMD_FWD_UTILS_HPP_
+
+#include "mscclpp_amd/utils.hpp"
+#include "mscclpp/namespace.hpp"
+
+#endif  // MSCCLPP_AMD_FWD_UTILS_HPP_

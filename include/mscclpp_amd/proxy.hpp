@@ -10,6 +10,7 @@
 #include <thread>
 
 #include "mscclpp_amd/fifo.hpp"
+#include "mscclpp_amd/numa.hpp"
 
 namespace mscclpp_amd {
 
@@ -44,11 +45,6 @@ class Proxy {
   std::atomic<uint64_t> maxGapNs_{0};
   std::atomic<bool> resetGap_{false};
 };
-
-// The NUMA node of a GPU (sysfs of its PCI device), -1 if unknown; numaBind pins the calling
-// thread to that node's CPUs and returns the node, or -1.
-int getDeviceNumaNode(int device);
-int numaBind(int node);
 
 }  // namespace mscclpp_amd
 

@@ -60,6 +60,11 @@ int main() {
     throw mscclpp::CudaError("y", 1);
   } catch (const mscclpp::BaseError&) {
   }
+  std::size_t seed = 0;
+  mscclpp::detail::hashCombine(seed, 42);
+  (void)mscclpp::getDeviceNumaNode(0);
+  if (mscclpp::getIBDeviceCount() != 0 || mscclpp::isFabricMemHandleAvailable()) return 1;
+  if (mscclpp::getHostName(1024, '.').empty()) return 1;
   return mscclpp::errorToString(mscclpp::ErrorCode::Timeout) == "Timeout" ? 0 : 1;
 }
 """
