@@ -38,6 +38,8 @@ using Q = mscclpp::ExecutionPlan;
 using R = mscclpp::collective::AlgorithmCollectionBuilder;
 using S = mscclpp::GpuBuffer<int>;
 using T = mscclpp::Host2HostSemaphore;
+static_assert(MSCCLPP_BULK_AVAILABLE == 0, "no Hopper bulk copies on gfx950");
+using U = mscclpp::BulkBarrier;
 static const mscclpp::PacketType kPt = mscclpp::PacketType::LL8;
 static const mscclpp::DataType kDt = mscclpp::DataType::FLOAT8_E4M3B15;
 __global__ void k(mscclpp::MemoryChannelDeviceHandle* h) { h->putPackets<mscclpp::LL16Packet>(0, 0, 64, threadIdx.x, blockDim.x, 1); }
