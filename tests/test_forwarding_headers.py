@@ -67,6 +67,7 @@ int main() {
   (void)mscclpp::getDeviceNumaNode(0);
   if (mscclpp::getIBDeviceCount() != 0 || mscclpp::isFabricMemHandleAvailable()) return 1;
   if (mscclpp::getHostName(1024, '.').empty()) return 1;
+  if (mscclpp::env()->logLevel.empty() || mscclpp::env()->ibGidIndex < 0) return 1;
   return mscclpp::errorToString(mscclpp::ErrorCode::Timeout) == "Timeout" ? 0 : 1;
 }
 """
