@@ -38,14 +38,20 @@
 #include <string>
 #include <vector>
 
+#include <mscclpp/atomic_device.hpp>
 #include <mscclpp/concurrency_device.hpp>
 #include <mscclpp/core.hpp>
+#include <mscclpp/env.hpp>
+#include <mscclpp/errors.hpp>
 #include <mscclpp/executor.hpp>
 #include <mscclpp/gpu_utils.hpp>
 #include <mscclpp/memory_channel.hpp>
 #include <mscclpp/memory_channel_device.hpp>
+#include <mscclpp/numa.hpp>
+#include <mscclpp/poll_device.hpp>
 #include <mscclpp/port_channel.hpp>
 #include <mscclpp/port_channel_device.hpp>
+#include <mscclpp/utils.hpp>
 
 #define CHECK(cond)                                                               \
   do {                                                                            \
@@ -530,8 +536,67 @@ static int forkPair(const std::function<int(int)>& worker, const char* name) {
   return bad ? 1 : 0;
 }
 
+// test/unit/numa_tests.cc, utils_tests.cc and errors: host utilities as the reference's unit tests
+// call them, plus one kernel on the atomic / poll spellings (a producer block publishes with
+// atomicStore release, a consumer block waits with POLL_MAYBE_JAILBREAK on atomicLoad acquire).
+__global__ void kernelAtomicPoll(int* data, uint32_t* flag, int* out) {
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) {
+      data[0] = 42;
+      mscclpp::atomicStore<uint32_t, mscclpp::scopeDevice>(flag, 1u, mscclpp::memoryOrderRelease);
+    }
+  } else if (threadIdx.x == 0) {
+    POLL_MAYBE_JAILBREAK((mscclpp::atomicLoad<uint32_t, mscclpp::scopeDevice>(flag, mscclpp::memoryOrderAcquire) == 0),
+                         -1);
+    out[0] = data[0];
+    (void)mscclpp::atomicFetchAdd<uint32_t, mscclpp::scopeDevice>(flag, 1u, mscclpp::memoryOrderRelaxed);
+  }
+}
+
+static int runUtils() {
+  int num = 0;
+  MSCCLPP_CUDATHROW(hipGetDeviceCount(&num));
+  for (int i = 0; i < num; i++) {
+    const int node = mscclpp::getDeviceNumaNode(i);
+    CHECK(node >= -1);  // a container without the PCI sysfs entry reports -1
+    if (node >= 0) mscclpp::numaBind(node);
+  }
+  const std::string h1 = mscclpp::getHostName(1024, '.');
+  CHECK(!h1.empty() && h1.size() <= 1024);
+  CHECK(mscclpp::getHostName(1024, h1[0]).empty());
+  CHECK(mscclpp::env()->logLevel.size() > 0 && mscclpp::env() == mscclpp::env());
+  bool threw = false;
+  try {
+    MSCCLPP_CUDATHROW(hipSetDevice(1 << 20));
+  } catch (const mscclpp::CudaError& e) {
+    threw = e.getErrorCode() != 0 && std::string(e.what()).find("Cuda failure") != std::string::npos;
+  }
+  CHECK(threw);
+  (void)hipGetLastError();  // clear the invalid-device error the check above provoked
+  try {
+    throw mscclpp::Error("x", mscclpp::ErrorCode::Timeout);
+  } catch (const mscclpp::BaseError& e) {
+    CHECK(e.getErrorCode() == (int)mscclpp::ErrorCode::Timeout);
+    CHECK(std::string(e.what()) == "x (mscclpp failure: Timeout)");
+  }
+  auto data = mscclpp::detail::gpuCallocShared<int>(1);
+  auto flag = mscclpp::detail::gpuCallocShared<uint32_t>(1);
+  auto out = mscclpp::detail::gpuCallocShared<int>(1);
+  hipLaunchKernelGGL(kernelAtomicPoll, dim3(2), dim3(64), 0, 0, data.get(), flag.get(), out.get());
+  MSCCLPP_CUDATHROW(hipGetLastError());
+  MSCCLPP_CUDATHROW(hipDeviceSynchronize());
+  int o = 0;
+  uint32_t f = 0;
+  MSCCLPP_CUDATHROW(hipMemcpy(&o, out.get(), sizeof(o), hipMemcpyDeviceToHost));
+  MSCCLPP_CUDATHROW(hipMemcpy(&f, flag.get(), sizeof(f), hipMemcpyDeviceToHost));
+  CHECK(o == 42 && f == 2);
+  std::printf("utils OK\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "";
+  if (mode == "utils") return runUtils();
   if (mode == "local") return runLocal();
   if (mode == "context") return runContext();
   if (mode == "pair" && argc > 2) {

@@ -59,3 +59,9 @@ def test_executor_api_reference_plans(built, plan):
     """test/executor_test.cc's sequence on the reference's own 2-rank plans (fixtures)."""
     out = _run(["executor", os.path.join(ROOT, "tests", "golden", "plans", "ref", plan)])
     assert "rank 0 executor OK" in out and "rank 1 executor OK" in out, out
+
+
+def test_host_utilities_errors_and_atomics(built):
+    """test/unit/numa_tests.cc and utils_tests.cc as the reference writes them, the BaseError /
+    CudaError hierarchy, and atomicStore / POLL_MAYBE_JAILBREAK(atomicLoad) between two blocks."""
+    assert "utils OK" in _run(["utils"])
