@@ -327,6 +327,16 @@ def bench_single(args):
                                            "all_threads": cpu_baseline_self_reduce(S, args.cpu_seconds / 2,
                                                                                    cpu_threads())}
         res["host_proxy_baseline"] = hp
+        # the reference's MemoryChannel packet ping-pong latency (memory_channel_tests.cu:98-107), from
+        # the same two host-proxy ranks: on a 1-GPU box both ranks share the GPU
+        pp = (hp or {}).get("pingpong") or {}
+        res["extras"] = {
+            "ll16_pingpong_us": pp.get("ll16", {}).get("us_per_iter"),
+            "ll8_pingpong_us": pp.get("ll8", {}).get("us_per_iter"),
+            "pingpong_correct": (hp or {}).get("pingpong_correct"),
+            "pingpong_note": "us per one-way hand-off of 1024 ints (100k timed iterations, 1 workgroup per rank), "
+                             "two processes on ONE GPU through IPC-mapped packet buffers: a shared-device figure, "
+                             "not an xGMI latency"}
     pk.free()
     return res
 

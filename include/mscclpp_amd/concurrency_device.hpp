@@ -3,9 +3,9 @@
 // workgroups, :28-69) and DeviceSemaphore (a device-wide counting semaphore, :97-132).  Both are
 // plain zero-initialisable structs meant to live in `__device__` globals, as the reference's are.
 //
-// gfx950 details.  The barrier is a generation counter: the last workgroup to arrive resets the
-// arrival count and bumps the generation, the others poll the generation -- no shared "previous
-// flag" that every workgroup rewrites.  A workgroup's stores are written back from its XCD's L2
+// gfx950 details.  The barrier is a generation counter: the last workgroup to arrive subtracts the
+// generation's arrivals from the count and then bumps the generation, the others poll the
+// generation -- no shared "previous flag" that every workgroup rewrites.  A workgroup's stores are written back from its XCD's L2
 // before it arrives (agent-scope release: the barrier spans the 8 XCDs) and the L2 is invalidated
 // after it leaves (acquire), so what one workgroup stored before sync() is what every other one
 // loads after it.  The waits poll with `s_sleep 1` between loads.  maxSpinCount bounds the polls
@@ -29,7 +29,13 @@ struct DeviceSyncer {
       const uint32_t g = __hip_atomic_load(&gen_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       release_agent();
       if (__hip_atomic_fetch_add(&count_, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)blockNum - 1) {
-        __hip_atomic_store(&count_, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // Take this generation's arrivals back out, and only then publish the new generation: a
+        // waiter that sees it may enter the next sync() at once, and its arrival must not be
+        // overwritten by a reset still in flight.  A subtraction (not a store of 0) keeps any such
+        // arrival whatever the order, and the release (fence + s_waitcnt) completes it before the
+        // generation store is issued.
+        __hip_atomic_fetch_sub(&count_, (uint32_t)blockNum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        release_agent();
         __hip_atomic_store(&gen_, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         int64_t spins = 0;

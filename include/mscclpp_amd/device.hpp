@@ -123,17 +123,28 @@ __device__ __forceinline__ void report_error(uint32_t* err, uint32_t code) {
   }
 }
 
-// As report_error; the first reporter also records three diagnostic words in err[1..3] (the error
-// word must then point at >= 16 bytes).
+// As report_error; the first reporter also records three diagnostic words in err[1..3].  Every
+// error word the library allocates or accepts is 4 words (16 bytes) or more: err[0] the code,
+// err[1..3] the detail of the first error.
 __device__ __forceinline__ void report_error_detail(uint32_t* err, uint32_t code, uint32_t a, uint32_t b, uint32_t c) {
   if (!err) return;
   uint32_t expected = kErrNone;
   if (__hip_atomic_compare_exchange_strong(err, &expected, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_SYSTEM)) {
-    err[1] = a;
-    err[2] = b;
-    err[3] = c;
+    __hip_atomic_store(err + 1, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(err + 2, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(err + 3, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// A packet that never carried the expected flag: err[1] = the flag waited for, err[2] = where the
+// packet sits (the byte offset of the packet, or of the 32-byte unit, from the polled region's
+// base), err[3] = the flag word last read there (the first of the packet's flag words that differed).
+// One failure then says which round (flag) and which packet stopped, and whether the slot held an
+// older round's flag (the packet was never written, or was overwritten after it landed) or zero (the
+// slot was cleared after the peer wrote it).
+__device__ __forceinline__ void report_packet_timeout(uint32_t* err, uint32_t flag, uint64_t where, uint32_t seen) {
+  report_error_detail(err, kErrPacketTimeout, flag, (uint32_t)where, seen);
 }
 
 // Release / acquire with the wait the fence needs on gfx950 (MI355X_MICROARCH.md, "Compiler hazard"

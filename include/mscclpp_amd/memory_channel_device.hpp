@@ -135,7 +135,7 @@ struct MemoryChannelDeviceHandle : public BaseMemoryChannelDeviceHandle {
           do {
             v = load16<kSystem>(r, off);
             if (g.expired()) {
-              report_error(semaphore_.err, kErrPacketTimeout);
+              report_packet_timeout(semaphore_.err, flag, targetOffset + i * 16, v.y != flag ? v.y : v.w);
               break;
             }
           } while (!LL16Packet::ready(v, flag));
@@ -152,7 +152,7 @@ struct MemoryChannelDeviceHandle : public BaseMemoryChannelDeviceHandle {
           do {
             v = load8<kSystem>(r, off);
             if (g.expired()) {
-              report_error(semaphore_.err, kErrPacketTimeout);
+              report_packet_timeout(semaphore_.err, flag, targetOffset + i * 8, v.y);
               break;
             }
           } while (v.y != flag);

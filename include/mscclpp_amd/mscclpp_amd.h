@@ -226,6 +226,12 @@ int mscclppAmdCommRegisterBuffer(ncclComm_t comm, void* ptr, void** peers);
  * when buffers that were used with the communicator are freed. */
 int mscclppAmdCommDeregisterAll(ncclComm_t comm);
 int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear);
+/* The communicator's whole error record: words4[0] = the code (as above), words4[1..3] = the detail
+ * its first reporter wrote.  kErrPacketTimeout (1): the flag waited for, the byte offset of the
+ * packet (or 32-byte unit) in the polled region, the flag word last read there; semaphore timeouts
+ * of the bulk and executor kernels: channel / block / expected value.  clear != 0
+ * zeroes all four words. */
+int mscclppAmdCommGetDeviceErrorDetail(ncclComm_t comm, uint32_t* words4, int clear);
 /* Registration cache state: user buffers registered (at most 64, least recently used retired
  * beyond), IPC mappings open in this process (all communicators), mappings waiting for a device
  * synchronize before they close.  Any pointer may be NULL. */
@@ -276,6 +282,18 @@ int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int* failures,
  * 4 GiB) on one GPU, nblocks x 256 lanes as one thread group; bad[0..3] = words that differ from the
  * source pattern after each of the four (memory_channel_device.hpp:101-215 take 64-bit offsets). */
 int mscclppAmdMemChannelBigTest(uint64_t bytes, int nblocks, unsigned long long* bad, uint32_t* devErr);
+/* The reference's MemoryChannel packet ping-pong latency (test/mp_unit/memory_channel_tests.cu:
+ * 98-107), collective over a 2-rank communicator: a MemoryChannel into the peer's packet buffer built
+ * with the host API, 1000 checked tries, then `iters` timed one-way hand-offs of nElem ints as LL8
+ * (ll8 != 0) or LL16 packets.  out[0] = us per iteration (host clock between the barriers around the
+ * launch), out[1] = 1 if every receive matched and no device error was recorded, out[2..5] (when
+ * outLen allows) = the error record: code, flag, packet byte, flag seen. */
+int mscclppAmdMemChannelPingPong(ncclComm_t comm, int nElem, int iters, int ll8, double* out, int outLen);
+/* One rank's ping-pong kernel: `handle` = a host MemoryChannelDeviceHandle (dst_ = the peer's packet
+ * buffer, packetBuffer_ = this rank's), rank 0 or 1, flags flagBase + 1 ... flagBase + nTries,
+ * *ret = 1 on a mismatch. */
+int mscclppAmdLaunchMemChannelPingPong(const void* handle, int* buff, int rank, int nElem, int nTries,
+                                       uint32_t flagBase, int ll8, int* ret, void* stream);
 
 /* ---- bootstrap (TcpBootstrap, src/core/bootstrap/bootstrap.cc:169-611) -------------------------
  * Host-only setup plane; uniqueId is the 128-byte ncclUniqueId from ncclGetUniqueId. */

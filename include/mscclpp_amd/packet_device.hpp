@@ -67,13 +67,16 @@ union alignas(16) LL16Packet {
     data.y = v2;
     return !ok;
   }
-  // Spin until both flags match; on timeout record kErrPacketTimeout and return zeros.
-  __device__ __forceinline__ bool read(uint32_t flag, uint32_t& v1, uint32_t& v2, uint64_t budget,
-                                       uint32_t* err) const {
+  // Spin until both flags match; on timeout record kErrPacketTimeout with the flag, `where` (the
+  // packet's byte offset in its region) and the flag word seen, and return zeros.
+  __device__ __forceinline__ bool read(uint32_t flag, uint32_t& v1, uint32_t& v2, uint64_t budget, uint32_t* err,
+                                       uint64_t where = 0) const {
     SpinGuard g(budget);
     while (!readOnce(flag, v1, v2)) {
       if (g.expired()) {
-        report_error(err, kErrPacketTimeout);
+        const uint64_t* q = reinterpret_cast<const uint64_t*>(this);
+        const uint32_t f1 = (uint32_t)(ld_relaxed_sys(q) >> 32), f2 = (uint32_t)(ld_relaxed_sys(q + 1) >> 32);
+        report_packet_timeout(err, flag, where, f1 != flag ? f1 : f2);
         v1 = v2 = 0;
         return false;
       }
@@ -120,11 +123,12 @@ union alignas(8) LL8Packet {
     data = (uint32_t)x;
     return (uint32_t)(x >> 32) != flag;
   }
-  __device__ __forceinline__ bool read(uint32_t flag, uint32_t& v, uint64_t budget, uint32_t* err) const {
+  __device__ __forceinline__ bool read(uint32_t flag, uint32_t& v, uint64_t budget, uint32_t* err,
+                                       uint64_t where = 0) const {
     SpinGuard g(budget);
     while (readOnce(flag, v)) {
       if (g.expired()) {
-        report_error(err, kErrPacketTimeout);
+        report_packet_timeout(err, flag, where, (uint32_t)(ld_relaxed_sys(&raw) >> 32));
         v = 0;
         return false;
       }
@@ -169,6 +173,14 @@ __device__ __forceinline__ bool ll16_try_unit(__amdgpu_buffer_rsrc_t pkts, uint3
   return LL16Packet::ready(a, flag) && LL16Packet::ready(b, flag);
 }
 
+// Timeout detail of a 32-byte unit (two LL16 or four LL8 packets; flag words 1 and 3 of each
+// 16 bytes): the first flag word that differs from `flag`, re-read once.
+template <int LoadPolicy>
+__device__ __forceinline__ uint32_t unit_flag_seen(__amdgpu_buffer_rsrc_t pkts, uint32_t pbyte, uint32_t flag) {
+  const u32x4 a = load16<LoadPolicy>(pkts, pbyte), b = load16<LoadPolicy>(pkts, pbyte + 16);
+  return a.y != flag ? a.y : a.w != flag ? a.w : b.y != flag ? b.y : b.w;
+}
+
 template <int LoadPolicy = kSystem>
 __device__ __forceinline__ u32x4 ll16_get_unit(__amdgpu_buffer_rsrc_t pkts, uint32_t pbyte, uint32_t flag,
                                                uint64_t budget, uint32_t* err) {
@@ -177,7 +189,7 @@ __device__ __forceinline__ u32x4 ll16_get_unit(__amdgpu_buffer_rsrc_t pkts, uint
   SpinGuard g(budget);
   while (!ll16_try_unit<LoadPolicy>(pkts, pbyte, flag, w)) {
     if (g.expired()) {
-      report_error(err, kErrPacketTimeout);
+      report_packet_timeout(err, flag, pbyte, unit_flag_seen<LoadPolicy>(pkts, pbyte, flag));
       return u32x4{0, 0, 0, 0};
     }
   }
@@ -216,7 +228,7 @@ __device__ __forceinline__ u32x4 ll8_get_unit(__amdgpu_buffer_rsrc_t pkts, uint3
   SpinGuard g(budget);
   while (!ll8_try_unit(pkts, pbyte, flag, w)) {
     if (g.expired()) {
-      report_error(err, kErrPacketTimeout);
+      report_packet_timeout(err, flag, pbyte, unit_flag_seen<kSystem>(pkts, pbyte, flag));
       return u32x4{0, 0, 0, 0};
     }
   }
@@ -238,7 +250,7 @@ __device__ __forceinline__ void copyFromPacketsLL16(void* dst, const void* src, 
   uint32_t* d = reinterpret_cast<uint32_t*>(dst);
   for (uint64_t i = tid; i < bytes / 8; i += nthreads) {
     uint32_t v1, v2;
-    s[i].read(flag, v1, v2, budget, err);
+    s[i].read(flag, v1, v2, budget, err, i * 16);
     d[2 * i] = v1;
     d[2 * i + 1] = v2;
   }
@@ -255,7 +267,7 @@ __device__ __forceinline__ void copyFromPacketsLL8(void* dst, const void* src, u
   uint32_t* d = reinterpret_cast<uint32_t*>(dst);
   for (uint64_t i = tid; i < bytes / 4; i += nthreads) {
     uint32_t v;
-    s[i].read(flag, v, budget, err);
+    s[i].read(flag, v, budget, err, i * 8);
     d[i] = v;
   }
 }

@@ -143,6 +143,7 @@ def lib():
         "mscclppAmdReduceType": [i32, i32],
         "mscclppAmdCommBarrier": [vp],
         "mscclppAmdCommGetDeviceError": [vp, ctypes.POINTER(ctypes.c_uint32), i32],
+        "mscclppAmdCommGetDeviceErrorDetail": [vp, ctypes.POINTER(ctypes.c_uint32), i32],
         "mscclppAmdCommScratch": [vp, ctypes.POINTER(vp), ctypes.POINTER(sz)],
         "mscclppAmdCommRegistrationStats": [vp, ctypes.POINTER(sz), ctypes.POINTER(sz), ctypes.POINTER(sz)],
         "mscclppAmdCommRegistrationExchanges": [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
@@ -558,6 +559,13 @@ class Communicator:
         c = ctypes.c_uint32()
         check(lib().mscclppAmdCommGetDeviceError(self.comm, ctypes.byref(c), 1 if clear else 0), "device error")
         return c.value
+
+    def device_error_detail(self, clear=True):
+        """[code, detail1, detail2, detail3]: for a packet timeout, the flag waited for, the packet's
+        byte offset in the polled region and the flag word last read there."""
+        w = (ctypes.c_uint32 * 4)()
+        check(lib().mscclppAmdCommGetDeviceErrorDetail(self.comm, w, 1 if clear else 0), "device error detail")
+        return list(w)
 
     def async_error(self):
         """ncclCommGetAsyncError: 0 (ncclSuccess), or 6 (ncclRemoteError) once a wait timed out."""

@@ -580,6 +580,15 @@ int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear) {
   });
 }
 
+int mscclppAmdCommGetDeviceErrorDetail(ncclComm_t comm, uint32_t* words4, int clear) {
+  return guarded([&] {
+    if (!comm || !words4) return (int)ncclInvalidArgument;
+    HIPCHECK(hipMemcpy(words4, comm->err, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (clear) HIPCHECK(hipMemset(comm->err, 0, 4 * sizeof(uint32_t)));
+    return (int)ncclSuccess;
+  });
+}
+
 int mscclppAmdCommRegistrationStats(ncclComm_t comm, size_t* userRegistrations, size_t* liveMappings,
                                     size_t* retiredMappings) {
   if (!comm) return ncclInvalidArgument;

@@ -85,18 +85,26 @@ bool pendingFits(UncachedPool& P, int dev, size_t cls) {
   return false;
 }
 
-// Move every pending block of `dev` to the free lists once the device has drained (the current
-// device is `dev`); blocks of a device that cannot synchronize are leaked.
+// Move the pending blocks of `dev` to the free lists once the device has drained (the current
+// device is `dev`); blocks of a device that cannot synchronize are leaked.  Only the blocks pending
+// BEFORE the synchronize are moved: they are taken out under the lock first, then the device is
+// synchronized, then they join the free lists.  A block another thread releases in between (its
+// kernels possibly queued after the synchronize returned) stays pending until the next drain.
 void drainPending(UncachedPool& P, int dev) {
+  std::vector<std::pair<size_t, void*>> snapshot;
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (auto it = P.pending.lower_bound({dev, 0}); it != P.pending.end() && it->first.first == dev; ++it) {
+      for (void* b : it->second) snapshot.emplace_back(it->first.second, b);
+      it->second.clear();
+    }
+  }
   const hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) (void)hipGetLastError();
   std::lock_guard<std::mutex> lk(P.mu);
-  for (auto it = P.pending.lower_bound({dev, 0}); it != P.pending.end() && it->first.first == dev; ++it) {
-    for (void* b : it->second) {
-      if (e == hipSuccess) P.freeBlocks[it->first].push_back(b);
-      else P.leaked += it->first.second;
-    }
-    it->second.clear();
+  for (const auto& sb : snapshot) {
+    if (e == hipSuccess) P.freeBlocks[{dev, sb.first}].push_back(sb.second);
+    else P.leaked += sb.first;
   }
 }
 

@@ -73,6 +73,13 @@ __device__ __forceinline__ bool unit_try(__amdgpu_buffer_rsrc_t pk, uint32_t pby
   w = u32x2{a.x, 0};
   return a.y == flag;
 }
+// Timeout detail of one packet unit: the first of its flag words that differs from `flag`, re-read.
+__device__ __forceinline__ uint32_t unit_flag_seen(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag,
+                                                   bool single) {
+  if (single) return load8<kSystem>(pk, pbyte).y;
+  const u32x4 a = load16<kSystem>(pk, pbyte);
+  return a.y != flag ? a.y : a.w;
+}
 __device__ __forceinline__ u32x2 unit_get(__amdgpu_buffer_rsrc_t pk, uint32_t pbyte, uint32_t flag, bool single,
                                           uint64_t budget, uint32_t* err) {
   u32x2 w;
@@ -81,7 +88,7 @@ __device__ __forceinline__ u32x2 unit_get(__amdgpu_buffer_rsrc_t pk, uint32_t pb
   while (!unit_try(pk, pbyte, flag, w, single)) {
     __builtin_amdgcn_s_sleep(1);
     if (g.expired()) {
-      report_error(err, kErrPacketTimeout);
+      report_packet_timeout(err, flag, pbyte, unit_flag_seen(pk, pbyte, flag, single));
       return u32x2{0, 0};
     }
   }
@@ -147,7 +154,7 @@ __device__ __forceinline__ u32x2 unit_wait(__amdgpu_buffer_rsrc_t pk, uint32_t p
     __builtin_amdgcn_s_sleep(1);
     if (unit_try(pk, pbyte, flag, w, single)) return w;
   } while (!g.expired());
-  report_error(err, kErrPacketTimeout);
+  report_packet_timeout(err, flag, pbyte, unit_flag_seen(pk, pbyte, flag, single));
   return u32x2{0, 0};
 }
 // Wave-level readiness probe (LL16 step 3 from kSentinelUnits units per slice): one lane polls the

@@ -66,6 +66,48 @@ __global__ void memChanSelfTestKernel(MemoryChannelDeviceHandle* chans, int* b0,
   }
 }
 
+// ---- two-process packet ping-pong (the reference's latency measurement) ------------------------
+// test/mp_unit/memory_channel_tests.cu:98-107 with kernelMemLL8/LL16PacketPingPong (:246-325): rank 0
+// and rank 1 take turns, round i's sender (rank == i & 1) fills its buffer and putPackets it into the
+// peer's packet buffer with flag flagBase + i + 1, the receiver unpackPackets and checks.  One
+// 1024-lane workgroup per rank.
+__global__ void memChanPingPongKernel(MemoryChannelDeviceHandle ch, int* buff, int rank, int nElem, int nTries,
+                                      uint32_t flagBase, int ll8, int* ret) {
+  // Lane t fills, and after the receive checks, exactly the words its own packets carry (LL8
+  // packet t: word t; LL16 packet t: words 2t, 2t + 1), so no workgroup barrier is needed between
+  // the fill and the put or between the unpack and the check -- the reference kernels' pattern.
+  volatile int* sendBuff = buff;
+  const int putOffset = rank == 0 ? 0 : 10000000;
+  const int getOffset = rank == 0 ? 10000000 : 0;
+  const int wordsPerPacket = ll8 ? 1 : 2;
+  const int nPkt = nElem / wordsPerPacket;
+  for (int i = 0; i < nTries; ++i) {
+    const uint32_t flag = flagBase + (uint32_t)i + 1;
+    if ((rank ^ (i & 1)) == 0) {
+      for (int t = threadIdx.x; t < nPkt; t += blockDim.x)
+        for (int w = 0; w < wordsPerPacket; ++w) {
+          const int j = t * wordsPerPacket + w;
+          sendBuff[j] = putOffset + i + j;
+        }
+      if (ll8)
+        ch.putPackets<LL8Packet>(0, 0, (uint64_t)nElem * 4, threadIdx.x, blockDim.x, flag);
+      else
+        ch.putPackets<LL16Packet>(0, 0, (uint64_t)nElem * 4, threadIdx.x, blockDim.x, flag);
+    } else {
+      if (ll8)
+        ch.unpackPackets<LL8Packet>(0, 0, (uint64_t)nElem * 4, threadIdx.x, blockDim.x, flag);
+      else
+        ch.unpackPackets<LL16Packet>(0, 0, (uint64_t)nElem * 4, threadIdx.x, blockDim.x, flag);
+      for (int t = threadIdx.x; t < nPkt; t += blockDim.x)
+        for (int w = 0; w < wordsPerPacket; ++w) {
+          const int j = t * wordsPerPacket + w;
+          if (sendBuff[j] != getOffset + i + j) *ret = 1;
+        }
+    }
+    __syncthreads();
+  }
+}
+
 // ---- buffers beyond 4 GiB (the primitives' buffer resources are rebased window by window) -------
 // word i of the pattern: distinct for words 2^30 apart, so a copy that wrapped at 4 GiB shows
 __device__ __forceinline__ uint32_t bigPattern(uint64_t i) {
@@ -164,6 +206,17 @@ done:
   return rc;
 }
 
+// One rank's side of the ping-pong; `handle` points at a host MemoryChannelDeviceHandle (dst_ = the
+// peer's packet buffer, src_ = buff, packetBuffer_ = this rank's packet buffer).
+extern "C" int mscclppAmdLaunchMemChannelPingPong(const void* handle, int* buff, int rank, int nElem, int nTries,
+                                                  uint32_t flagBase, int ll8, int* ret, void* stream) {
+  if (!handle || !buff || !ret || rank < 0 || rank > 1 || nElem <= 0 || nElem % 2 || nTries <= 0) return 4;
+  const MemoryChannelDeviceHandle h = *static_cast<const MemoryChannelDeviceHandle*>(handle);
+  hipLaunchKernelGGL(memChanPingPongKernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, h, buff, rank, nElem, nTries,
+                     flagBase, ll8, ret);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // Returns 0 on success, the mismatch count in *failures, any device error code in *devErr.
 extern "C" int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int* failures, uint32_t* devErr) {
   if (!failures || !devErr || nElem <= 0 || nElem % 2 || mode < 0 || mode > 2) return 4;
@@ -191,8 +244,8 @@ extern "C" int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int
   CK(hipMemset(exp, 0, 64));
   CK(hipMalloc((void**)&ret, 4));
   CK(hipMemset(ret, 0, 4));
-  CK(hipMalloc((void**)&err, 4));
-  CK(hipMemset(err, 0, 4));
+  CK(hipMalloc((void**)&err, 16));  // code + the three detail words of a packet timeout
+  CK(hipMemset(err, 0, 16));
   {
     MemoryChannelDeviceHandle h[2];
     for (int r = 0; r < 2; ++r) {

@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(64 * W) selfReduceLL16LdsKernel(const uint8_t*
             do {
               v[i2] = load16<kSystem>(rp, off);
               if (g.expired()) {
-                report_error(err, kErrPacketTimeout);
+                report_packet_timeout(err, flag, 2 * c + off, v[i2].y != flag ? v[i2].y : v[i2].w);
                 break;
               }
             } while (!LL16Packet::ready(v[i2], flag));

@@ -17,6 +17,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -47,18 +48,27 @@ using mscclpp::DeviceHandle;
 
 static int gRank = -1;
 
+// Flag ranges of the packet ping-pongs.  Each (size, packet type) case and the timed run get a range
+// of their own, so a packet slot never holds a flag a later case waits for: no clear of the packet
+// buffer is needed between cases (the reference's packetPingPongTest does not clear either,
+// memory_channel_tests.cu:91-96).
+constexpr uint32_t kCaseFlagStride = 1u << 12;      // >= nTries of a correctness case (1000)
+constexpr uint32_t kTimedFlagBase = 1u << 20;       // the timed ping-pongs: up to 2^20 tries each
+constexpr uint32_t kUnpackFlagBase = 3u << 21;      // unpackPacket: beyond both timed ranges
+constexpr int kTimedTries = 100000;                 // timed ping-pong iterations (>= 100k)
+
 __constant__ DeviceHandle<mscclpp::MemoryChannel> gChannelOneToOneTestConstMemChans;
 __constant__ DeviceHandle<mscclpp::PortChannel> gChannelOneToOneTestConstPortChans;
 
 // ---- memory channel ---------------------------------------------------------------------------
-__global__ void kernelMemLL8PacketPingPong(int* buff, int rank, int nElem, int* ret, int nTries) {
+__global__ void kernelMemLL8PacketPingPong(int* buff, int rank, int nElem, int* ret, int nTries, uint32_t flagBase) {
   if (rank > 1) return;
   DeviceHandle<mscclpp::MemoryChannel>& memChan = gChannelOneToOneTestConstMemChans;
   volatile int* sendBuff = (volatile int*)buff;
   int putOffset = (rank == 0) ? 0 : 10000000;
   int getOffset = (rank == 0) ? 10000000 : 0;
   for (int i = 0; i < nTries; i++) {
-    uint64_t flag = (uint64_t)i + 1;
+    uint64_t flag = (uint64_t)flagBase + i + 1;
     if ((rank ^ (i & 1)) == 0) {
       for (int j = threadIdx.x; j < nElem; j += blockDim.x) sendBuff[j] = putOffset + i + j;
       memChan.putPackets<mscclpp::LL8Packet>(0, 0, nElem * sizeof(int), threadIdx.x, blockDim.x, flag);
@@ -75,14 +85,14 @@ __global__ void kernelMemLL8PacketPingPong(int* buff, int rank, int nElem, int* 
   }
 }
 
-__global__ void kernelMemLL16PacketPingPong(int* buff, int rank, int nElem, int* ret, int nTries) {
+__global__ void kernelMemLL16PacketPingPong(int* buff, int rank, int nElem, int* ret, int nTries, uint32_t flagBase) {
   if (rank > 1) return;
   DeviceHandle<mscclpp::MemoryChannel>& memChan = gChannelOneToOneTestConstMemChans;
   volatile int* sendBuff = (volatile int*)buff;
   int putOffset = (rank == 0) ? 0 : 10000000;
   int getOffset = (rank == 0) ? 10000000 : 0;
   for (int i = 0; i < nTries; i++) {
-    uint64_t flag = (uint64_t)i + 1;
+    uint64_t flag = (uint64_t)flagBase + i + 1;
     if ((rank ^ (i & 1)) == 0) {
       for (int j = threadIdx.x; j < nElem / 2; j += blockDim.x) {
         sendBuff[2 * j] = putOffset + i + 2 * j;
@@ -109,7 +119,7 @@ __global__ void kernelMemUnpackPacket(int* buff, int rank, int nElem, int* ret, 
   int putOffset = (rank == 0) ? 0 : 10000000;
   int getOffset = (rank == 0) ? 10000000 : 0;
   for (int i = 0; i < nTries; i++) {
-    uint32_t flag = (uint32_t)(100000 + i);  // beyond every flag the ping-pongs above used
+    uint32_t flag = (uint32_t)(kUnpackFlagBase + i);  // beyond every flag the ping-pongs above used
     if ((rank ^ (i & 1)) == 0) {
       for (int j = threadIdx.x; j < nElem; j += blockDim.x) sendBuff[j] = putOffset + i + 7 * j;
       memChan.putPackets(0, 0, nElem * sizeof(int), threadIdx.x, blockDim.x, flag);
@@ -323,20 +333,40 @@ static int worker(int rank, ncclUniqueId id, int nElemMax) {
 
   auto sem = std::make_shared<mscclpp::MemoryDevice2DeviceSemaphore>(*comm, conn);
   int* r = ret.get();
-  auto run = [&](const char* name, auto kernel, int nElem, int nTries) {
+  // A failed case prints the error record: for a packet timeout the flag waited for, the packet's
+  // byte offset and the flag word last read there (mscclppAmdCommGetDeviceErrorDetail).
+  auto verdict = [&](const char* name, int nElem, int h) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    CHECK(mscclppAmdCommGetDeviceErrorDetail(comm->ncclComm(), w, 1) == 0);
+    if (h != 0 || w[0] != 0) {
+      std::fprintf(stderr, "[rank %d] %s nElem %d: ret %d device error %u (flag %u, packet byte %u, flag seen %u)\n",
+                   rank, name, nElem, h, w[0], w[1], w[2], w[3]);
+      std::exit(1);
+    }
+  };
+  // Every host-side fill (hipMemset of the result word) has completed on the device before the
+  // barrier that lets the peer launch: a fill still queued behind the barrier could land after the
+  // peer's first stores.
+  auto launch = [&](auto&& go) {
     HIP_OK(hipMemset(r, 0, sizeof(int)));
+    HIP_OK(hipDeviceSynchronize());
     comm->bootstrap()->barrier();
-    hipLaunchKernelGGL(kernel, dim3(1), dim3(1024), 0, 0, buff.get(), rank, nElem, r, nTries);
+    go();
     HIP_OK(hipGetLastError());
     HIP_OK(hipDeviceSynchronize());
     int h = -1;
     HIP_OK(hipMemcpy(&h, r, sizeof(int), hipMemcpyDeviceToHost));
-    uint32_t code = 0;
-    CHECK(mscclppAmdCommGetDeviceError(comm->ncclComm(), &code, 1) == 0);
-    if (h != 0 || code != 0) {
-      std::fprintf(stderr, "[rank %d] %s nElem %d: ret %d device error %u\n", rank, name, nElem, h, code);
-      std::exit(1);
-    }
+    return h;
+  };
+  auto run = [&](const char* name, auto kernel, int nElem, int nTries) {
+    const int h = launch([&] { hipLaunchKernelGGL(kernel, dim3(1), dim3(1024), 0, 0, buff.get(), rank, nElem, r, nTries); });
+    verdict(name, nElem, h);
+    comm->bootstrap()->barrier();
+  };
+  auto runPkt = [&](const char* name, auto kernel, int nElem, int nTries, uint32_t flagBase) {
+    const int h = launch(
+        [&] { hipLaunchKernelGGL(kernel, dim3(1), dim3(1024), 0, 0, buff.get(), rank, nElem, r, nTries, flagBase); });
+    verdict(name, nElem, h);
     comm->bootstrap()->barrier();
   };
   {
@@ -344,14 +374,49 @@ static int worker(int rank, ncclUniqueId id, int nElemMax) {
     mscclpp::MemoryChannel memChan(sem, remotePkt, buffMem, pkt.get());
     DeviceHandle<mscclpp::MemoryChannel> h = mscclpp::deviceHandle(memChan);
     HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(gChannelOneToOneTestConstMemChans), &h, sizeof(h)));
+    // correctness: 1000 tries per size and packet type, each case in a flag range of its own
+    // (memory_channel_tests.cu:91-96; the packet buffer is zeroed once, at allocation)
+    uint32_t flagBase = 0;
     for (int n : {2, 1024, 1024 * 1024}) {
       if (n > nElemMax) continue;
-      HIP_OK(hipMemset(pkt.get(), 0, bytes * 2));
-      comm->bootstrap()->barrier();
-      run("LL8 ping-pong", kernelMemLL8PacketPingPong, n, 1000);
-      HIP_OK(hipMemset(pkt.get(), 0, bytes * 2));
-      comm->bootstrap()->barrier();
-      run("LL16 ping-pong", kernelMemLL16PacketPingPong, n, 1000);
+      runPkt("LL8 ping-pong", kernelMemLL8PacketPingPong, n, 1000, flagBase);
+      flagBase += kCaseFlagStride;
+      runPkt("LL16 ping-pong", kernelMemLL16PacketPingPong, n, 1000, flagBase);
+      flagBase += kCaseFlagStride;
+    }
+    CHECK(flagBase < kTimedFlagBase);
+    // timed: kTimedTries one-way hand-offs of 1024 ints, the reference's latency measurement
+    // (memory_channel_tests.cu:98-107: host timer between barriers around one launch, us/iter)
+    if (nElemMax >= 1024) {
+      const char* names[2] = {"LL8 ping-pong (timed)", "LL16 ping-pong (timed)"};
+      double usPerIter[2] = {0, 0};
+      for (int k = 0; k < 2; ++k) {
+        HIP_OK(hipMemset(r, 0, sizeof(int)));
+        HIP_OK(hipDeviceSynchronize());
+        comm->bootstrap()->barrier();
+        const auto t0 = std::chrono::steady_clock::now();
+        if (k == 0)
+          hipLaunchKernelGGL(kernelMemLL8PacketPingPong, dim3(1), dim3(1024), 0, 0, buff.get(), rank, 1024, r,
+                             kTimedTries, kTimedFlagBase);
+        else
+          hipLaunchKernelGGL(kernelMemLL16PacketPingPong, dim3(1), dim3(1024), 0, 0, buff.get(), rank, 1024, r,
+                             kTimedTries, kTimedFlagBase + (1u << 20));
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipDeviceSynchronize());
+        comm->bootstrap()->barrier();
+        usPerIter[k] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() /
+                       kTimedTries;
+        int h = -1;
+        HIP_OK(hipMemcpy(&h, r, sizeof(int), hipMemcpyDeviceToHost));
+        verdict(names[k], 1024, h);
+      }
+      if (rank == 0)  // framework.cc:339-345's [   PERF   ] lines
+        std::printf("[   PERF   ] MemoryChannelOneToOneTest.PacketPingPong\n"
+                    "[   PERF   ]        LL8 latency: %.4g us/iter\n"
+                    "[   PERF   ]       LL16 latency: %.4g us/iter\n"
+                    "PINGPONG_JSON {\"ll8_pingpong_us\": %.4f, \"ll16_pingpong_us\": %.4f, \"nElem\": 1024, "
+                    "\"iters\": %d}\n",
+                    usPerIter[0], usPerIter[1], usPerIter[0], usPerIter[1], kTimedTries);
     }
     run("unpackPacket", kernelMemUnpackPacket, 4096, 50);
   }
@@ -382,6 +447,7 @@ static int worker(int rank, ncclUniqueId id, int nElemMax) {
         if (n > nElemMax) continue;
         HIP_OK(hipMemset(getPkt.get(), 0, pktBytes));
         HIP_OK(hipMemset(r, 0, sizeof(int)));
+        HIP_OK(hipDeviceSynchronize());  // both fills have landed before the peer may put into getPkt
         comm->bootstrap()->barrier();
         hipLaunchKernelGGL(kernelProxyLLPingPong, dim3(1), dim3(1024), 0, 0, buff.get(), putPkt.get(), getPkt.get(),
                            rank, n, 1000, r);
@@ -389,12 +455,7 @@ static int worker(int rank, ncclUniqueId id, int nElemMax) {
         HIP_OK(hipDeviceSynchronize());
         int hr = -1;
         HIP_OK(hipMemcpy(&hr, r, sizeof(int), hipMemcpyDeviceToHost));
-        uint32_t code = 0;
-        CHECK(mscclppAmdCommGetDeviceError(comm->ncclComm(), &code, 1) == 0);
-        if (hr != 0 || code != 0) {
-          std::fprintf(stderr, "[rank %d] proxy LL ping-pong nElem %d: ret %d device error %u\n", rank, n, hr, code);
-          std::exit(1);
-        }
+        verdict("proxy LL ping-pong", n, hr);
         comm->bootstrap()->barrier();
       }
     }

@@ -13,6 +13,7 @@
   algorithm/): PortChannels through ProxyService, reached through ncclAllGather, direct and
   graph-captured, exact.
 Both C++ programs include the reference's header paths (include/mscclpp/*.hpp) and spell mscclpp::."""
+import json
 import os
 import subprocess
 
@@ -45,6 +46,12 @@ def test_fifo_known_answers_on_device(built):
 def test_memory_and_port_channels_reference_spellings(built):
     out = _run("test_channels", ["gpu", str(1 << 20)], 200)
     assert "gpu OK" in out and "rank 0 OK" in out and "rank 1 OK" in out, out
+    # the timed 1024-int ping-pongs (memory_channel_tests.cu:98-107), printed in framework.cc's form
+    line = [x for x in out.splitlines() if x.startswith("PINGPONG_JSON ")]
+    assert len(line) == 1 and "LL16 latency:" in out and "LL8 latency:" in out, out
+    pp = json.loads(line[0].split(" ", 1)[1])
+    assert pp["iters"] >= 100000 and 0 < pp["ll8_pingpong_us"] < 1000 and 0 < pp["ll16_pingpong_us"] < 1000, pp
+    print(line[0])
 
 
 @pytest.mark.gpu
@@ -66,3 +73,12 @@ def test_port_channel_strict_refuses_cached_destination(built, n):
     ncclInvalidUsage and the reason in ncclGetLastError, on every rank and with no rank left waiting."""
     out = _run("test_customized_allgather", ["gpu", str(n), str(1 << 12), "refuse"], 120)
     assert "gpu OK" in out and all(f"rank {r} refused OK" in out for r in range(n)), out
+
+
+@pytest.mark.gpu
+def test_device_syncer_back_to_back(built):
+    """DeviceSyncer.sync() called back to back by 128 workgroups for 3 x 20000 rounds (two
+    barriers each): no arrival lost to the previous generation's reset (no spin-bound expiry) and
+    every slot stored before a barrier is read after it."""
+    out = _run("test_device_syncer", ["gpu", "128", "20000"], 100)
+    assert "gpu OK" in out and "mismatches 0 timedOut 0" in out, out

@@ -21,3 +21,17 @@ def test_host_offload_and_portchannel_four_ranks(built):
     assert r["correct"] is True and r["ranks"] == 4 and r["cores"] == 8
     for mode, row in r["portchannel_alltoall_1MiB"].items():
         assert row["correct"] is True, mode
+
+
+def test_memory_channel_pingpong_two_ranks(built):
+    """The reference's MemoryChannel packet ping-pong latency (memory_channel_tests.cu:98-107) through
+    the library entry the bench line uses: both packet types correct over 1000 checked and 100k timed
+    one-way hand-offs of 1024 ints, with a finite us/iter (two processes sharing this GPU)."""
+    import host_proxy_baseline as H
+
+    r = H.run(2, 4096, timeout=150)
+    assert r["correct"] is True and r["pingpong_correct"] is True, r.get("pingpong")
+    for name in ("ll16", "ll8"):
+        row = r["pingpong"][name]
+        assert row["error_record"] == [0, 0, 0, 0] and 0 < row["us_per_iter"] < 1000, (name, row)
+    print("pingpong", r["pingpong"])

@@ -185,3 +185,60 @@ def test_create_destroy_cycles_pool_and_imports_bounded(built):
         assert res["capture_code"] == 5, (rank, res)  # ncclInvalidUsage
         assert res["bad_graph"] == 0, (rank, res)
         assert res["released"] >= kept[0] and res["kept_after_release"] == 0, (rank, res)
+
+
+def test_uncached_pool_release_during_reuse_drain(built):
+    """a block released by another thread while an allocation drains the pool's pending
+    list must not be handed out before its own queued work has run.  One thread keeps allocating
+    pooled blocks, queuing a delayed fill of 0xAB into each on its own stream and freeing it at once
+    (no synchronize); another keeps allocating the same size class and requires every block it gets
+    to read back all zero (the pool's zero fill ran after, not before, the previous owner's fill)."""
+    import threading
+
+    import torch
+
+    import mscclpp_amd as m
+
+    torch.cuda.set_device(0)
+    nbytes, rounds = 1 << 20, 300
+    bad, errors = [], []
+
+    def writer():
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for _ in range(rounds):
+                    b = m.DeviceBuffer(nbytes)
+                    v = m.device_view(b.ptr, nbytes)
+                    torch.cuda._sleep(20000)  # the fill lands well after the free below
+                    v.fill_(0xAB)
+                    b.free()  # no synchronize: the block goes to the pending list with its fill queued
+            s.synchronize()
+        except Exception:  # noqa: BLE001
+            errors.append(traceback.format_exc())
+
+    def reader():
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for i in range(rounds):
+                    b = m.DeviceBuffer(nbytes)
+                    v = m.device_view(b.ptr, nbytes)
+                    nz = int(torch.count_nonzero(v).item())
+                    if nz:
+                        bad.append((i, nz))
+                    b.free()
+        except Exception:  # noqa: BLE001
+            errors.append(traceback.format_exc())
+
+    ts = [threading.Thread(target=writer), threading.Thread(target=reader)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    torch.cuda.synchronize()
+    assert not any(t.is_alive() for t in ts), "pool stress threads did not finish"
+    assert not errors, errors[0]
+    assert not bad, f"{len(bad)} reused blocks held the previous owner's late fill, first {bad[:3]}"

@@ -13,6 +13,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+PINGPONG_ITERS = 100000  # timed MemoryChannel ping-pong iterations (>= 100k)
 PC_ITERS = 20  # PortChannel all-to-all iterations per mode (median / min / max over >= 20)
 
 
@@ -47,6 +48,19 @@ def worker(rank, n, uid, size, q):
                 "mean_us_wall": round(o[0], 2), "slowest_iteration": int(o[6]), "iterations": PC_ITERS,
                 "proxy_max_poll_gap_us": round(o[7], 1), "correct": o[1] == 1.0}
         res["portchannel_alltoall_1MiB"] = pc
+        if n == 2:
+            # the reference's MemoryChannel packet ping-pong latency (memory_channel_tests.cu:98-107):
+            # 1024 ints, PINGPONG_ITERS one-way hand-offs per packet type after 1000 checked ones
+            L.mscclppAmdMemChannelPingPong.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                       ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+            pp = {}
+            for name, ll8 in (("ll16", 0), ("ll8", 1)):
+                print(f"[host_proxy rank {rank}/{n}] {name} ping-pong", file=sys.stderr, flush=True)
+                o = (ctypes.c_double * 6)()
+                m.check(L.mscclppAmdMemChannelPingPong(comm.comm, 1024, PINGPONG_ITERS, ll8, o, 6), "ping-pong")
+                pp[name] = {"us_per_iter": round(o[0], 3), "correct": o[1] == 1.0,
+                            "error_record": [int(o[k]) for k in range(2, 6)]}
+            res["pingpong"] = pp
         comm.destroy()
         q.put((rank, res, None))
     except Exception as e:  # noqa: BLE001
@@ -93,6 +107,9 @@ def run(n=2, size=4096, timeout=180):
             "correct": all(g["correct"] for g in got.values()),
             "cores": 2 * n, "cores_note": "per rank: 1 busy-poll proxy thread + 1 launching thread",
             "proxy_numa_node": r0["proxy_numa_node"], "portchannel_alltoall_1MiB": r0["portchannel_alltoall_1MiB"],
+            "pingpong": r0.get("pingpong"),
+            "pingpong_correct": all(g.get("pingpong", {}).get(k, {}).get("correct", False)
+                                    for g in got.values() for k in ("ll16", "ll8")) if n == 2 else None,
             "path": "test/allgather_test_host_offloading.cu restated on libmscclpp_amd (FIFO + proxy + hipMemcpyAsync)"}
 
 
