@@ -259,7 +259,11 @@ int mscclppAmdPortChannelAllToAll(ncclComm_t comm, size_t chunk, int mode, int i
 /* The same with each iteration's own duration (a HIP event before every launch): with outLen >= 7,
  * out[3] = median, out[4] = min, out[5] = max us per iteration, out[6] = index of the slowest one;
  * with outLen >= 8, out[7] = the proxy thread's longest gap between FIFO polls in us over the timed
- * iterations (measured with MSCCLPP_AMD_PROXY_GAP_STATS=1, else 0). */
+ * iterations (measured with MSCCLPP_AMD_PROXY_GAP_STATS=1, else 0).  With outLen >= 16 the proxy
+ * stamps every timed trigger (ProxyService::enableStamps) and out[8..15] = medians over iterations,
+ * us: launch -> this rank's last data copy complete, launch -> its last token update complete, that
+ * token update -> kernel end (the wait for the peers' tokens), host submit time of a data copy, of a
+ * token update, of a whole trigger; the slowest iteration's launch -> token complete; stamps taken. */
 int mscclppAmdPortChannelAllToAllStats(ncclComm_t comm, size_t chunk, int mode, int iters, double* out, int outLen);
 /* mscclpp-test allreduce1 (test/mscclpp-test/allreduce_test.cu:730-839): int32 ring RS + AG whose data
  * moves through PortChannels and the host proxy (hipMemcpyAsync).  out[0] = us per AllReduce (graph of

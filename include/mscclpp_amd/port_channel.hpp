@@ -49,8 +49,28 @@ class ProxyService : public BaseProxyService {
   uint64_t proxyMaxPollGapNs() const;  // Proxy::maxPollGapNs of this service's proxy thread
   void resetProxyPollGap();
   uint64_t triggersHandled() const { return handled_; }
+  // Per-trigger stamps for latency analysis (off by default; the harnesses of DESIGN.md §9 turn them
+  // on).  For each of the next `cap` triggers the proxy thread records the host clock when it got
+  // the trigger and after it had submitted the data copy, the token update and the flush, plus HIP
+  // events on the connection stream after the data copy and after the token update (the device
+  // times at which they completed).  Read them after stopProxy(); the events stay owned by the
+  // service until the next enableStamps or its destruction.
+  struct TriggerStamp {
+    uint32_t type = 0;       // TriggerData | TriggerFlag | TriggerSync bits of the trigger
+    uint64_t seenNs = 0;     // steady clock when the handler started
+    uint64_t dataNs = 0;     // after the data copy was submitted (0: no data)
+    uint64_t flagNs = 0;     // after the token update was submitted (0: no flag)
+    uint64_t doneNs = 0;     // handler end (after the flush for a sync trigger)
+    void* dataEvent = nullptr;  // hipEvent_t recorded after the data copy (nullptr: none)
+    void* flagEvent = nullptr;  // hipEvent_t recorded after the token update
+  };
+  void enableStamps(size_t cap);
+  const std::vector<TriggerStamp>& stamps() const { return stamps_; }
 
  private:
+  std::vector<TriggerStamp> stamps_;
+  std::vector<void*> stampEvents_;  // hipEvent_t pool, 2 per stamp
+  size_t stampCap_ = 0;
   struct ConnState;
   std::vector<std::shared_ptr<Host2DeviceSemaphore>> semaphores_;
   std::vector<RegisteredMemory> memories_;

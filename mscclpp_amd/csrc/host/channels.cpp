@@ -177,7 +177,22 @@ ProxyService::ProxyService(int fifoSize) {
   proxy_ = std::make_shared<Proxy>([this](ProxyTrigger t, uint64_t pos) { return handleTrigger(t, pos); }, fifoSize);
 }
 
-ProxyService::~ProxyService() { stopProxy(); }
+ProxyService::~ProxyService() {
+  stopProxy();
+  for (void* e : stampEvents_) (void)hipEventDestroy((hipEvent_t)e);
+}
+
+void ProxyService::enableStamps(size_t cap) {
+  if (cap > (1u << 20)) throw Error("ProxyService::enableStamps: at most 2^20 stamps", ErrorCode::InvalidUsage);
+  stamps_.clear();
+  stamps_.reserve(cap);
+  while (stampEvents_.size() < 2 * cap) {
+    hipEvent_t e = nullptr;
+    gpuCheck(hipEventCreate(&e), "hipEventCreate");
+    stampEvents_.push_back((void*)e);
+  }
+  stampCap_ = cap;
+}
 
 SemaphoreId ProxyService::buildAndAddSemaphore(Communicator& communicator, const Connection& connection) {
   if (!err_) err_ = communicator.deviceErrorWord();
@@ -291,6 +306,12 @@ void reportProxyFailure(uint32_t* err, const std::string& what) {
 }
 }  // namespace
 
+static inline uint64_t steadyNs() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 ProxyHandlerResult ProxyService::handleTrigger(ProxyTrigger t, uint64_t pos) {
   ++handled_;
   const uint32_t id = (uint32_t)t.fields.semaphoreId;
@@ -300,18 +321,38 @@ ProxyHandlerResult ProxyService::handleTrigger(ProxyTrigger t, uint64_t pos) {
   }
   Host2DeviceSemaphore& sem = *semaphores_[id];
   Connection& conn = sem.connection();
+  TriggerStamp* st = nullptr;
+  if (stamps_.size() < stampCap_) {
+    stamps_.emplace_back();
+    st = &stamps_.back();
+    st->type = (uint32_t)t.fields.type;
+    st->seenNs = steadyNs();
+  }
   try {
     if (t.fields.type & TriggerData) {
       const uint32_t d = (uint32_t)t.fields.dstMemoryId, s = (uint32_t)t.fields.srcMemoryId;
       if (d >= memories_.size() || s >= memories_.size())
         throw Error("trigger names an unknown memory id", ErrorCode::InvalidUsage);
       conn.write(memories_[d], t.fields.dstOffset, memories_[s], t.fields.srcOffset, t.fields.size);
+      if (st) {
+        st->dataNs = steadyNs();
+        st->dataEvent = stampEvents_[2 * (stamps_.size() - 1)];
+        (void)hipEventRecord((hipEvent_t)st->dataEvent, conn.stream());
+      }
     }
-    if (t.fields.type & TriggerFlag) sem.signal();
+    if (t.fields.type & TriggerFlag) {
+      sem.signal();
+      if (st) {
+        st->flagNs = steadyNs();
+        st->flagEvent = stampEvents_[2 * (stamps_.size() - 1) + 1];
+        (void)hipEventRecord((hipEvent_t)st->flagEvent, conn.stream());
+      }
+    }
     if (t.fields.type & TriggerSync) {
       conn.flush();
       __atomic_store_n(semConn_[id]->flushDone, pos + 1, __ATOMIC_RELEASE);
     }
+    if (st) st->doneNs = steadyNs();
   } catch (const std::exception& e) {
     reportProxyFailure(err_, e.what());
     if (t.fields.type & TriggerSync) __atomic_store_n(semConn_[id]->flushDone, pos + 1, __ATOMIC_RELEASE);

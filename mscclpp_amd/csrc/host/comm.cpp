@@ -215,8 +215,7 @@ ncclResult_t ncclGetUniqueId(ncclUniqueId* uniqueId) {
 }
 
 ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank) {
-  const char* to = std::getenv("MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S");
-  return (ncclResult_t)host::commInitRank(comm, nranks, &commId, rank, to ? std::atoi(to) : 600);
+  return (ncclResult_t)host::commInitRank(comm, nranks, &commId, rank, 0);
 }
 
 }  // extern "C"
@@ -224,6 +223,10 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
 namespace mscclpp_amd {
 namespace host {
 int commInitRank(ncclComm_t* comm, int nranks, const void* commId, int rank, int timeoutSec) {
+  if (timeoutSec <= 0) {  // every caller without a timeout of its own: the environment's, else 600 s
+    const char* to = std::getenv("MSCCLPP_AMD_BOOTSTRAP_TIMEOUT_S");
+    timeoutSec = to && std::atoi(to) > 0 ? std::atoi(to) : 600;
+  }
   return guarded([&] {
     if (!comm || !commId) return (int)ncclInvalidArgument;
     if (nranks <= 0 || rank < 0 || rank >= nranks) return (int)ncclInvalidArgument;

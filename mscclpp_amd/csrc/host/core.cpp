@@ -432,12 +432,31 @@ void Connection::write(RegisteredMemory dst, uint64_t dstOffset, RegisteredMemor
   if (e != hipSuccess) throw Error(std::string("Connection::write: ") + hipGetErrorString(e), ErrorCode::SystemError);
 }
 
+// How a token update reaches the peer (MSCCLPP_AMD_TOKEN_WRITE): "memcpy" (default) = an 8-byte
+// hipMemcpyAsync H2D from a pinned slot, as the reference (connection.cc:159-177); "writevalue" =
+// hipStreamWriteValue64, a stream-ordered write the command processor performs itself (no copy
+// engine or blit kernel behind it).  A/B of the two: DESIGN.md §9.
+static int tokenWriteMode() {
+  static const int m = [] {
+    const char* e = std::getenv("MSCCLPP_AMD_TOKEN_WRITE");
+    return e && std::string(e) == "writevalue" ? 1 : 0;
+  }();
+  return m;
+}
+
 void Connection::updateAndSync(RegisteredMemory dst, uint64_t dstOffset, uint64_t* src, uint64_t newValue) {
   if (!pimpl_) throw Error("updateAndSync on an empty Connection", ErrorCode::InvalidUsage);
   if (dstOffset + sizeof(uint64_t) > dst.size())
     throw Error("Connection::updateAndSync out of the registered range", ErrorCode::InvalidUsage);
   if (src) *src = newValue;
   Impl& c = *pimpl_;
+  if (tokenWriteMode() == 1) {
+    const hipError_t e = hipStreamWriteValue64(c.stream, (char*)dst.data() + dstOffset, newValue, 0);
+    if (e != hipSuccess)
+      throw Error(std::string("Connection::updateAndSync (hipStreamWriteValue64): ") + hipGetErrorString(e),
+                  ErrorCode::SystemError);
+    return;
+  }
   ++c.nvals;
   if (c.nvals % Impl::kSlots == 0) c.drain(-1);
   uint64_t* slot = &c.slots[c.nvals % Impl::kSlots];

@@ -270,6 +270,7 @@ extern "C" int mscclppAmdPortChannelAllToAllStats(ncclComm_t comm, size_t chunk,
     int numa = -1;
     std::vector<double> per;  // us per iteration (HIP events)
     double maxGapUs = 0;      // longest proxy-thread gap between FIFO polls (MSCCLPP_AMD_PROXY_GAP_STATS=1)
+    double stampStats[8] = {-1, -1, -1, -1, -1, -1, -1, 0};  // outLen >= 16: the trigger-stamp breakdown
     {
       Communicator cx(comm);
       ProxyService proxy;
@@ -316,6 +317,8 @@ extern "C" int mscclppAmdPortChannelAllToAllStats(ncclComm_t comm, size_t chunk,
       for (auto& x : ev) HIPCHECK(hipEventCreate(&x));
       comm->boot->barrier();
       proxy.resetProxyPollGap();
+      const int trigPerIter = (int)ch.size() * (mode == 0 ? 2 : 1);
+      if (outLen >= 16) proxy.enableStamps((size_t)iters * trigPerIter);
       t0 = nowSec();
       for (int i = 0; i < iters; ++i) {
         HIPCHECK(hipEventRecord(ev[(size_t)i], st));
@@ -331,6 +334,55 @@ extern "C" int mscclppAmdPortChannelAllToAllStats(ncclComm_t comm, size_t chunk,
         float ms = 0;
         HIPCHECK(hipEventElapsedTime(&ms, ev[(size_t)i], ev[(size_t)i + 1]));
         per[(size_t)i] = ms * 1e3;
+      }
+      if (outLen >= 16) {
+        // where an iteration's time goes: device time from the iteration's launch
+        // event to this rank's last data copy / last token update completing on the copy stream,
+        // from that token update to the end of the kernel (the wait for the peers' tokens), and the
+        // proxy thread's host time to submit a data copy, a token update, and a whole trigger.
+        // Every rank's kernels have finished after this barrier, so every trigger of this rank has
+        // been handled (a peer's last wait needed its token); the proxy thread is joined before its
+        // stamps are read.
+        comm->boot->barrier();
+        proxy.stopProxy();
+        const auto& sts = proxy.stamps();
+        std::vector<double> toData, toToken, tokenToEnd, subData, subFlag, handler;
+        double slowStartToToken = 0;
+        const size_t slow = (size_t)(std::max_element(per.begin(), per.end()) - per.begin());
+        for (int i = 0; i < iters && (size_t)(i + 1) * trigPerIter <= sts.size(); ++i) {
+          float lastData = -1, lastTok = -1;
+          for (int k = 0; k < trigPerIter; ++k) {
+            const auto& x = sts[(size_t)i * trigPerIter + k];
+            float ms = 0;
+            if (x.dataEvent && hipEventElapsedTime(&ms, ev[(size_t)i], (hipEvent_t)x.dataEvent) == hipSuccess)
+              lastData = std::max(lastData, ms * 1e3f);
+            if (x.flagEvent && hipEventElapsedTime(&ms, ev[(size_t)i], (hipEvent_t)x.flagEvent) == hipSuccess)
+              lastTok = std::max(lastTok, ms * 1e3f);
+            if (x.dataNs) subData.push_back((x.dataNs - x.seenNs) * 1e-3);
+            if (x.flagNs) subFlag.push_back((x.flagNs - (x.dataNs ? x.dataNs : x.seenNs)) * 1e-3);
+            handler.push_back((x.doneNs - x.seenNs) * 1e-3);
+          }
+          if (lastData >= 0) toData.push_back(lastData);
+          if (lastTok >= 0) {
+            toToken.push_back(lastTok);
+            tokenToEnd.push_back(per[(size_t)i] - lastTok);
+            if ((size_t)i == slow) slowStartToToken = lastTok;
+          }
+        }
+        auto med = [](std::vector<double> v) {
+          if (v.empty()) return -1.0;
+          std::sort(v.begin(), v.end());
+          const size_t m = v.size();
+          return m % 2 ? v[m / 2] : 0.5 * (v[m / 2 - 1] + v[m / 2]);
+        };
+        stampStats[0] = med(toData);
+        stampStats[1] = med(toToken);
+        stampStats[2] = med(tokenToEnd);
+        stampStats[3] = med(subData);
+        stampStats[4] = med(subFlag);
+        stampStats[5] = med(handler);
+        stampStats[6] = slowStartToToken;
+        stampStats[7] = (double)sts.size();
       }
       for (auto& x : ev) (void)hipEventDestroy(x);
       comm->boot->barrier();
@@ -375,6 +427,8 @@ extern "C" int mscclppAmdPortChannelAllToAllStats(ncclComm_t comm, size_t chunk,
       out[6] = (double)(std::max_element(per.begin(), per.end()) - per.begin());
     }
     if (outLen >= 8) out[7] = maxGapUs;
+    if (outLen >= 16)
+      for (int k = 0; k < 8; ++k) out[8 + k] = stampStats[k];
     freeDevice(src);
     freeDevice(dst);
     return (int)ncclSuccess;

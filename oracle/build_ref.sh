@@ -18,12 +18,18 @@ if ! { [ "$OUT/libref.so" -nt "$HERE/ref_harness.hip" ] && [ "$OUT/libref.so" -n
     -I"$REF/include" "$HERE/ref_harness.hip" -o "$OUT/libref.so"
   echo "built $OUT/libref.so"
 fi
-# The reference's python benchmark kernels (python/mscclpp_benchmark/allreduce.cu), a code object
-# with TYPE=int, whose allreduce2 ref_harness.hip's refBench2* run as n ranks on one GPU.
+# The reference's python benchmark kernels (python/mscclpp_benchmark/allreduce.cu), one code object
+# per TYPE (int, float, __half), whose allreduce2 ref_harness.hip's refBench2* run as n ranks on one
+# GPU.  int pins geometry, packet images and flags; float and __half also pin the order and the
+# rounding of the sum (0 + peers ascending + own, unclipped, :257-264).
 BENCH_CU="$REF/python/mscclpp_benchmark/allreduce.cu"
-if [ -f "$BENCH_CU" ] && ! { [ "$OUT/bench_allreduce_int.hsaco" -nt "$BENCH_CU" ] && \
-    [ "$OUT/bench_allreduce_int.hsaco" -nt "$HERE/build_ref.sh" ]; }; then
-  /opt/rocm/bin/hipcc --genco --offload-arch=gfx950 -O3 -std=c++17 -D__HIP_PLATFORM_AMD__ -DTYPE=int \
-    -I"$REF/include" "$BENCH_CU" -o "$OUT/bench_allreduce_int.hsaco"
-  echo "built $OUT/bench_allreduce_int.hsaco"
-fi
+for spec in int:int float:float half:__half; do
+  name=${spec%%:*}
+  type=${spec#*:}
+  obj="$OUT/bench_allreduce_$name.hsaco"
+  if [ -f "$BENCH_CU" ] && ! { [ "$obj" -nt "$BENCH_CU" ] && [ "$obj" -nt "$HERE/build_ref.sh" ]; }; then
+    /opt/rocm/bin/hipcc --genco --offload-arch=gfx950 -O3 -std=c++17 -D__HIP_PLATFORM_AMD__ -DTYPE="$type" \
+      -I"$REF/include" "$BENCH_CU" -o "$obj"
+    echo "built $obj"
+  fi
+done

@@ -594,6 +594,59 @@ void oracle_mscclpp_test_ll(int n, const uint32_t* const* in, uint64_t nelems, u
   free(acc);
 }
 
+/* One 32-bit word of python/mscclpp_benchmark/allreduce.cu's add_vectors<TYPE>(a, b) (:37-96):
+ * TYPE=int wrapping add, TYPE=float `a + b` (RNE, no clip), TYPE=__half __hadd2 on the word's two
+ * halves (RNE, no clip: inf on overflow, a NaN operand propagates, quieted, with its payload). */
+static uint32_t bench_add_word(int dtype, uint32_t a, uint32_t b) {
+  if (dtype == ORC_F32) return f2u(u2f(a) + u2f(b));
+  if (dtype == ORC_F16) {
+    uint16_t lo = float_to_half_rne(half_to_float((uint16_t)a) + half_to_float((uint16_t)b));
+    uint16_t hi = float_to_half_rne(half_to_float((uint16_t)(a >> 16)) + half_to_float((uint16_t)(b >> 16)));
+    return (uint32_t)lo | ((uint32_t)hi << 16);
+  }
+  return a + b;
+}
+
+/* python/mscclpp_benchmark/allreduce.cu:223-289 allreduce2 for TYPE = int (ORC_I32), float (ORC_F32)
+ * or __half (ORC_F16), on one node; nwords = the rank's buffer in 32-bit words (the kernel's nelems
+ * after its `nelems / (sizeof(int) / sizeof(TYPE))`, :229).  Same packets and scratch layout as
+ * allreduce6 above (:239-248); per 32-bit word the reduction is, as the kernel orders its operands,
+ *   order 0:  data = 0;  data = val_p + data  for peers p ascending (:257-262);  data = data + own (:263)
+ * and, only to show that the test can tell orders apart,
+ *   order 1:  data = own;  data = data + val_p  for peers p ascending.
+ * A float/half 0 + (-0) is +0, so order 0 turns an all-(-0) word into +0 where order 1 keeps -0. */
+void oracle_bench_allreduce2(int dtype, int order, int n, const uint32_t* const* in, uint64_t nwords, uint32_t flag,
+                             uint32_t* const* scratch, uint32_t* const* out) {
+  uint64_t nPkts = nwords / 2, epr = nwords / (uint64_t)n, ppr = epr / 2;
+  uint64_t inBase = (flag & 1u) ? 0 : nPkts, resBase = (flag & 1u) ? 2 * nPkts : 3 * nPkts;
+  for (int s = 0; s < n; s++) /* step 1 */
+    for (int q = 0; q < n; q++)
+      if (q != s) oracle_ll16_pack(in[s] + (uint64_t)q * epr, ppr, flag, scratch[q] + (inBase + (uint64_t)s * ppr) * 4);
+  uint32_t* tmp = (uint32_t*)malloc(epr * 4 + 8);
+  uint32_t* acc = (uint32_t*)malloc(epr * 4 + 8);
+  for (int r = 0; r < n; r++) { /* step 2 */
+    const uint32_t* own = in[r] + (uint64_t)r * epr;
+    if (order == 0) memset(acc, 0, epr * 4);
+    else memcpy(acc, own, epr * 4);
+    for (int p = 0; p < n; p++) {
+      if (p == r) continue;
+      oracle_ll16_unpack(scratch[r] + (inBase + (uint64_t)p * ppr) * 4, ppr, flag, tmp);
+      for (uint64_t i = 0; i < epr; i++)
+        acc[i] = order == 0 ? bench_add_word(dtype, tmp[i], acc[i]) : bench_add_word(dtype, acc[i], tmp[i]);
+    }
+    if (order == 0)
+      for (uint64_t i = 0; i < epr; i++) acc[i] = bench_add_word(dtype, acc[i], own[i]);
+    memcpy(out[r] + (uint64_t)r * epr, acc, epr * 4);
+    for (int q = 0; q < n; q++)
+      if (q != r) oracle_ll16_pack(acc, ppr, flag, scratch[q] + (resBase + (uint64_t)r * ppr) * 4);
+  }
+  for (int r = 0; r < n; r++) /* step 3 */
+    for (int p = 0; p < n; p++)
+      if (p != r) oracle_ll16_unpack(scratch[r] + (resBase + (uint64_t)p * ppr) * 4, ppr, flag, out[r] + (uint64_t)p * epr);
+  free(tmp);
+  free(acc);
+}
+
 /* mscclpp-test allreduce2, single node (test/mscclpp-test/allreduce_test.cu:841-943, worldSize ==
  * nRanksPerNode), int32, nelems even.  One hop of LL16 packets (LLPacket = {x, flag, y, flag}):
  * rank s puts its whole buffer into every peer q's scratch at packet

@@ -224,6 +224,7 @@ int refB15Convert(const float* in, size_t n, uint8_t* enc, uint8_t* encX4, float
 // per rank, and the caller runs with GPU_MAX_HW_QUEUES > 8 so no two streams share a hardware queue.
 struct RefBench2 {
   int n = 0;
+  int elemBytes = 4;  // sizeof(TYPE) the code object was built with (int / float 4, __half 2)
   std::vector<hipModule_t> mod;
   std::vector<hipFunction_t> fn;
   std::vector<MemoryChannelDeviceHandle*> chans;  // device, n - 1 per rank
@@ -248,10 +249,13 @@ static bool rankStreams() {
 
 void refBench2Close(void* handle);
 
-void* refBench2Open(const char* hsaco, int n) {
-  if (n < 2 || n > 8 || !rankStreams()) return nullptr;
+// elemBytes: sizeof(TYPE) of the code object (4 for TYPE=int or float, 2 for __half); the kernel takes
+// its buffer length in TYPE elements and divides by sizeof(int) / sizeof(TYPE) itself (:229).
+void* refBench2OpenTyped(const char* hsaco, int n, int elemBytes) {
+  if (n < 2 || n > 8 || (elemBytes != 2 && elemBytes != 4) || !rankStreams()) return nullptr;
   auto* h = new RefBench2;
   h->n = n;
+  h->elemBytes = elemBytes;
   h->mod.resize(n);
   h->fn.resize(n);
   h->chans.resize(n);
@@ -281,6 +285,8 @@ void* refBench2Open(const char* hsaco, int n) {
   }
   return h;
 }
+
+void* refBench2Open(const char* hsaco, int n) { return refBench2OpenTyped(hsaco, n, 4); }
 
 // After a timeout: which ranks' launches finished (done[r]) and each rank's globalFlag (flags[r]),
 // read on the diagnostic stream while the others may still spin.  0 on success.
@@ -368,7 +374,7 @@ int refBench2Run(void* handle, void* const* bufs, void* const* scratch, void* co
     void* scr = scratch[r];
     void* res = results[r];
     int rank = r, world = n;
-    size_t ne = nelems;
+    size_t ne = nelems * 4 / (uint64_t)h->elemBytes;  // TYPE elements
     void* args[] = {&c, &buff, &scr, &res, &rank, &world, &ne};
     if (hipModuleLaunchKernel(h->fn[r], blocksPerPeer * nPeers, 1, 1, threads, 1, 1, 0, gRankStream[r], args,
                               nullptr) != hipSuccess)

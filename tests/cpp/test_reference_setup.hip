@@ -401,9 +401,11 @@ static int portWorker(int myRank, const std::string& ipPort) {
   MSCCLPP_CUDATHROW(hipSetDevice(0));
   int gpuId = 0;
   MSCCLPP_CUDATHROW(hipGetDevice(&gpuId));
-  const int remoteRank = myRank ^ 1, nRanks = 2, iter = 20;
+  // the tutorial's shape: 1000 graph-captured iterations of 1 KiB, 1 MiB and 128 MiB
+  // (bidir_port_channel.cu:70-75, :119-170)
+  const int remoteRank = myRank ^ 1, nRanks = 2, iter = 1000;
   const mscclpp::Transport transport = mscclpp::Transport::CudaIpc;
-  const size_t maxBytes = 16 << 20;
+  const size_t maxBytes = (size_t)128 << 20;
   auto bootstrap = std::make_shared<mscclpp::TcpBootstrap>(myRank, nRanks);
   bootstrap->initialize(ipPort);
   mscclpp::Communicator comm(bootstrap);
@@ -444,8 +446,25 @@ static int portWorker(int myRank, const std::string& ipPort) {
     MSCCLPP_CUDATHROW(hipDeviceSynchronize());
     proxyService.startProxy();
     bootstrap->barrier();
+    hipEvent_t start, end;
+    MSCCLPP_CUDATHROW(hipEventCreate(&start));
+    MSCCLPP_CUDATHROW(hipEventCreate(&end));
+    MSCCLPP_CUDATHROW(hipEventRecord(start, stream));
     MSCCLPP_CUDATHROW(hipGraphLaunch(graphExec, stream));
+    MSCCLPP_CUDATHROW(hipEventRecord(end, stream));
     MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+    if (myRank == 0) {  // the tutorial's line (bidir_port_channel.cu:155-161)
+      float ms = 0;
+      MSCCLPP_CUDATHROW(hipEventElapsedTime(&ms, start, end));
+      const float perIter = ms / iter;
+      std::printf("Rank %d: [Bidir PutWithSignal] bytes %zu, elapsed %g ms/iter, BW %g GB/s\n", myRank, copyBytes,
+                  perIter, (float)copyBytes / perIter * 1e-6f);
+      std::printf("PORT_JSON {\"bytes\": %zu, \"us_per_iter\": %.3f, \"GBs\": %.3f, \"iters\": %d}\n", copyBytes,
+                  perIter * 1e3, (float)copyBytes / perIter * 1e-6f, iter);
+      std::fflush(stdout);
+    }
+    MSCCLPP_CUDATHROW(hipEventDestroy(start));
+    MSCCLPP_CUDATHROW(hipEventDestroy(end));
     proxyService.stopProxy();
     bootstrap->barrier();
     std::vector<int> got(n);

@@ -67,6 +67,7 @@ def L():
             ("oracle_allreduce_allpairs", [i32, i32, i32, vp, u64, u32, u64, vp, vp], None),
             ("oracle_allreduce_sliced", [i32, i32, i32, vp, u64, u64, i32, vp], None),
             ("oracle_mscclpp_test_ll", [i32, vp, u64, u32, vp, vp], None),
+            ("oracle_bench_allreduce2", [i32, i32, i32, vp, u64, u32, vp, vp], None),
             ("oracle_mscclpp_test_k2", [i32, vp, u64, u32, vp, vp], None),
             ("oracle_allreduce_owned", [i32, i32, i32, vp, u64, u64, u64, i32, vp], None),
             ("oracle_trigger_encode", [u64, u32, u64, u32, u64, u64, u32, vp], None),
@@ -161,6 +162,18 @@ def mscclpp_test_ll(inputs, nelems, flag, scratch_bytes):
     scr = [np.zeros(scratch_bytes // 4, np.uint32) for _ in range(n)]
     outs = [np.zeros(nelems, np.uint32) for _ in range(n)]
     L().oracle_mscclpp_test_ll(n, _ptr_array(ins), nelems, flag, _ptr_array(scr), _ptr_array(outs))
+    return outs, scr
+
+
+def bench_allreduce2(dtype, inputs, nwords, flag, scratch_bytes, order=0):
+    """python/mscclpp_benchmark/allreduce.cu allreduce2 with TYPE = int (I32), float (F32) or __half
+    (F16): outputs and full scratch images.  order 0 is the kernel's (0 + peers ascending + own);
+    order 1 (own + peers ascending) exists only to show that a test tells the two apart."""
+    n = len(inputs)
+    ins = [np.ascontiguousarray(a).view(np.uint32) for a in inputs]
+    scr = [np.zeros(scratch_bytes // 4, np.uint32) for _ in range(n)]
+    outs = [np.zeros(nwords, np.uint32) for _ in range(n)]
+    L().oracle_bench_allreduce2(dtype, order, n, _ptr_array(ins), nwords, flag, _ptr_array(scr), _ptr_array(outs))
     return outs, scr
 
 

@@ -21,6 +21,9 @@ import oracle_lib as O  # noqa: E402
 
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref.so")
 HSACO = os.path.join(ROOT, "oracle", "_ref", "bench_allreduce_int.hsaco")
+# TYPE=float / __half code objects of the same kernel: (oracle dtype, sizeof(TYPE), file)
+TYPED = {"f32": (O.F32, 4, os.path.join(ROOT, "oracle", "_ref", "bench_allreduce_float.hsaco")),
+         "f16": (O.F16, 2, os.path.join(ROOT, "oracle", "_ref", "bench_allreduce_half.hsaco"))}
 
 
 def _lib():
@@ -28,6 +31,8 @@ def _lib():
     vp = ctypes.c_void_p
     L.refBench2Open.argtypes = [ctypes.c_char_p, ctypes.c_int]
     L.refBench2Open.restype = vp
+    L.refBench2OpenTyped.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    L.refBench2OpenTyped.restype = vp
     L.refBench2Close.argtypes = [vp]
     L.refBench2Diag.argtypes = [vp, vp, vp]
     L.refBench2Run.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -100,14 +105,124 @@ def run_case(L, m, n, count, blocks_per_peer, threads):
     return rec
 
 
+def typed_inputs(kind, n, nwords, seed):
+    """Per-rank buffers of `nwords` 32-bit words holding float32 or float16 elements: random values,
+    plus lanes chosen by element index (k = i % 64, owner = the rank whose chunk holds element i):
+      k == 1  -0 on every rank (0 + -0 = +0: the kernel's leading 0 shows),
+      k == 2  1.0 on the owner, half an ulp of 1.0 elsewhere (n >= 3: only peers-first keeps them),
+      k == 3  a large value of one sign on every rank (the unclipped sum overflows to inf),
+      k == 4  +max / -max alternating by rank (exact cancellation near the top of the range),
+      k == 5  a NaN (quiet or signalling, payload from i, either sign) on one rank, finite elsewhere,
+      k == 7  subnormals of either sign."""
+    rng = np.random.default_rng(seed)
+    ftype, utype = (np.float32, np.uint32) if kind == "f32" else (np.float16, np.uint16)
+    per_word = 1 if kind == "f32" else 2
+    ne = nwords * per_word
+    epr = ne // n
+    i = np.arange(ne)
+    k, owner = i % 64, i // epr
+    outs = []
+    for r in range(n):
+        if kind == "f32":
+            v = (rng.standard_normal(ne) * np.exp2(rng.integers(-20, 21, ne))).astype(np.float32)
+            half_ulp, big, top = np.float32(2.0 ** -24), np.float32(2.0e38), np.float32(3.4028234663852886e38)
+            sub = (rng.integers(1, 1 << 20, ne) * 2.0 ** -149).astype(np.float32)
+        else:
+            v = rng.uniform(-8, 8, ne).astype(np.float16)
+            half_ulp, big, top = np.float16(2.0 ** -11), np.float16(40000.0), np.float16(65504.0)
+            sub = (rng.integers(1, 1024, ne) * 2.0 ** -24).astype(np.float16)
+        v[k == 1] = -0.0
+        v[k == 2] = np.where(owner[k == 2] == r, ftype(1.0), half_ulp)
+        v[k == 3] = big
+        v[k == 4] = top if r % 2 == 0 else -top
+        v[k == 7] = np.where(rng.integers(0, 2, ne)[k == 7] == 1, sub[k == 7], -sub[k == 7])
+        u = v.view(utype)
+        nan_lane = (k == 5) & ((i // 64) % n == r)
+        if kind == "f32":
+            payload = (i.astype(np.uint64) * 2654435761 % (1 << 22)).astype(np.uint32) | 1
+            quiet = np.where(i % 3 == 0, 0, 1 << 22).astype(np.uint32)
+            sign = np.where((i // 128) % 2 == 1, 1 << 31, 0).astype(np.uint32)
+            u[nan_lane] = (sign | 0x7F800000 | quiet | payload)[nan_lane]
+        else:
+            payload = ((i * 40503) % (1 << 9)).astype(np.uint16) | 1
+            quiet = np.where(i % 3 == 0, 0, 1 << 9).astype(np.uint16)
+            sign = np.where((i // 128) % 2 == 1, 0x8000, 0).astype(np.uint16)
+            u[nan_lane] = (sign | 0x7C00 | quiet | payload)[nan_lane]
+        outs.append(np.ascontiguousarray(u).view(np.uint32))
+    return outs
+
+
+def run_typed_case(L, kind, n, nwords, blocks_per_peer, threads):
+    """The reference's allreduce2 built with TYPE=float / __half: outputs bit-equal to the oracle's
+    restatement in the kernel's order (0 + peers ascending + own, unclipped) for 3 calls, and the
+    whole scratch images after the first; the own-first order must differ somewhere (the check
+    discriminates order)."""
+    dtype, ebytes, hsaco = TYPED[kind]
+    sb = 32 * nwords  # 4 regions of nwords / 2 LL16 packets (allreduce.cu:244-248)
+    h = L.refBench2OpenTyped(hsaco.encode(), n, ebytes)
+    assert h, "refBench2OpenTyped failed"
+    dev = torch.device("cuda", 0)
+    rptr = [L.refMallocUncached(sb) for _ in range(n)]
+    assert all(rptr), "refMallocUncached failed"
+    import mscclpp_amd as m
+
+    rscr = [m.device_view(p, sb).view(torch.int32) for p in rptr]
+    rec = {"type": kind, "n": n, "words": nwords, "blocks_per_peer": blocks_per_peer, "threads": threads,
+           "nan_words": 0, "inf_words": 0, "order_sensitive_words": 0}
+    try:
+        for call, flag in enumerate((1, 2, 3)):
+            ins = typed_inputs(kind, n, nwords, 7000 * n + 10 * call + nwords % 991 + (1 if kind == "f16" else 0))
+            dins = [torch.from_numpy(a.view(np.int32).copy()).to(dev) for a in ins]
+            rout = [torch.zeros_like(d) for d in dins]
+            torch.cuda.synchronize()
+            rc = L.refBench2Run(h, _ptrs(dins), _ptrs(rscr), _ptrs(rout), nwords, blocks_per_peer, threads, 20000)
+            if rc == 2:
+                print(json.dumps({"timeout": rec, "call": call}), flush=True)
+                os._exit(3)
+            assert rc == 0, f"refBench2Run returned {rc}"
+            exp, scr = O.bench_allreduce2(dtype, ins, nwords, flag, sb, order=0)
+            alt, _ = O.bench_allreduce2(dtype, ins, nwords, flag, sb, order=1)
+            for r in range(n):
+                got = rout[r].cpu().numpy().view(np.uint32)
+                bad = np.nonzero(got != exp[r])[0]
+                if bad.size:
+                    rows = [{"word": int(w), "ref": hex(int(got[w])), "oracle": hex(int(exp[r][w])),
+                             "inputs": [hex(int(a[w])) for a in ins]} for w in bad[:8]]
+                    raise AssertionError(json.dumps({"case": rec, "call": call, "rank": r, "mismatched_words":
+                                                     int(bad.size), "first": rows}))
+                rec["order_sensitive_words"] += int(np.count_nonzero(alt[r] != exp[r]))
+                halves = got.view(np.uint16) if kind == "f16" else got
+                ab = halves & (0x7FFF if kind == "f16" else 0x7FFFFFFF)
+                top = 0x7C00 if kind == "f16" else 0x7F800000
+                rec["nan_words"] += int(np.count_nonzero(ab > top))
+                rec["inf_words"] += int(np.count_nonzero(ab == top))
+            if call == 0:
+                for r in range(n):
+                    img = rscr[r].cpu().numpy().view(np.uint32)
+                    assert np.array_equal(scr[r], img), f"oracle vs reference scratch image ({kind}), rank {r}"
+                rec["scratch_words_compared"] = int(n * sb // 4)
+        assert rec["order_sensitive_words"] > 0, "own-first order matched everywhere: the check cannot see order"
+        assert rec["nan_words"] > 0 and rec["inf_words"] > 0, rec
+        rec["calls"] = 3
+    finally:
+        torch.cuda.synchronize()
+        L.refBench2Close(h)
+        for p in rptr:
+            L.refFree(p)
+    return rec
+
+
 def main():
     cases = json.loads(sys.argv[1])
+    typed = json.loads(sys.argv[2]) if len(sys.argv) > 2 else []
     import mscclpp_amd as m
 
     torch.cuda.set_device(0)
     L = _lib()
     for n, count, bpp, threads in cases:
         print(json.dumps(run_case(L, m, n, count, bpp, threads)), flush=True)
+    for kind, n, nwords, bpp, threads in typed:
+        print(json.dumps(run_typed_case(L, kind, n, nwords, bpp, threads)), flush=True)
     print("WORKER OK", flush=True)
 
 

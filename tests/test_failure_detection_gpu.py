@@ -58,6 +58,9 @@ def test_absent_peer_ends_in_error_word(built, algo_name, count, code):
     assert err[0] == code, err
     if code == ERR_SEMAPHORE_TIMEOUT:  # detail: channel | peer << 16, rank, tokens seen | wanted << 16
         assert err[1] >> 16 == 1 and err[2] == 0 and (err[3] >> 16) >= 1, err
+    else:  # detail: the flag waited for (the first call's), the packet's byte offset, the flag seen there
+        # (0: the absent peer never wrote the zeroed slot)
+        assert err[1] >= 1 and err[2] < ranks.scratch_bytes and err[3] == 0, err
     assert ranks.errors()[1] == 0  # the absent rank reported nothing
     assert took < 60, took
 

@@ -120,3 +120,44 @@ def test_fifo_commit_parity():
     L = O.L()
     for pos in range(0, 4 * 512, 37):
         assert L.oracle_fifo_commit_bit(pos, 9) == ((pos >> 9) & 1) ^ 1
+
+
+def test_bench_allreduce2_typed_restatement():
+    """oracle_bench_allreduce2 (python/mscclpp_benchmark/allreduce.cu:223-289 for TYPE = int, float,
+    __half): for int it is allreduce6's restatement word for word (same packets, same scratch image);
+    for float / half its sum is 0 + peers ascending + own, unclipped -- an all-(-0) lane comes out +0
+    where the own-first order keeps -0, half-ulp peers survive only when added before the owner's
+    1.0 (n >= 3), and +-40000 halves overflow to inf instead of clipping to 65504."""
+    n, nwords, flag = 4, 64, 3
+    sb = 32 * nwords
+    rng = np.random.default_rng(11)
+    ins = [rng.integers(0, 2 ** 32, nwords, dtype=np.uint64).astype(np.uint32) for _ in range(n)]
+    a, sa = O.bench_allreduce2(O.I32, ins, nwords, flag, sb)
+    b, sbimg = O.mscclpp_test_ll(ins, nwords, flag, sb)
+    for r in range(n):
+        assert np.array_equal(a[r], b[r]) and np.array_equal(sa[r], sbimg[r])
+    # float16: word w holds halves 2w, 2w+1; owner of word w = w // (nwords / n)
+    epr = nwords // n
+    h = [np.zeros(2 * nwords, np.float16) for _ in range(n)]
+    for r in range(n):
+        h[r][0::2] = -0.0  # low half of every word: -0 everywhere
+        h[r][1::2] = np.float16(2.0 ** -11)  # high half: half an ulp of 1.0 ...
+        for w in range(nwords):
+            if w // epr == r:
+                h[r][2 * w + 1] = np.float16(1.0)  # ... and 1.0 on the owner
+    hw = [x.view(np.uint32) for x in h]
+    o0, _ = O.bench_allreduce2(O.F16, hw, nwords, 1, sb, order=0)
+    o1, _ = O.bench_allreduce2(O.F16, hw, nwords, 1, sb, order=1)
+    for r in range(n):
+        lo0, hi0 = o0[r].view(np.uint16)[0::2], o0[r].view(np.float16)[1::2]
+        lo1, hi1 = o1[r].view(np.uint16)[0::2], o1[r].view(np.float16)[1::2]
+        assert np.all(lo0 == 0x0000) and np.all(lo1 == 0x8000)  # +0 vs -0
+        # 3 peers: 3 * 2^-11 exactly, then + 1.0 = 1 + 1.5 ulp, a tie that rounds to even: 1 + 2^-9
+        assert np.all(hi0 == np.float16(1.0 + 2.0 ** -9))
+        assert np.all(hi1 == np.float16(1.0))
+    big = [np.full(2 * nwords, 40000.0, np.float16).view(np.uint32) for _ in range(2)]
+    o, _ = O.bench_allreduce2(O.F16, big, nwords, 1, sb)
+    assert np.all(o[0].view(np.uint16) == 0x7C00)  # inf, not clipped to 65504
+    f = [np.full(nwords, -0.0, np.float32).view(np.uint32) for _ in range(2)]
+    o, _ = O.bench_allreduce2(O.F32, f, nwords, 1, sb)
+    assert np.all(o[0] == 0) and np.all(o[1] == 0)

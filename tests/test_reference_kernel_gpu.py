@@ -31,6 +31,14 @@ CASES = [(2, 4096, 2, 1024), (3, 1536, 4, 256), (4, 8192, 2, 512), (8, 6144, 1, 
          (8, 16, 1, 64), (5, 10000, 2, 512), (6, 12288, 1, 1024), (7, 28672, 3, 256), (2, 1 << 20, 8, 1024)]
 
 
+# TYPE=float / __half builds of the same kernel: (type, ranks, 32-bit words per rank, blocks per peer,
+# threads); words % (2 n) == 0
+TYPED_CASES = [("f16", 2, 4096, 2, 1024), ("f16", 3, 6144, 2, 512), ("f16", 8, 16384, 2, 1024),
+               ("f16", 5, 10240, 1, 256), ("f32", 2, 4096, 2, 1024), ("f32", 4, 8192, 1, 512),
+               ("f32", 8, 16384, 3, 1024), ("f32", 7, 14336, 2, 256)]
+TYPED_HSACO = [os.path.join(ROOT, "oracle", "_ref", f"bench_allreduce_{t}.hsaco") for t in ("float", "half")]
+
+
 def test_reference_allreduce2_matches_k6_and_oracle(built):
     if not (os.path.exists(HSACO) and os.path.exists(REF_SO)):
         pytest.skip("oracle/_ref not built (needs /root/reference at build time)")
@@ -41,3 +49,27 @@ def test_reference_allreduce2_matches_k6_and_oracle(built):
     recs = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
     assert [(x["n"], x["count"]) for x in recs] == [(c[0], c[1]) for c in CASES]
     assert all(x["calls"] == 3 and x["scratch_words_compared"] == x["n"] * 8 * x["count"] for x in recs)
+
+
+def test_reference_allreduce2_fp16_fp32_order_and_rounding(built):
+    """the same reference kernel built with TYPE=__half and TYPE=float sums in its
+    own order -- 0, then the peers ascending (`data = val + data`), then the own chunk, with the
+    unclipped __hadd2 / float add (allreduce.cu:44-46, :257-264).  Its outputs equal the oracle's
+    restatement in that order bit for bit (n = 2 ... 8, three calls), including -0 lanes (0 + -0 =
+    +0), half-ulp lanes that only a peers-first order keeps, overflow to inf, cancellation at +-max,
+    subnormals and NaN lanes (quiet and signalling, payloads, both signs); the whole scratch images
+    match after the first call; and the own-first order differs on some words of every case, so the
+    check discriminates order."""
+    if not (all(os.path.exists(p) for p in TYPED_HSACO) and os.path.exists(REF_SO)):
+        pytest.skip("oracle/_ref typed code objects not built (needs /root/reference at build time)")
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "ref_kernel_worker.py"), "[]",
+                        json.dumps(TYPED_CASES)],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=150, env=env, cwd=ROOT)
+    assert r.returncode == 0 and "WORKER OK" in r.stdout, r.stdout[-6000:]
+    recs = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert [(x["type"], x["n"], x["words"]) for x in recs] == [c[:3] for c in TYPED_CASES]
+    for x in recs:
+        assert x["calls"] == 3 and x["scratch_words_compared"] == x["n"] * 8 * x["words"], x
+        assert x["order_sensitive_words"] > 0 and x["nan_words"] > 0 and x["inf_words"] > 0, x
+    print(json.dumps(recs))

@@ -4,6 +4,7 @@ DeviceSyncer, on this library -- a PortChannel loopback on one rank (test/unit/l
 the memory-channel tutorial's put / get / packet round between two processes meeting at "ip:port"
 (examples/tutorials/03-memory-channel), a UniqueId made in the parent, and the Context / Endpoint /
 SemaphoreStub ping-pong of examples/tutorials/01-basic-concepts in one process."""
+import json
 import os
 import socket
 import subprocess
@@ -40,8 +41,15 @@ def test_memory_channel_tutorial_ip_port(built):
 
 
 def test_port_channel_tutorial_graph_replays(built):
+    """examples/tutorials/04-port-channel as written: 1000 graph-captured bidirectional putWithSignal
+    iterations at 1 KiB, 1 MiB and 128 MiB, exact, with the tutorial's own `elapsed ms/iter, BW` line
+    (docs/tutorials/04-port-channel.md:25 publishes 25.0 us/iter, 41.9 GB/s at 1 MiB)."""
     out = _run(["port", str(_free_port())])
     assert "rank 0 port OK" in out and "rank 1 port OK" in out, out
+    rows = [json.loads(x.split(" ", 1)[1]) for x in out.splitlines() if x.startswith("PORT_JSON ")]
+    assert [r["bytes"] for r in rows] == [1024, 1 << 20, 128 << 20], out
+    assert all(r["us_per_iter"] > 0 for r in rows), rows
+    print([x for x in out.splitlines() if "[Bidir PutWithSignal]" in x])
 
 
 def test_unique_id_from_parent(built):
