@@ -192,6 +192,9 @@ int runRank(int rank, int n, ncclUniqueId id, size_t count, const std::string& m
   auto resetOutput = [&] {
     REQUIRE(hipMemset(recv, 0xFF, bytes * n) == hipSuccess);
     REQUIRE(hipMemcpy(recv + rank * count, send, bytes, hipMemcpyDeviceToDevice) == hipSuccess);
+    // both fills have landed before the barrier that lets the peers write into `recv` (DESIGN.md §8:
+    // a host barrier orders host calls, not device work still queued)
+    REQUIRE(hipDeviceSynchronize() == hipSuccess);
   };
   resetOutput();
   hipStream_t stream;
