@@ -647,6 +647,29 @@ void oracle_bench_allreduce2(int dtype, int order, int n, const uint32_t* const*
   free(acc);
 }
 
+/* python/mscclpp_benchmark/allreduce.cu:123-221 allreduce1 (TYPE = int, float or __half), in place,
+ * for a chunk of nwords / n words per rank that is a whole number of int4 vectors (the kernel's
+ * remainder path is then empty, :166-185).  The owner r of chunk r reduces it as the kernel orders
+ * its operands (:147-156): tmp = own; for index = 0 .. n - 2: p = (index + r) mod (n - 1), the
+ * channel to rank p < r ? p : p + 1, tmp = tmp + that rank's chunk; every rank's buffer ends holding
+ * tmp in chunk r (written to the peers, :158-164, and to the own buffer, :165). */
+void oracle_bench_allreduce1(int dtype, int n, const uint32_t* const* in, uint64_t nwords, uint32_t* const* out) {
+  const uint64_t cw = nwords / (uint64_t)n;
+  const int nPeer = n - 1;
+  for (int r = 0; r < n; r++) {
+    for (uint64_t i = r * cw; i < (uint64_t)(r + 1) * cw; i++) {
+      uint32_t tmp = in[r][i];
+      for (int index = 0; index < nPeer; index++) {
+        int peerIdx = index + r;
+        if (peerIdx >= nPeer) peerIdx -= nPeer;
+        const int remote = peerIdx < r ? peerIdx : peerIdx + 1;
+        tmp = bench_add_word(dtype, tmp, in[remote][i]);
+      }
+      for (int q = 0; q < n; q++) out[q][i] = tmp;
+    }
+  }
+}
+
 /* mscclpp-test allreduce2, single node (test/mscclpp-test/allreduce_test.cu:841-943, worldSize ==
  * nRanksPerNode), int32, nelems even.  One hop of LL16 packets (LLPacket = {x, flag, y, flag}):
  * rank s puts its whole buffer into every peer q's scratch at packet

@@ -227,6 +227,7 @@ struct RefBench2 {
   int elemBytes = 4;  // sizeof(TYPE) the code object was built with (int / float 4, __half 2)
   std::vector<hipModule_t> mod;
   std::vector<hipFunction_t> fn;
+  std::vector<hipFunction_t> fn1;                 // allreduce1 of the same code object
   std::vector<MemoryChannelDeviceHandle*> chans;  // device, n - 1 per rank
 };
 
@@ -258,10 +259,12 @@ void* refBench2OpenTyped(const char* hsaco, int n, int elemBytes) {
   h->elemBytes = elemBytes;
   h->mod.resize(n);
   h->fn.resize(n);
+  h->fn1.resize(n);
   h->chans.resize(n);
   for (int r = 0; r < n; ++r) {
     if (hipModuleLoad(&h->mod[r], hsaco) != hipSuccess ||
         hipModuleGetFunction(&h->fn[r], h->mod[r], "allreduce2") != hipSuccess ||
+        hipModuleGetFunction(&h->fn1[r], h->mod[r], "allreduce1") != hipSuccess ||
         hipMalloc(&h->chans[r], sizeof(MemoryChannelDeviceHandle) * (n - 1)) != hipSuccess) {
       refBench2Close(h);
       return nullptr;
@@ -378,6 +381,60 @@ int refBench2Run(void* handle, void* const* bufs, void* const* scratch, void* co
     void* args[] = {&c, &buff, &scr, &res, &rank, &world, &ne};
     if (hipModuleLaunchKernel(h->fn[r], blocksPerPeer * nPeers, 1, 1, threads, 1, 1, 0, gRankStream[r], args,
                               nullptr) != hipSuccess)
+      return 1;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int r = 0; r < n;) {
+    const hipError_t e = hipStreamQuery(gRankStream[r]);
+    if (e == hipSuccess) {
+      ++r;
+      continue;
+    }
+    if (e != hipErrorNotReady) return 1;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) return 2;
+  }
+  return 0;
+}
+
+// One in-place allreduce1 call (python/mscclpp_benchmark/allreduce.cu:123-221: signal / wait every
+// peer, grid barrier, read-reduce the own chunk from every peer's buffer -- own first, then channel
+// (index + rank) mod (n - 1) -- and, read_only == 0, write it back into every peer's buffer; grid
+// barrier, signal / wait again; read_only == 1 then gets the peers' chunks instead).  bufs: n device
+// buffers of nelems 32-bit words each, uncached (the ranks read and write each other's); tokens /
+// expected: n device arrays of n - 1 uint64 each, zeroed before the first call and kept across calls
+// (the semaphores are monotonic).  Channel p of rank r reaches rank p < r ? p : p + 1 (as :200).
+// Returns as refBench2Run.
+int refBench1Run(void* handle, void* const* bufs, void* const* tokens, void* const* expected, uint64_t nelems,
+                 int nblocks, int threads, int readOnly, int timeoutMs) {
+  auto* h = static_cast<RefBench2*>(handle);
+  if (!h) return 1;
+  const int n = h->n, nPeers = n - 1;
+  if (nelems == 0 || nelems > (1ull << 30) || nblocks < 1 || nblocks > 16 || threads < 64 || threads > 1024 ||
+      threads % 64 != 0 || (uint64_t)nblocks * threads < 2 * (uint64_t)nPeers)
+    return 4;
+  for (int r = 0; r < n; ++r) {
+    std::vector<MemoryChannelDeviceHandle> hc(nPeers);
+    for (int p = 0; p < nPeers; ++p) {
+      const int remote = p < r ? p : p + 1;
+      std::memset(static_cast<void*>(&hc[p]), 0, sizeof(hc[p]));
+      hc[p].semaphore_.inboundToken = static_cast<uint64_t*>(tokens[r]) + p;
+      hc[p].semaphore_.remoteInboundToken = static_cast<uint64_t*>(tokens[remote]) + (r < remote ? r : r - 1);
+      hc[p].semaphore_.expectedInboundToken = static_cast<uint64_t*>(expected[r]) + p;
+      hc[p].dst_ = bufs[remote];
+      hc[p].src_ = bufs[r];
+      hc[p].packetBuffer_ = nullptr;
+    }
+    if (hipMemcpy(h->chans[r], hc.data(), sizeof(hc[0]) * nPeers, hipMemcpyHostToDevice) != hipSuccess) return 1;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  for (int r = 0; r < n; ++r) {
+    MemoryChannelDeviceHandle* c = h->chans[r];
+    void* buff = bufs[r];
+    int rank = r, world = n, ro = readOnly;
+    size_t ne = nelems * 4 / (uint64_t)h->elemBytes;  // TYPE elements
+    void* args[] = {&c, &buff, &rank, &world, &ne, &ro};
+    if (hipModuleLaunchKernel(h->fn1[r], nblocks, 1, 1, threads, 1, 1, 0, gRankStream[r], args, nullptr) !=
+        hipSuccess)
       return 1;
   }
   const auto t0 = std::chrono::steady_clock::now();

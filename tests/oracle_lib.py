@@ -68,6 +68,7 @@ def L():
             ("oracle_allreduce_sliced", [i32, i32, i32, vp, u64, u64, i32, vp], None),
             ("oracle_mscclpp_test_ll", [i32, vp, u64, u32, vp, vp], None),
             ("oracle_bench_allreduce2", [i32, i32, i32, vp, u64, u32, vp, vp], None),
+            ("oracle_bench_allreduce1", [i32, i32, vp, u64, vp], None),
             ("oracle_mscclpp_test_k2", [i32, vp, u64, u32, vp, vp], None),
             ("oracle_allreduce_owned", [i32, i32, i32, vp, u64, u64, u64, i32, vp], None),
             ("oracle_trigger_encode", [u64, u32, u64, u32, u64, u64, u32, vp], None),
@@ -175,6 +176,16 @@ def bench_allreduce2(dtype, inputs, nwords, flag, scratch_bytes, order=0):
     outs = [np.zeros(nwords, np.uint32) for _ in range(n)]
     L().oracle_bench_allreduce2(dtype, order, n, _ptr_array(ins), nwords, flag, _ptr_array(scr), _ptr_array(outs))
     return outs, scr
+
+
+def bench_allreduce1(dtype, inputs, nwords):
+    """python/mscclpp_benchmark/allreduce.cu allreduce1 (in place, own chunk first then the peers in
+    the kernel's rotated channel order): every rank's resulting buffer."""
+    n = len(inputs)
+    ins = [np.ascontiguousarray(a).view(np.uint32) for a in inputs]
+    outs = [np.zeros(nwords, np.uint32) for _ in range(n)]
+    L().oracle_bench_allreduce1(dtype, n, _ptr_array(ins), nwords, _ptr_array(outs))
+    return outs
 
 
 def mscclpp_test_k2(inputs, nelems, flag, scratch_bytes):

@@ -37,6 +37,9 @@ def _lib():
     L.refBench2Diag.argtypes = [vp, vp, vp]
     L.refBench2Run.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     L.refBench2Run.restype = ctypes.c_int
+    L.refBench1Run.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_int]
+    L.refBench1Run.restype = ctypes.c_int
     L.refMallocUncached.argtypes = [ctypes.c_uint64]
     L.refMallocUncached.restype = vp
     L.refFree.argtypes = [vp]
@@ -212,9 +215,71 @@ def run_typed_case(L, kind, n, nwords, blocks_per_peer, threads):
     return rec
 
 
+def run_bench1_case(L, kind, n, nwords, nblocks, threads, read_only):
+    """The reference's allreduce1 (TYPE = int, float or __half; in place, semaphores + grid barrier,
+    own chunk first then the peers in rotated channel order): every rank's buffer bit-equal to the
+    oracle's restatement after each of 3 calls on fresh inputs; for float / half, the order of
+    allreduce2 (0 + peers ascending + own) differs somewhere, so the check sees order."""
+    import mscclpp_amd as m
+
+    if kind == "i32":
+        dtype, ebytes, hsaco = O.I32, 4, HSACO
+    else:
+        dtype, ebytes, hsaco = TYPED[kind]
+    h = L.refBench2OpenTyped(hsaco.encode(), n, ebytes)
+    assert h, "refBench2OpenTyped failed"
+    nb = nwords * 4
+    bufs = [L.refMallocUncached(nb) for _ in range(n)]
+    toks = [L.refMallocUncached(8 * (n - 1)) for _ in range(n)]
+    exps = [L.refMallocUncached(8 * (n - 1)) for _ in range(n)]
+    assert all(bufs) and all(toks) and all(exps), "refMallocUncached failed"
+    views = [m.device_view(p, nb).view(torch.int32) for p in bufs]
+    rec = {"kernel": "allreduce1", "type": kind, "n": n, "words": nwords, "nblocks": nblocks, "threads": threads,
+           "read_only": read_only, "order_sensitive_words": 0}
+    arr = lambda ps: (ctypes.c_void_p * n)(*ps)  # noqa: E731
+    try:
+        for call in range(3):
+            seed = 9000 * n + 10 * call + nwords % 983 + read_only
+            if kind == "i32":
+                rng = np.random.default_rng(seed)
+                ins = [rng.integers(-2 ** 31, 2 ** 31, nwords, dtype=np.int64).astype(np.int32).view(np.uint32)
+                       for _ in range(n)]
+            else:
+                ins = typed_inputs(kind, n, nwords, seed)
+            for v, a in zip(views, ins):
+                v.copy_(torch.from_numpy(a.view(np.int32).copy()))
+            torch.cuda.synchronize()
+            rc = L.refBench1Run(h, arr(bufs), arr(toks), arr(exps), nwords, nblocks, threads, read_only, 20000)
+            if rc == 2:
+                print(json.dumps({"timeout": rec, "call": call}), flush=True)
+                os._exit(3)
+            assert rc == 0, f"refBench1Run returned {rc}"
+            exp = O.bench_allreduce1(dtype, ins, nwords)
+            alt, _ = O.bench_allreduce2(dtype, ins, nwords, 1, 32 * nwords, order=0)
+            for r in range(n):
+                got = views[r].cpu().numpy().view(np.uint32)
+                bad = np.nonzero(got != exp[r])[0]
+                if bad.size:
+                    rows = [{"word": int(w), "ref": hex(int(got[w])), "oracle": hex(int(exp[r][w])),
+                             "inputs": [hex(int(a[w])) for a in ins]} for w in bad[:8]]
+                    raise AssertionError(json.dumps({"case": rec, "call": call, "rank": r, "mismatched_words":
+                                                     int(bad.size), "first": rows}))
+                rec["order_sensitive_words"] += int(np.count_nonzero(alt[r] != exp[r]))
+        if kind != "i32":
+            assert rec["order_sensitive_words"] > 0, "allreduce2's order matched everywhere: the check cannot see order"
+        rec["calls"] = 3
+    finally:
+        torch.cuda.synchronize()
+        L.refBench2Close(h)
+        for p in bufs + toks + exps:
+            L.refFree(p)
+    return rec
+
+
 def main():
     cases = json.loads(sys.argv[1])
     typed = json.loads(sys.argv[2]) if len(sys.argv) > 2 else []
+    bench1 = json.loads(sys.argv[3]) if len(sys.argv) > 3 else []
     import mscclpp_amd as m
 
     torch.cuda.set_device(0)
@@ -223,6 +288,8 @@ def main():
         print(json.dumps(run_case(L, m, n, count, bpp, threads)), flush=True)
     for kind, n, nwords, bpp, threads in typed:
         print(json.dumps(run_typed_case(L, kind, n, nwords, bpp, threads)), flush=True)
+    for kind, n, nwords, nblocks, threads, read_only in bench1:
+        print(json.dumps(run_bench1_case(L, kind, n, nwords, nblocks, threads, read_only)), flush=True)
     print("WORKER OK", flush=True)
 
 

@@ -161,3 +161,26 @@ def test_bench_allreduce2_typed_restatement():
     f = [np.full(nwords, -0.0, np.float32).view(np.uint32) for _ in range(2)]
     o, _ = O.bench_allreduce2(O.F32, f, nwords, 1, sb)
     assert np.all(o[0] == 0) and np.all(o[1] == 0)
+
+
+def test_bench_allreduce1_restatement():
+    """oracle_bench_allreduce1 (allreduce.cu:123-221): int32 gives the wrapping sum on every rank; for
+    half the owner's value comes first -- an all-(-0) lane stays -0 (allreduce2's leading 0 makes it
+    +0) -- and the peers follow in rotated channel order (rank r starts at channel r mod (n - 1))."""
+    n, nwords = 4, 64
+    rng = np.random.default_rng(5)
+    ins = [rng.integers(0, 2 ** 32, nwords, dtype=np.uint64).astype(np.uint32) for _ in range(n)]
+    out = O.bench_allreduce1(O.I32, ins, nwords)
+    want = (np.sum(np.stack([a.astype(np.uint64) for a in ins]), axis=0) % (1 << 32)).astype(np.uint32)
+    assert all(np.array_equal(o, want) for o in out)
+    h = [np.full(2 * nwords, -0.0, np.float16).view(np.uint32) for _ in range(n)]
+    assert all(np.all(o == 0x80008000) for o in O.bench_allreduce1(O.F16, h, nwords))
+    # rotation: owner 1 of 3 ranks adds rank 2 before rank 0 (channel 1 then channel 0)
+    n, cw = 3, 4
+    vals = {0: 2.0 ** -11, 1: 1.0, 2: 2.0 ** -11}  # owner 1.0, the two peers half an ulp each
+    f = [np.zeros(2 * n * cw, np.float16) for _ in range(n)]
+    for q in range(n):
+        f[q][:] = vals[q]
+    out = O.bench_allreduce1(O.F16, [x.view(np.uint32) for x in f], n * cw)
+    # owner-first: 1 + 2^-11 ties to 1 twice, whichever peer comes first
+    assert np.all(out[0].view(np.float16)[2 * cw:4 * cw] == np.float16(1.0))

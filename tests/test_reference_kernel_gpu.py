@@ -73,3 +73,31 @@ def test_reference_allreduce2_fp16_fp32_order_and_rounding(built):
         assert x["calls"] == 3 and x["scratch_words_compared"] == x["n"] * 8 * x["words"], x
         assert x["order_sensitive_words"] > 0 and x["nan_words"] > 0 and x["inf_words"] > 0, x
     print(json.dumps(recs))
+
+
+# allreduce1: (type, ranks, 32-bit words per rank, blocks, threads, read_only); the chunk (words / n)
+# is a whole number of int4 vectors (4 words), so the kernel's remainder path is empty
+BENCH1_CASES = [("i32", 2, 4096, 2, 1024, 0), ("i32", 5, 10240, 3, 512, 1), ("f16", 2, 4096, 2, 1024, 0),
+                ("f16", 3, 6144, 4, 256, 0), ("f16", 8, 16384, 2, 1024, 1), ("f32", 4, 8192, 2, 512, 0),
+                ("f32", 7, 14336, 1, 1024, 1), ("f32", 8, 32768, 4, 1024, 0)]
+
+
+def test_reference_allreduce1_order_and_rounding(built):
+    """VERDICT r5 item 2, second kernel: the reference's all-pairs read-reduce allreduce1
+    (allreduce.cu:123-221; memory channels with device-to-device semaphores and a grid barrier, in
+    place, write-back and read-only variants), built with TYPE=int, float and __half, run as n ranks:
+    every rank's buffer equals the oracle's restatement -- own chunk first, then the peers in the
+    kernel's rotated channel order (:147-156), unclipped -- bit for bit after each of 3 calls, with the
+    same -0 / overflow / NaN / subnormal lanes; for float / half allreduce2's order differs somewhere."""
+    if not (all(os.path.exists(p) for p in TYPED_HSACO + [HSACO]) and os.path.exists(REF_SO)):
+        pytest.skip("oracle/_ref code objects not built (needs /root/reference at build time)")
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "ref_kernel_worker.py"), "[]", "[]",
+                        json.dumps(BENCH1_CASES)],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=150, env=env, cwd=ROOT)
+    assert r.returncode == 0 and "WORKER OK" in r.stdout, r.stdout[-6000:]
+    recs = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+    assert [(x["type"], x["n"], x["words"], x["read_only"]) for x in recs] == \
+        [(c[0], c[1], c[2], c[5]) for c in BENCH1_CASES]
+    assert all(x["calls"] == 3 for x in recs)
+    print(json.dumps(recs))
