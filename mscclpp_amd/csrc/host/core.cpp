@@ -380,6 +380,21 @@ RegisteredMemory RegisteredMemory::deserialize(const std::vector<char>& data) {
 // process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues, and a connection stream that lands
 // on the queue of a kernel spinning for that connection's data never runs -- the PortChannel
 // all-to-all hung with 4 ranks on one GPU.
+// The connections' copy stream.  MSCCLPP_AMD_COPY_STREAM_PRIORITY=high creates it at the device's
+// greatest stream priority (an A/B of DESIGN.md §9: whether the hardware scheduler then picks the
+// proxy's copies up sooner while other processes' kernels hold the GPU); default: normal priority.
+static hipError_t createCopyStream(hipStream_t* s) {
+  static const bool high = [] {
+    const char* e = std::getenv("MSCCLPP_AMD_COPY_STREAM_PRIORITY");
+    return e && std::string(e) == "high";
+  }();
+  if (!high) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  const hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}
+
 struct SharedCopyStream {
   hipStream_t stream = nullptr;
   ~SharedCopyStream() {
@@ -726,7 +741,7 @@ std::shared_future<Connection> Communicator::connect(const EndpointConfig& local
       int cur = 0;
       gpuCheck(hipGetDevice(&cur), "hipGetDevice");
       gpuCheck(hipSetDevice(device), "hipSetDevice");
-      const hipError_t e = hipStreamCreateWithFlags(&copy->stream, hipStreamNonBlocking);
+      const hipError_t e = createCopyStream(&copy->stream);
       gpuCheck(hipSetDevice(cur), "hipSetDevice");
       gpuCheck(e, "hipStreamCreateWithFlags");
       comm_->ipcStream = copy;
@@ -996,7 +1011,7 @@ Connection Context::connect(const Endpoint& localEndpoint, const Endpoint& remot
       auto& slot = pimpl_->copy[dev];
       if (!slot) {
         slot = std::make_shared<SharedCopyStream>();
-        gpuCheck(hipStreamCreateWithFlags(&slot->stream, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+        gpuCheck(createCopyStream(&slot->stream), "hipStreamCreateWithFlags");
       }
       copy = slot;
     }

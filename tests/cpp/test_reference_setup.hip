@@ -79,6 +79,11 @@ __global__ void localPortChannelKernel(int* dst, int* src, size_t bytes, int* re
   }
 }
 
+__global__ void loopbackPutWaitKernel(size_t bytes) {
+  gPortChannel.putWithSignal(0, bytes);
+  gPortChannel.wait();
+}
+
 static int runLocal() {
   MSCCLPP_CUDATHROW(hipSetDevice(0));
   auto bootstrap = std::make_shared<mscclpp::TcpBootstrap>(/*rank*/ 0, /*nRanks*/ 1);
@@ -106,8 +111,40 @@ static int runLocal() {
   hipLaunchKernelGGL(localPortChannelKernel, dim3(2), dim3(1024), 0, 0, (int*)dstBuff.get(), (int*)srcBuff.get(),
                      bytes, ret.get());
   MSCCLPP_CUDATHROW(hipDeviceSynchronize());
-  proxyService->stopProxy();
   CHECK(*ret == 0);
+  // One process, one proxy, the GPU to itself: 1000 graph-replayed iterations of putWithSignal +
+  // wait through the loopback channel (the 2-rank port mode's shape with no second process on the
+  // device), so DESIGN.md §9 can tell the proxy path's own latency from cross-process scheduling.
+  hipStream_t stream;
+  MSCCLPP_CUDATHROW(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  const int iter = 1000;
+  for (size_t copyBytes : {(size_t)1024, (size_t)1 << 20}) {
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+    MSCCLPP_CUDATHROW(hipStreamBeginCapture(stream, hipStreamCaptureModeGlobal));
+    for (int i = 0; i < iter; ++i) hipLaunchKernelGGL(loopbackPutWaitKernel, dim3(1), dim3(1), 0, stream, copyBytes);
+    MSCCLPP_CUDATHROW(hipStreamEndCapture(stream, &graph));
+    MSCCLPP_CUDATHROW(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    MSCCLPP_CUDATHROW(hipGraphLaunch(exec, stream));  // warm
+    MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+    hipEvent_t t0, t1;
+    MSCCLPP_CUDATHROW(hipEventCreate(&t0));
+    MSCCLPP_CUDATHROW(hipEventCreate(&t1));
+    MSCCLPP_CUDATHROW(hipEventRecord(t0, stream));
+    MSCCLPP_CUDATHROW(hipGraphLaunch(exec, stream));
+    MSCCLPP_CUDATHROW(hipEventRecord(t1, stream));
+    MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+    float ms = 0;
+    MSCCLPP_CUDATHROW(hipEventElapsedTime(&ms, t0, t1));
+    std::printf("LOCAL_JSON {\"bytes\": %zu, \"us_per_iter\": %.3f, \"iters\": %d}\n", copyBytes, ms * 1e3 / iter,
+                iter);
+    MSCCLPP_CUDATHROW(hipEventDestroy(t0));
+    MSCCLPP_CUDATHROW(hipEventDestroy(t1));
+    MSCCLPP_CUDATHROW(hipGraphExecDestroy(exec));
+    MSCCLPP_CUDATHROW(hipGraphDestroy(graph));
+  }
+  MSCCLPP_CUDATHROW(hipStreamDestroy(stream));
+  proxyService->stopProxy();
   std::printf("local OK\n");
   return 0;
 }

@@ -32,7 +32,11 @@ def _free_port():
 
 
 def test_port_channel_loopback_one_rank(built):
-    assert "local OK" in _run(["local"])
+    out = _run(["local"])
+    assert "local OK" in out
+    rows = [json.loads(x.split(" ", 1)[1]) for x in out.splitlines() if x.startswith("LOCAL_JSON ")]
+    assert [r["bytes"] for r in rows] == [1024, 1 << 20] and all(r["us_per_iter"] > 0 for r in rows), out
+    print(rows)
 
 
 def test_memory_channel_tutorial_ip_port(built):

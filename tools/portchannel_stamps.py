@@ -45,10 +45,11 @@ def worker(rank, uid, iters, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-def run(token, iters=200):
+def run(token, iters=200, priority=""):
     import mscclpp_amd as m
 
     os.environ["MSCCLPP_AMD_TOKEN_WRITE"] = token
+    os.environ["MSCCLPP_AMD_COPY_STREAM_PRIORITY"] = priority
     os.environ["MSCCLPP_AMD_PROXY_GAP_STATS"] = "1"
     uid = m.Communicator.unique_id()
     ctx = mp.get_context("spawn")
@@ -82,8 +83,22 @@ def tutorial(token):
     return {"rc": r.returncode, "rows": rows, "tail": r.stdout[-300:] if r.returncode else ""}
 
 
+def summary(rec):
+    """Median over both ranks of each column, per mode."""
+    out = {}
+    for mode in NAMES:
+        rows = [r[mode] for r in rec.values()]
+        out[mode] = {k: round(sorted(x[k] for x in rows)[len(rows) // 2], 2) for k in KEYS[3:]}
+    return out
+
+
 if __name__ == "__main__":
     tokens = sys.argv[1].split(",") if len(sys.argv) > 1 else ["memcpy", "writevalue"]
+    prios = sys.argv[2].split(",") if len(sys.argv) > 2 else [""]
     for tok in tokens:
-        print(json.dumps({"token_write": tok, "tutorial": tutorial(tok)}), flush=True)
-        print(json.dumps({"token_write": tok, "alltoall_1MiB": run(tok)}), flush=True)
+        for prio in prios:
+            print(json.dumps({"token_write": tok, "copy_stream_priority": prio or "normal",
+                              "tutorial": tutorial(tok) if not prio else None}), flush=True)
+            rec = run(tok, priority=prio)
+            print(json.dumps({"token_write": tok, "copy_stream_priority": prio or "normal",
+                              "alltoall_1MiB": rec, "summary": summary(rec)}), flush=True)
