@@ -53,8 +53,9 @@ class ProxyService : public BaseProxyService {
   // on).  For each of the next `cap` triggers the proxy thread records the host clock when it got
   // the trigger and after it had submitted the data copy, the token update and the flush, plus HIP
   // events on the connection stream after the data copy and after the token update (the device
-  // times at which they completed).  Read them after stopProxy(); the events stay owned by the
-  // service until the next enableStamps or its destruction.
+  // times at which they completed).  Call it with no trigger in flight (before startProxy, or once
+  // the kernels pushing triggers have completed on every rank); read them after stopProxy(); the
+  // events stay owned by the service until its destruction.
   struct TriggerStamp {
     uint32_t type = 0;       // TriggerData | TriggerFlag | TriggerSync bits of the trigger
     uint64_t seenNs = 0;     // steady clock when the handler started

@@ -5,7 +5,9 @@
 //                                 the peer's device (semaphore.cc:118-167)
 //   MemoryDevice2DeviceSemaphore  signalled by a device thread with a system-scope atomic add into
 //                                 the peer's token over xGMI (semaphore.cc:215-238)
-// Device handles carry the communicator's spin budget and error word.
+// Device handles carry the communicator's spin budget and error word.  An error word passed
+// explicitly (the `err` argument) must point at 4 words (16 bytes): a timed-out wait records the code
+// in err[0] and its detail in err[1..3] (device.hpp report_error_detail).
 #ifndef MSCCLPP_AMD_SEMAPHORE_HPP_
 #define MSCCLPP_AMD_SEMAPHORE_HPP_
 

@@ -18,9 +18,12 @@ namespace detail {
 __device__ __forceinline__ bool spinUntilAtLeast(uint64_t* token, uint64_t want, bool acquire, uint64_t budget,
                                                  uint32_t* err) {
   SpinGuard g(budget ? budget : kDefaultSpinTicks);
-  while (ld_relaxed_sys(token) < want) {
+  uint64_t seen;
+  while ((seen = ld_relaxed_sys(token)) < want) {
     if (g.expired()) {
-      report_error(err, kErrSemaphoreTimeout);
+      // detail: a channel-handle wait (marker), the token value waited for and the one seen (low 32
+      // bits): seen == want - 1 means the peer's last signal never arrived
+      report_error_detail(err, kErrSemaphoreTimeout, 0x5E000000u, (uint32_t)want, (uint32_t)seen);
       return false;
     }
   }
