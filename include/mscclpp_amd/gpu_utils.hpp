@@ -47,13 +47,51 @@ struct CudaDeviceGuard {
   int origDeviceId_;
 };
 
+// Relaxed stream-capture mode for the guard's lifetime (the reference's AvoidCudaGraphCaptureGuard,
+// gpu_utils.hpp:30-38): a set-up call made while another thread captures a graph neither joins nor
+// invalidates that capture.
+struct AvoidCudaGraphCaptureGuard {
+  AvoidCudaGraphCaptureGuard() : mode_(hipStreamCaptureModeRelaxed) {
+    (void)hipThreadExchangeStreamCaptureMode(&mode_);
+  }
+  ~AvoidCudaGraphCaptureGuard() { (void)hipThreadExchangeStreamCaptureMode(&mode_); }
+  AvoidCudaGraphCaptureGuard(const AvoidCudaGraphCaptureGuard&) = delete;
+  AvoidCudaGraphCaptureGuard& operator=(const AvoidCudaGraphCaptureGuard&) = delete;
+  hipStreamCaptureMode mode_;
+};
+
 namespace detail {
+// Run op(stream) on a stream of its own and wait for it: the reference's gpuCalloc / gpuMemcpy /
+// gpuMemset are synchronous (gpu_utils.cc:120-128, :262-283) -- the fill or copy has completed on the
+// device when they return.  (A bare hipMemset of device memory is asynchronous to the host: a host
+// barrier after it does not order it before a peer's kernel)
+template <typename F>
+void syncOnOwnStream(F&& op, const char* what) {
+  AvoidCudaGraphCaptureGuard guard;
+  hipStream_t s = nullptr;
+  gpuCheck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+  hipError_t e = op(s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipStreamDestroy(s);
+  gpuCheck(e, what);
+}
+
+inline void* gpuCalloc(size_t bytes) {
+  AvoidCudaGraphCaptureGuard guard;
+  void* p = nullptr;
+  gpuCheck(hipMalloc(&p, bytes), "hipMalloc");
+  try {
+    syncOnOwnStream([&](hipStream_t s) { return hipMemsetAsync(p, 0, bytes, s); }, "hipMemsetAsync");
+  } catch (...) {
+    (void)hipFree(p);
+    throw;
+  }
+  return p;
+}
+
 template <typename T>
 std::shared_ptr<T> gpuCallocShared(size_t nelems = 1) {
-  void* p = nullptr;
-  gpuCheck(hipMalloc(&p, nelems * sizeof(T)), "hipMalloc");
-  gpuCheck(hipMemset(p, 0, nelems * sizeof(T)), "hipMemset");
-  return std::shared_ptr<T>(static_cast<T*>(p), [](T* q) { (void)hipFree(q); });
+  return std::shared_ptr<T>(static_cast<T*>(gpuCalloc(nelems * sizeof(T))), [](T* q) { (void)hipFree(q); });
 }
 // Uncached memory comes from the library's process-lifetime pool (mscclppAmdMallocUncached, zeroed;
 // released back to the pool, never to HIP, while the process runs: DESIGN.md §21).
@@ -86,10 +124,7 @@ using UniqueGpuUncachedPtr = std::unique_ptr<T, GpuUncachedDeleter<T>>;
 
 template <class T>
 UniqueGpuPtr<T> gpuCallocUnique(size_t nelems = 1) {
-  void* p = nullptr;
-  gpuCheck(hipMalloc(&p, nelems * sizeof(T)), "hipMalloc");
-  gpuCheck(hipMemset(p, 0, nelems * sizeof(T)), "hipMemset");
-  return UniqueGpuPtr<T>(static_cast<T*>(p));
+  return UniqueGpuPtr<T>(static_cast<T*>(gpuCalloc(nelems * sizeof(T))));
 }
 // Zeroed host memory the GPU can reach (hipHostMalloc; mapped by default, gpu_utils.hpp:233-241).
 inline void* gpuCallocHost(size_t bytes, unsigned int flags) {
@@ -115,15 +150,21 @@ UniqueGpuUncachedPtr<T> gpuCallocUncachedUnique(size_t nelems = 1) {
 }
 }  // namespace detail
 
+// Synchronous copy and fill, each on a stream of its own (gpu_utils.cc:262-283): complete on the
+// device when they return, whatever the direction.
 template <typename T = char>
 void gpuMemcpy(T* dst, const T* src, size_t nelems, hipMemcpyKind kind = hipMemcpyDefault) {
-  gpuCheck(hipMemcpy(dst, src, nelems * sizeof(T), kind), "hipMemcpy");
+  detail::syncOnOwnStream(
+      [&](hipStream_t s) { return hipMemcpyAsync(dst, src, nelems * sizeof(T), kind, s); }, "hipMemcpyAsync");
 }
 template <typename T = char>
 void gpuMemcpyAsync(T* dst, const T* src, size_t nelems, hipStream_t stream, hipMemcpyKind kind = hipMemcpyDefault) {
+  AvoidCudaGraphCaptureGuard guard;
   gpuCheck(hipMemcpyAsync(dst, src, nelems * sizeof(T), kind, stream), "hipMemcpyAsync");
 }
-inline void gpuMemset(void* ptr, int value, size_t bytes) { gpuCheck(hipMemset(ptr, value, bytes), "hipMemset"); }
+inline void gpuMemset(void* ptr, int value, size_t bytes) {
+  detail::syncOnOwnStream([&](hipStream_t s) { return hipMemsetAsync(ptr, value, bytes, s); }, "hipMemsetAsync");
+}
 
 // No NVSwitch multicast or Hopper bulk copies on MI355X (gpu_utils.hpp:334-336).
 inline bool isNvlsSupported() { return false; }

@@ -32,7 +32,7 @@ int mscclppAmdMemChannelPingPong(ncclComm_t comm, int nElem, int iters, int ll8,
     void* pkt = allocUncached(bytes * 2);           // LL16: nElem / 2 16-byte packets; LL8: nElem 8-byte
     int* ret = nullptr;
     HIPCHECK(hipMalloc((void**)&ret, sizeof(int)));
-    HIPCHECK(hipMemset(ret, 0, sizeof(int)));
+    memsetSync(ret, 0, sizeof(int));
     hipStream_t st = nullptr;
     HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     double us = 0;

@@ -67,9 +67,9 @@ Fifo::Fifo(int size) : size_(size) {
   gpuCheck(hipHostGetDevicePointer((void**)&dTriggers_, (void*)triggers_, 0), "hipHostGetDevicePointer");
   gpuCheck(hipHostGetDevicePointer((void**)&dTail_, (void*)tail_, 0), "hipHostGetDevicePointer");
   gpuCheck(hipMalloc((void**)&head_, 64), "hipMalloc");
-  gpuCheck(hipMemset(head_, 0, 64), "hipMemset");
+  memsetSync(head_, 0, 64);
   gpuCheck(hipMalloc((void**)&tailCache_, 64), "hipMalloc");
-  gpuCheck(hipMemset(tailCache_, 0, 64), "hipMemset");
+  memsetSync(tailCache_, 0, 64);
 }
 
 Fifo::~Fifo() {

@@ -247,14 +247,14 @@ int commInitRank(ncclComm_t* comm, int nranks, const void* commId, int rank, int
     const size_t tokBytes = sizeof(uint64_t) * MSCCLPP_AMD_MAX_RANKS * MSCCLPP_AMD_MAX_CHANNELS;
     c->tokens = (uint64_t*)allocUncached(tokBytes);
     HIPCHECK(hipMalloc((void**)&c->expected, tokBytes));
-    HIPCHECK(hipMemset(c->expected, 0, tokBytes));
+    memsetSync(c->expected, 0, tokBytes);
     HIPCHECK(hipMalloc((void**)&c->flags, MSCCLPP_AMD_FLAG_SLOTS * sizeof(uint32_t)));
     {
       std::vector<uint32_t> ones(MSCCLPP_AMD_FLAG_SLOTS, 1u);
       HIPCHECK(hipMemcpy(c->flags, ones.data(), ones.size() * 4, hipMemcpyHostToDevice));
     }
     HIPCHECK(hipMalloc((void**)&c->err, 256));
-    HIPCHECK(hipMemset(c->err, 0, 256));
+    memsetSync(c->err, 0, 256);
     if (nranks > 1) {
       info("rank " + std::to_string(rank) + ": exchanging semaphore tokens");
       c->peerTok = c->exchange(c->tokens);
@@ -578,7 +578,7 @@ int mscclppAmdCommGetDeviceError(ncclComm_t comm, uint32_t* code, int clear) {
   return guarded([&] {
     if (!comm || !code) return (int)ncclInvalidArgument;
     HIPCHECK(hipMemcpy(code, comm->err, sizeof(uint32_t), hipMemcpyDeviceToHost));
-    if (clear) HIPCHECK(hipMemset(comm->err, 0, sizeof(uint32_t)));
+    if (clear) memsetSync(comm->err, 0, sizeof(uint32_t));
     return (int)ncclSuccess;
   });
 }
@@ -587,7 +587,7 @@ int mscclppAmdCommGetDeviceErrorDetail(ncclComm_t comm, uint32_t* words4, int cl
   return guarded([&] {
     if (!comm || !words4) return (int)ncclInvalidArgument;
     HIPCHECK(hipMemcpy(words4, comm->err, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    if (clear) HIPCHECK(hipMemset(comm->err, 0, 4 * sizeof(uint32_t)));
+    if (clear) memsetSync(comm->err, 0, 4 * sizeof(uint32_t));
     return (int)ncclSuccess;
   });
 }

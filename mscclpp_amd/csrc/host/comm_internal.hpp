@@ -143,6 +143,12 @@ inline size_t bulkScratchInitBytes() {
 // at the allocation that reuses it (uncached_pool.cpp).
 void* allocUncached(size_t bytes);
 bool releaseUncached(void* p, hipError_t* syncError) noexcept;
+// Fill `bytes` of device memory with `value` and return once the fill has completed on the device
+// (own non-blocking stream + synchronize, as the reference's gpuMemset, gpu_utils.cc:274-283).  Every
+// set-up fill of memory that a peer, a proxy or a kernel on another stream may touch next goes
+// through it: a plain hipMemset is asynchronous to the host, so a host barrier or exchange after it
+// orders nothing on the device.
+void memsetSync(void* p, int value, size_t bytes);
 void freeDevice(void* p) noexcept;
 void uncachedPoolStats(size_t* held, size_t* inUse, size_t* freeBytes);
 bool isPooledUncached(const void* base);  // `base` is a live block of the pool (an allocation base)

@@ -838,7 +838,7 @@ Host2DeviceSemaphore::Host2DeviceSemaphore(const Semaphore& semaphore, uint64_t 
     : semaphore_(semaphore) {
   if (!semaphore.valid()) throw Error("Host2DeviceSemaphore: empty Semaphore", ErrorCode::InvalidUsage);
   gpuCheck(hipMalloc((void**)&expectedInboundToken_, sizeof(uint64_t)), "hipMalloc");
-  gpuCheck(hipMemset(expectedInboundToken_, 0, sizeof(uint64_t)), "hipMemset");
+  memsetSync(expectedInboundToken_, 0, sizeof(uint64_t));
   budget_ = budget ? budget : semaphore.pimpl()->budget;
   err_ = err ? err : semaphore.pimpl()->err;
 }
@@ -869,7 +869,7 @@ MemoryDevice2DeviceSemaphore::MemoryDevice2DeviceSemaphore(const Semaphore& sema
     : semaphore_(semaphore) {
   if (!semaphore.valid()) throw Error("MemoryDevice2DeviceSemaphore: empty Semaphore", ErrorCode::InvalidUsage);
   gpuCheck(hipMalloc((void**)&expectedInboundToken_, sizeof(uint64_t)), "hipMalloc");
-  gpuCheck(hipMemset(expectedInboundToken_, 0, sizeof(uint64_t)), "hipMemset");
+  memsetSync(expectedInboundToken_, 0, sizeof(uint64_t));
   budget_ = budget ? budget : semaphore.pimpl()->budget;
   err_ = err ? err : semaphore.pimpl()->err;
 }

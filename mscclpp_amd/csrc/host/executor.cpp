@@ -454,11 +454,11 @@ struct mscclppAmdExecutor {
     const size_t tokBytes = sizeof(uint64_t) * ex::kMaxRanks * ex::kMaxTags;
     tokens = (uint64_t*)allocUncached(tokBytes);
     HIPCHECK(hipMalloc((void**)&expected, tokBytes));
-    HIPCHECK(hipMemset(expected, 0, tokBytes));
+    memsetSync(expected, 0, tokBytes);
     HIPCHECK(hipMalloc((void**)&syncers, sizeof(ex::Syncer) * ex::kMaxSyncers));
-    HIPCHECK(hipMemset(syncers, 0, sizeof(ex::Syncer) * ex::kMaxSyncers));
+    memsetSync(syncers, 0, sizeof(ex::Syncer) * ex::kMaxSyncers);
     HIPCHECK(hipMalloc((void**)&err, 256));
-    HIPCHECK(hipMemset(err, 0, 256));
+    memsetSync(err, 0, 256);
     HIPCHECK(hipDeviceSynchronize());
     if (comm->nranks > 1) peerTokens = comm->exchange(tokens);
     else peerTokens[0] = tokens;
@@ -722,7 +722,7 @@ int mscclppAmdExecutorGetDeviceError(mscclppAmdExecutor_t executor, uint32_t* wo
     if (!executor || !words4) return (int)ncclInvalidArgument;
     HIPCHECK(hipDeviceSynchronize());
     HIPCHECK(hipMemcpy(words4, executor->err, 16, hipMemcpyDeviceToHost));
-    if (clear) HIPCHECK(hipMemset(executor->err, 0, 16));
+    if (clear) memsetSync(executor->err, 0, 16);
     return (int)ncclSuccess;
   });
 }

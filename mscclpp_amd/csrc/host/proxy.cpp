@@ -127,9 +127,9 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
     uint64_t* tok = nullptr;
     uint64_t* expct = nullptr;
     HIPCHECK(hipMalloc((void**)&tok, 2 * n * 8));
-    HIPCHECK(hipMemset(tok, 0, 2 * n * 8));
+    memsetSync(tok, 0, 2 * n * 8);
     HIPCHECK(hipMalloc((void**)&expct, 2 * n * 8));
-    HIPCHECK(hipMemset(expct, 0, 2 * n * 8));
+    memsetSync(expct, 0, 2 * n * 8);
     auto peerTok = comm->exchange(tok);
     std::vector<std::unique_ptr<TokenWriter>> writers(2 * n);
     for (auto& w : writers) w = std::make_unique<TokenWriter>();
@@ -150,7 +150,7 @@ extern "C" int mscclppAmdHostOffloadAllGather(ncclComm_t comm, size_t dataSize, 
       if (r != rank) conns[r].stream = copyStream;
     uint32_t* err = nullptr;
     HIPCHECK(hipMalloc((void**)&err, 64));
-    HIPCHECK(hipMemset(err, 0, 64));
+    memsetSync(err, 0, 64);
     // MyProxyService::handleTrigger (:135-155)
     std::string proxyFailure;  // first copy / token failure on the proxy thread
     Proxy proxy([&](ProxyTrigger t, uint64_t) {
@@ -473,7 +473,7 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     uint64_t* tok = (uint64_t*)allocUncached(2 * n * 8);
     uint64_t* expct = nullptr;
     HIPCHECK(hipMalloc((void**)&expct, 2 * n * 8));
-    HIPCHECK(hipMemset(expct, 0, 2 * n * 8));
+    memsetSync(expct, 0, 2 * n * 8);
     auto peerTok = comm->exchange(tok);
     uint64_t *flushDone = nullptr, *dFlushDone = nullptr;
     TokenWriter writers[2];
@@ -482,10 +482,10 @@ extern "C" int mscclppAmdProxyRingAllReduce(ncclComm_t comm, size_t nelems, int 
     HIPCHECK(hipHostGetDevicePointer((void**)&dFlushDone, flushDone, 0));
     uint32_t* err = nullptr;
     HIPCHECK(hipMalloc((void**)&err, 64));
-    HIPCHECK(hipMemset(err, 0, 64));
+    memsetSync(err, 0, 64);
     void* gb = nullptr;
     HIPCHECK(hipMalloc(&gb, 64));
-    HIPCHECK(hipMemset(gb, 0, 64));
+    memsetSync(gb, 0, 64);
     Conn conn;
     HIPCHECK(hipStreamCreateWithFlags(&conn.stream, hipStreamNonBlocking));
     // MemoryId 0 = my buffer, 1 = next's scratch, 2 = next's buffer; semaphoreId = round

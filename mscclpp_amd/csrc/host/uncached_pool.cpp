@@ -209,6 +209,16 @@ void* allocUncached(size_t bytes) {
   return p;
 }
 
+void memsetSync(void* p, int value, size_t bytes) {
+  if (!p || bytes == 0) return;
+  hipStream_t s = nullptr;
+  HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipError_t e = hipMemsetAsync(p, value, bytes, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipStreamDestroy(s);
+  HIPCHECK(e);
+}
+
 bool releaseUncached(void* p, hipError_t* syncError) noexcept {
   if (syncError) *syncError = hipSuccess;
   if (!p) return true;
