@@ -330,13 +330,17 @@ def bench_single(args):
         # the reference's MemoryChannel packet ping-pong latency (memory_channel_tests.cu:98-107), from
         # the same two host-proxy ranks: on a 1-GPU box both ranks share the GPU
         pp = (hp or {}).get("pingpong") or {}
+        devs = (hp or {}).get("devices") or []
+        where = ("two processes on ONE GPU through IPC-mapped packet buffers: a shared-device figure, not an "
+                 "xGMI latency" if len(devs) == 1 else
+                 f"two processes on GPUs {devs} through IPC-mapped peer packet buffers: one xGMI hop")
         res["extras"] = {
             "ll16_pingpong_us": pp.get("ll16", {}).get("us_per_iter"),
             "ll8_pingpong_us": pp.get("ll8", {}).get("us_per_iter"),
             "pingpong_correct": (hp or {}).get("pingpong_correct"),
+            "pingpong_devices": devs,
             "pingpong_note": "us per one-way hand-off of 1024 ints (100k timed iterations, 1 workgroup per rank), "
-                             "two processes on ONE GPU through IPC-mapped packet buffers: a shared-device figure, "
-                             "not an xGMI latency"}
+                             + where}
     pk.free()
     return res
 

@@ -36,7 +36,7 @@ def worker(rank, n, uid, size, q):
         m.check(L.mscclppAmdHostOffloadAllGather(comm.comm, size, 10, 10, out), "host offload")
         print(f"[host_proxy rank {rank}/{n}] PortChannel all-to-all", file=sys.stderr, flush=True)
         res = {"us_per_kernel_nograph": out[0], "us_per_kernel_graph": out[1], "correct": out[2] == 1.0,
-               "proxy_numa_node": int(out[3])}
+               "proxy_numa_node": int(out[3]), "device": rank % ndev}
         pc = {}
         for mode in (0, 1, 2):
             # PC_ITERS back-to-back iterations after one untimed launch; each iteration's own time from
@@ -108,6 +108,7 @@ def run(n=2, size=4096, timeout=180):
             "cores": 2 * n, "cores_note": "per rank: 1 busy-poll proxy thread + 1 launching thread",
             "proxy_numa_node": r0["proxy_numa_node"], "portchannel_alltoall_1MiB": r0["portchannel_alltoall_1MiB"],
             "pingpong": r0.get("pingpong"),
+            "devices": sorted({g["device"] for g in got.values()}),
             "pingpong_correct": all(g.get("pingpong", {}).get(k, {}).get("correct", False)
                                     for g in got.values() for k in ("ll16", "ll8")) if n == 2 else None,
             "path": "test/allgather_test_host_offloading.cu restated on libmscclpp_amd (FIFO + proxy + hipMemcpyAsync)"}
