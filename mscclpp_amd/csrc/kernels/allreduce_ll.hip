@@ -94,6 +94,25 @@ __device__ __forceinline__ u32x2 unit_get(__amdgpu_buffer_rsrc_t pk, uint32_t pb
   }
   return w;
 }
+// add_vectors<TYPE>(a, b) of python/mscclpp_benchmark/allreduce.cu:37-96 on one 8-byte payload: int
+// wrapping adds, float `a + b`, __half __hadd2 -- round to nearest even and no clip (inf on overflow),
+// unlike the collectives' f16x2 operator+ (gpu_data_types.hpp:389-397).
+template <int DT>
+__device__ __forceinline__ u32x2 bench_add2(u32x2 a, u32x2 b) {
+  if constexpr (DT == kF16) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 x0 = __builtin_bit_cast(h2, a.x), y0 = __builtin_bit_cast(h2, b.x);
+    const h2 x1 = __builtin_bit_cast(h2, a.y), y1 = __builtin_bit_cast(h2, b.y);
+    return u32x2{__builtin_bit_cast(uint32_t, x0 + y0), __builtin_bit_cast(uint32_t, x1 + y1)};
+  } else if constexpr (DT == kF32) {
+    return u32x2{__builtin_bit_cast(uint32_t, __builtin_bit_cast(float, a.x) + __builtin_bit_cast(float, b.x)),
+                 __builtin_bit_cast(uint32_t, __builtin_bit_cast(float, a.y) + __builtin_bit_cast(float, b.y))};
+  } else {
+    static_assert(DT == kI32 || DT == kU32, "the benchmark's allreduce2 types are int, float and __half");
+    return u32x2{a.x + b.x, a.y + b.y};
+  }
+}
+
 // First poll of unit `pbyte` in every peer's region (peer p's at p * stride of `base`): all loads
 // are issued, unconditionally and in one basic block, before any value is compared, so they are in
 // flight together (a compare right after each load, or a load under a branch, made the compiler wait
@@ -312,17 +331,28 @@ __global__ void __launch_bounds__(512) allreduceLL16Kernel(Views<NV> views, LL16
         own = payload_ld(rin, in, off, valid);
         missing = poll_eval(raw, flag, peers, w);
       }
-      Accum<DT, OP, 2> sum(own);  // upcastVector (:98-99)
       count_misses<V>(v.err + 8, (uint32_t)__builtin_popcount(missing));
       if (missing) {
 #pragma unroll
         for (int p = 0; p < kMaxRanks; ++p)
           if ((missing >> p) & 1u) w[p] = unit_wait(rscr, (uint32_t)(p * g.ppr * 16) + j * 16u, flag, false, budget, v.err);
       }
+      u32x2 acc;
+      if constexpr ((V & 2048) != 0) {
+        // mscclpp-test allreduce6 / the benchmark's allreduce2 (allreduce.cu:254-264): data = 0, then
+        // data = val + data for the peers ascending, then data + own, each add unclipped
+        acc = u32x2{0u, 0u};
 #pragma unroll
-      for (int p = 0; p < kMaxRanks; ++p)
-        if ((peers >> p) & 1u) sum.add(w[p]);
-      const u32x2 acc = sum.template get<u32x2>();  // downcastVector (:107-108)
+        for (int p = 0; p < kMaxRanks; ++p)
+          if ((peers >> p) & 1u) acc = bench_add2<DT>(w[p], acc);
+        acc = bench_add2<DT>(acc, own);
+      } else {
+        Accum<DT, OP, 2> sum(own);  // upcastVector (:98-99)
+#pragma unroll
+        for (int p = 0; p < kMaxRanks; ++p)
+          if ((peers >> p) & 1u) sum.add(w[p]);
+        acc = sum.template get<u32x2>();  // downcastVector (:107-108)
+      }
       payload_st(rout, out, off, acc, valid);
       // broadcast: a runtime loop, so one descriptor is live at a time (SGPR budget)
 #pragma unroll 1
@@ -631,6 +661,26 @@ static void launchLL8(const mscclppAmdRankView* views, int nviews, const LL8Geom
     launchLL8T<DT, OP, kMaxRanks, V>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
   }
 }
+// mscclpp-test allreduce6 / allreduce7 and the benchmark's allreduce2: the LL16 kernel with the harness
+// geometry and the benchmark's sum order (V 2048).  int32 for the harness kernels; fp16 and fp32 as the
+// benchmark builds allreduce2 with TYPE=__half / float.
+template <int DT, int OP>
+static void launchTestK6(const mscclppAmdRankView* views, int nviews, const LL16Geom& g, int nranks, int nblocks,
+                         int nthreads, uint64_t budget, hipStream_t s) {
+  if constexpr ((DT == kI32 || DT == kU32 || DT == kF16 || DT == kF32) && OP == kSum) {
+    if (nviews == 1) {
+      Views<1> vw;
+      vw.v[0] = views[0];
+      launchLL16T<DT, OP, 1, 2048>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+    } else {
+      Views<kMaxRanks> vw{};
+      for (int i = 0; i < nviews; ++i) vw.v[i] = views[i];
+      launchLL16T<DT, OP, kMaxRanks, 2048>(vw, nviews, g, nranks, nblocks, nthreads, budget, s);
+    }
+  } else {
+    launchLL16<DT, OP>(views, nviews, g, nranks, nblocks, nthreads, budget, s);  // int32 MIN: order-free
+  }
+}
 template <int DT, int OP>
 static void launchTestK2(const mscclppAmdRankView* views, int nviews, const LL8Geom& g, int nranks, int nblocks,
                          int nthreads, uint64_t budget, hipStream_t s) {
@@ -714,12 +764,20 @@ int launchAllReduceLL(int algo, const mscclppAmdRankView* views, int nviews, int
     nblocks = nblocks / (nranks - 1) * (nranks - 1);
     if (nblocks < nranks - 1) nblocks = nranks - 1;
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;
-    if (dtype != kI32 && dtype != kU32) return 4;  // the mscclpp-test kernels are int32 AllReduces
+    // the mscclpp-test kernels are int32 AllReduces; k6 also runs fp16 / fp32 SUM as the benchmark's
+    // allreduce2 (python/mscclpp_benchmark/allreduce.cu:223-289, TYPE=__half / float) does
+    const bool benchTyped = algo == MSCCLPP_AMD_ALGO_TEST_K6 && (dtype == kF16 || dtype == kF32) && op == kSum;
+    if (dtype != kI32 && dtype != kU32 && !benchTyped) return 4;
     LL16Geom g;
     if (!testLLGeometry(nranks, bytes, &g) || !ll16Fits(nranks, g)) return 5;
     for (int i = 0; i < nviews; ++i)
       if (views[i].scratchBytes < testLLScratchRequired(nranks, bytes)) return 5;
-    MSCCLPP_AMD_DISPATCH(dtype, op, launchLL16, views, nviews, g, nranks, nblocks, nthreads, budget, s);
+    if (dtype == kF16)
+      launchTestK6<kF16, kSum>(views, nviews, g, nranks, nblocks, nthreads, budget, s);
+    else if (dtype == kF32)
+      launchTestK6<kF32, kSum>(views, nviews, g, nranks, nblocks, nthreads, budget, s);
+    else
+      MSCCLPP_AMD_DISPATCH(dtype, op, launchTestK6, views, nviews, g, nranks, nblocks, nthreads, budget, s);
   } else {
     ll8Defaults(nranks, bytes, nblocks, nthreads);
     if (nblocks > kFlagSlots || nthreads > 512 || nthreads % 64) return 4;

@@ -169,9 +169,13 @@ def run_typed_case(L, kind, n, nwords, blocks_per_peer, threads):
     assert all(rptr), "refMallocUncached failed"
     import mscclpp_amd as m
 
+    tdt = torch.float16 if kind == "f16" else torch.float32
+    mdt = m.F16 if kind == "f16" else m.F32
+    assert m.scratch_required(m.ALGO_TEST_K6, n, nwords * 4, mdt) == sb
+    ours = m.InProcessRanks(n, sb)  # this library's k6 on the same inputs: the product kernel, typed
     rscr = [m.device_view(p, sb).view(torch.int32) for p in rptr]
     rec = {"type": kind, "n": n, "words": nwords, "blocks_per_peer": blocks_per_peer, "threads": threads,
-           "nan_words": 0, "inf_words": 0, "order_sensitive_words": 0}
+           "nan_words": 0, "inf_words": 0, "order_sensitive_words": 0, "k6_compared": True}
     try:
         for call, flag in enumerate((1, 2, 3)):
             ins = typed_inputs(kind, n, nwords, 7000 * n + 10 * call + nwords % 991 + (1 if kind == "f16" else 0))
@@ -183,10 +187,21 @@ def run_typed_case(L, kind, n, nwords, blocks_per_peer, threads):
                 print(json.dumps({"timeout": rec, "call": call}), flush=True)
                 os._exit(3)
             assert rc == 0, f"refBench2Run returned {rc}"
+            douts = [torch.zeros_like(d) for d in dins]
+            ours.all_reduce([d.view(tdt) for d in dins], [o.view(tdt) for o in douts], m.ALGO_TEST_K6)
+            torch.cuda.synchronize()
+            assert ours.errors() == [0] * n
             exp, scr = O.bench_allreduce2(dtype, ins, nwords, flag, sb, order=0)
             alt, _ = O.bench_allreduce2(dtype, ins, nwords, flag, sb, order=1)
             for r in range(n):
                 got = rout[r].cpu().numpy().view(np.uint32)
+                mine = douts[r].cpu().numpy().view(np.uint32)
+                bad_k6 = np.nonzero(mine != got)[0]
+                if bad_k6.size:
+                    rows = [{"word": int(w), "ref": hex(int(got[w])), "k6": hex(int(mine[w])),
+                             "inputs": [hex(int(a[w])) for a in ins]} for w in bad_k6[:8]]
+                    raise AssertionError(json.dumps({"case": rec, "call": call, "rank": r, "k6_mismatched_words":
+                                                     int(bad_k6.size), "first": rows}))
                 bad = np.nonzero(got != exp[r])[0]
                 if bad.size:
                     rows = [{"word": int(w), "ref": hex(int(got[w])), "oracle": hex(int(exp[r][w])),
@@ -203,6 +218,8 @@ def run_typed_case(L, kind, n, nwords, blocks_per_peer, threads):
                 for r in range(n):
                     img = rscr[r].cpu().numpy().view(np.uint32)
                     assert np.array_equal(scr[r], img), f"oracle vs reference scratch image ({kind}), rank {r}"
+                    our_img = ours.scratch_tensor(r, sb).cpu().numpy().view(np.uint32)
+                    assert np.array_equal(our_img, img), f"k6 vs reference scratch image ({kind}), rank {r}"
                 rec["scratch_words_compared"] = int(n * sb // 4)
         assert rec["order_sensitive_words"] > 0, "own-first order matched everywhere: the check cannot see order"
         assert rec["nan_words"] > 0 and rec["inf_words"] > 0, rec

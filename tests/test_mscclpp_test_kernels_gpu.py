@@ -128,7 +128,9 @@ def test_harness_kat(built):
 
 
 def test_restrictions(built):
-    """k5 runs in place; k2/k5/k6/k7 are int32 kernels; k6/k7 need bytes % (8 * n) == 0, k2 an even count."""
+    """k5 runs in place; k2/k5/k7 are int32 kernels and k6 runs int32, or fp16 / fp32 SUM as the
+    benchmark's allreduce2 (bf16 and fp16 MIN are refused); k6/k7 need bytes % (8 * n) == 0, k2 an
+    even count."""
     import mscclpp_amd as m
 
     n = 4
@@ -138,8 +140,13 @@ def test_restrictions(built):
     with pytest.raises(m.MscclppError):
         ranks.all_reduce(a, b, m.ALGO_TEST_K5)  # out of place
     f = [torch.zeros(1024, dtype=torch.float16, device="cuda") for _ in range(n)]
+    bf = [torch.zeros(1024, dtype=torch.bfloat16, device="cuda") for _ in range(n)]
     with pytest.raises(m.MscclppError):
-        ranks.all_reduce(f, f, m.ALGO_TEST_K6)
+        ranks.all_reduce(bf, [torch.empty_like(t) for t in bf], m.ALGO_TEST_K6)
+    with pytest.raises(m.MscclppError):
+        ranks.all_reduce(f, [torch.empty_like(t) for t in f], m.ALGO_TEST_K6, op=m.MIN)
+    with pytest.raises(m.MscclppError):
+        ranks.all_reduce(f, [torch.empty_like(t) for t in f], m.ALGO_TEST_K7)
     odd = [torch.zeros(4 * n + 4, dtype=torch.int32, device="cuda") for _ in range(n)]
     with pytest.raises(m.MscclppError):
         ranks.all_reduce(odd, [torch.empty_like(t) for t in odd], m.ALGO_TEST_K6)

@@ -59,7 +59,9 @@ def test_reference_allreduce2_fp16_fp32_order_and_rounding(built):
     +0), half-ulp lanes that only a peers-first order keeps, overflow to inf, cancellation at +-max,
     subnormals and NaN lanes (quiet and signalling, payloads, both signs); the whole scratch images
     match after the first call; and the own-first order differs on some words of every case, so the
-    check discriminates order."""
+    check discriminates order.  This library's k6 (the same two-hop kernel with the benchmark's sum
+    order, run on fp16 / fp32 buffers) matches the reference kernel's outputs and scratch images bit
+    for bit on the same inputs."""
     if not (all(os.path.exists(p) for p in TYPED_HSACO) and os.path.exists(REF_SO)):
         pytest.skip("oracle/_ref typed code objects not built (needs /root/reference at build time)")
     env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
@@ -72,6 +74,7 @@ def test_reference_allreduce2_fp16_fp32_order_and_rounding(built):
     for x in recs:
         assert x["calls"] == 3 and x["scratch_words_compared"] == x["n"] * 8 * x["words"], x
         assert x["order_sensitive_words"] > 0 and x["nan_words"] > 0 and x["inf_words"] > 0, x
+        assert x["k6_compared"] is True, x
     print(json.dumps(recs))
 
 
