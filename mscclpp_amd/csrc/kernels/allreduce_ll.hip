@@ -97,19 +97,24 @@ __device__ __forceinline__ u32x2 unit_get(__amdgpu_buffer_rsrc_t pk, uint32_t pb
 // add_vectors<TYPE>(a, b) of python/mscclpp_benchmark/allreduce.cu:37-96 on one 8-byte payload: int
 // wrapping adds, float `a + b`, __half __hadd2 -- round to nearest even and no clip (inf on overflow),
 // unlike the collectives' f16x2 operator+ (gpu_data_types.hpp:389-397).
+// The words are copied out of the vectors before the bit casts: this compiler (ROCm 7.2 clang)
+// lowers __builtin_bit_cast of an ext_vector element such as `a.y` to a cast of element 0 -- the
+// kernel then summed the first word twice (caught by tests/test_reference_kernel_gpu.py).
 template <int DT>
 __device__ __forceinline__ u32x2 bench_add2(u32x2 a, u32x2 b) {
+  const uint32_t a0 = a.x, a1 = a.y, b0 = b.x, b1 = b.y;
   if constexpr (DT == kF16) {
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    const h2 x0 = __builtin_bit_cast(h2, a.x), y0 = __builtin_bit_cast(h2, b.x);
-    const h2 x1 = __builtin_bit_cast(h2, a.y), y1 = __builtin_bit_cast(h2, b.y);
-    return u32x2{__builtin_bit_cast(uint32_t, x0 + y0), __builtin_bit_cast(uint32_t, x1 + y1)};
+    const h2 s0 = __builtin_bit_cast(h2, a0) + __builtin_bit_cast(h2, b0);
+    const h2 s1 = __builtin_bit_cast(h2, a1) + __builtin_bit_cast(h2, b1);
+    return u32x2{__builtin_bit_cast(uint32_t, s0), __builtin_bit_cast(uint32_t, s1)};
   } else if constexpr (DT == kF32) {
-    return u32x2{__builtin_bit_cast(uint32_t, __builtin_bit_cast(float, a.x) + __builtin_bit_cast(float, b.x)),
-                 __builtin_bit_cast(uint32_t, __builtin_bit_cast(float, a.y) + __builtin_bit_cast(float, b.y))};
+    const float s0 = __builtin_bit_cast(float, a0) + __builtin_bit_cast(float, b0);
+    const float s1 = __builtin_bit_cast(float, a1) + __builtin_bit_cast(float, b1);
+    return u32x2{__builtin_bit_cast(uint32_t, s0), __builtin_bit_cast(uint32_t, s1)};
   } else {
     static_assert(DT == kI32 || DT == kU32, "the benchmark's allreduce2 types are int, float and __half");
-    return u32x2{a.x + b.x, a.y + b.y};
+    return u32x2{a0 + b0, a1 + b1};
   }
 }
 
