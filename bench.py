@@ -190,6 +190,27 @@ def host_proxy_baseline(n=2, timeout=240):
         return {"error": str(e)[-400:]}
 
 
+def pingpong_extras(hp):
+    """The N=1 line's extras: the reference's MemoryChannel packet ping-pong latency
+    (memory_channel_tests.cu:98-107), measured by the two host-proxy ranks (tools/host_proxy_baseline.py),
+    labelled by where those ranks ran: one shared GPU, or two GPUs one xGMI hop apart."""
+    hp = hp or {}
+    pp = hp.get("pingpong") or {}
+    devs = hp.get("devices") or []
+    if len(devs) == 1:
+        where = "two processes on ONE GPU through IPC-mapped packet buffers: a shared-device figure, not an xGMI latency"
+    elif len(devs) == 2:
+        where = f"two processes on GPUs {devs} through IPC-mapped peer packet buffers: one xGMI hop"
+    else:
+        where = "not measured: " + str(hp.get("error", "no host-proxy ranks"))[-200:]
+    return {"ll16_pingpong_us": (pp.get("ll16") or {}).get("us_per_iter"),
+            "ll8_pingpong_us": (pp.get("ll8") or {}).get("us_per_iter"),
+            "pingpong_correct": hp.get("pingpong_correct"),
+            "pingpong_devices": devs,
+            "pingpong_note": "us per one-way hand-off of 1024 ints (100k timed iterations, 1 workgroup per rank), "
+                             + where}
+
+
 def staged_rate(m, S, x, y, out, pk, flags, err, reps=10):
     """IB/proxy staging: buckets start and end in host-pinned memory, so time H2D(x, y) + kernel + D2H(out)."""
     hx = torch.empty(x.numel(), dtype=x.dtype).pin_memory()
@@ -329,18 +350,7 @@ def bench_single(args):
         res["host_proxy_baseline"] = hp
         # the reference's MemoryChannel packet ping-pong latency (memory_channel_tests.cu:98-107), from
         # the same two host-proxy ranks: on a 1-GPU box both ranks share the GPU
-        pp = (hp or {}).get("pingpong") or {}
-        devs = (hp or {}).get("devices") or []
-        where = ("two processes on ONE GPU through IPC-mapped packet buffers: a shared-device figure, not an "
-                 "xGMI latency" if len(devs) == 1 else
-                 f"two processes on GPUs {devs} through IPC-mapped peer packet buffers: one xGMI hop")
-        res["extras"] = {
-            "ll16_pingpong_us": pp.get("ll16", {}).get("us_per_iter"),
-            "ll8_pingpong_us": pp.get("ll8", {}).get("us_per_iter"),
-            "pingpong_correct": (hp or {}).get("pingpong_correct"),
-            "pingpong_devices": devs,
-            "pingpong_note": "us per one-way hand-off of 1024 ints (100k timed iterations, 1 workgroup per rank), "
-                             + where}
+        res["extras"] = pingpong_extras(hp)
     pk.free()
     return res
 

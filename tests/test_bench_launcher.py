@@ -309,3 +309,20 @@ def test_extras_check_every_timed_size():
     extra_false = {"correct_bitexact": dict(ok["correct_bitexact"], **{"crossover:4KiB:packet:0x0": False})}
     assert not bench.extras_correct(extra_false, True)
     assert bench.ll16_ceiling(8) == pytest.approx(307.2)
+
+
+def test_pingpong_extras_labels():
+    """The N=1 line's ping-pong extras: the two host-proxy ranks' LL16 / LL8
+    latencies, labelled a shared-device figure on a 1-GPU box and one xGMI hop on a node; a failed
+    host-proxy run leaves them null with the reason, never an exception."""
+    import bench
+
+    pp = {"ll16": {"us_per_iter": 2.6, "correct": True}, "ll8": {"us_per_iter": 2.4, "correct": True}}
+    one = bench.pingpong_extras({"pingpong": pp, "pingpong_correct": True, "devices": [0]})
+    assert one["ll16_pingpong_us"] == 2.6 and one["ll8_pingpong_us"] == 2.4 and one["pingpong_correct"] is True
+    assert "shared-device" in one["pingpong_note"]
+    two = bench.pingpong_extras({"pingpong": pp, "pingpong_correct": True, "devices": [0, 1]})
+    assert "xGMI hop" in two["pingpong_note"] and two["pingpong_devices"] == [0, 1]
+    bad = bench.pingpong_extras({"error": "boom"})
+    assert bad["ll16_pingpong_us"] is None and "boom" in bad["pingpong_note"]
+    assert bench.pingpong_extras(None)["ll8_pingpong_us"] is None
