@@ -210,6 +210,7 @@ static int pairWorker(int myRank, const std::string& ipPort) {
   const int remoteRank = myRank ^ 1, nRanks = 2;
   const mscclpp::Transport transport = mscclpp::Transport::CudaIpc;
   const size_t copyBytes = 1 << 20, n = copyBytes / sizeof(int);
+  const size_t maxBytes = (size_t)128 << 20;  // the tutorial's largest size (bidir_memory_channel.cu:173)
 
   auto bootstrap = std::make_shared<mscclpp::TcpBootstrap>(myRank, nRanks);
   bootstrap->initialize(ipPort);
@@ -217,9 +218,9 @@ static int pairWorker(int myRank, const std::string& ipPort) {
   auto conn = comm.connect({transport, {mscclpp::DeviceType::GPU, gpuId}}, remoteRank).get();
   auto sema = comm.buildSemaphore(conn, remoteRank).get();
 
-  mscclpp::GpuBuffer buffer(2 * copyBytes);
-  mscclpp::GpuBuffer pktBuffer(4 * copyBytes);
-  CHECK(buffer.bytes() == 2 * copyBytes && buffer.deviceId() == gpuId);
+  mscclpp::GpuBuffer buffer(2 * maxBytes);
+  mscclpp::GpuBuffer pktBuffer(4 * maxBytes);
+  CHECK(buffer.bytes() == 2 * maxBytes && buffer.deviceId() == gpuId);
   auto localRegMem = comm.registerMemory(buffer.data(), buffer.bytes(), transport);
   auto localPktRegMem = comm.registerMemory(pktBuffer.data(), pktBuffer.bytes(), transport);
   comm.sendMemory(localRegMem, remoteRank);
@@ -282,6 +283,55 @@ static int pairWorker(int myRank, const std::string& ipPort) {
     MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
     bootstrap->barrier();
     expectAt(myRank, remoteRank, 10 + (int)flag, "putPackets/unpackPackets");
+  }
+
+  // the tutorial's timing (bidir_memory_channel.cu:170-210): 1000 graph-captured launches per kernel
+  // and size, one event pair on rank 0, its own log line; packet flags keep counting from 4, one per
+  // captured launch.  (This get kernel ends with one more signal / wait than the tutorial's, so the
+  // peer never overwrites what a rank still reads; its rows carry that extra round trip.)
+  const int iter = 1000;
+  uint32_t flag = 4;
+  for (int k = 0; k < 3; ++k) {
+    const char* name = k == 0 ? "Bidir Put" : k == 1 ? "Bidir Get" : "Bidir Put Packets";
+    for (size_t bytes : {(size_t)1024, (size_t)1 << 20, maxBytes}) {
+      hipGraph_t graph;
+      hipGraphExec_t exec;
+      MSCCLPP_CUDATHROW(hipStreamBeginCapture(stream, hipStreamCaptureModeGlobal));
+      for (int i = 0; i < iter; ++i) {
+        if (k == 0)
+          hipLaunchKernelGGL(bidirPutKernel, dim3(32), dim3(1024), 0, stream, dh.get(), bytes, myRank);
+        else if (k == 1)
+          hipLaunchKernelGGL(bidirGetKernel, dim3(32), dim3(1024), 0, stream, dh.get(), bytes, myRank);
+        else
+          hipLaunchKernelGGL(bidirPutPacketKernel, dim3(32), dim3(1024), 0, stream, dhp.get(), bytes, myRank, flag++);
+      }
+      MSCCLPP_CUDATHROW(hipStreamEndCapture(stream, &graph));
+      MSCCLPP_CUDATHROW(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      MSCCLPP_CUDATHROW(hipDeviceSynchronize());
+      bootstrap->barrier();
+      hipEvent_t t0, t1;
+      MSCCLPP_CUDATHROW(hipEventCreate(&t0));
+      MSCCLPP_CUDATHROW(hipEventCreate(&t1));
+      MSCCLPP_CUDATHROW(hipEventRecord(t0, stream));
+      MSCCLPP_CUDATHROW(hipGraphLaunch(exec, stream));
+      MSCCLPP_CUDATHROW(hipEventRecord(t1, stream));
+      MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+      if (myRank == 0) {
+        float ms = 0;
+        MSCCLPP_CUDATHROW(hipEventElapsedTime(&ms, t0, t1));
+        const float per = ms / iter;
+        std::printf("Rank %d (GPU %d): [%s] bytes %zu, elapsed %g ms/iter, BW %g GB/s\n", myRank, gpuId, name, bytes,
+                    per, (float)bytes / per * 1e-6f);
+        std::printf("PAIR_JSON {\"kernel\": \"%s\", \"bytes\": %zu, \"us_per_iter\": %.3f, \"GBs\": %.3f}\n", name,
+                    bytes, per * 1e3, (float)bytes / per * 1e-6f);
+        std::fflush(stdout);
+      }
+      MSCCLPP_CUDATHROW(hipEventDestroy(t0));
+      MSCCLPP_CUDATHROW(hipEventDestroy(t1));
+      MSCCLPP_CUDATHROW(hipGraphExecDestroy(exec));
+      MSCCLPP_CUDATHROW(hipGraphDestroy(graph));
+      bootstrap->barrier();
+    }
   }
   MSCCLPP_CUDATHROW(hipStreamDestroy(stream));
   bootstrap->barrier();

@@ -40,8 +40,17 @@ def test_port_channel_loopback_one_rank(built):
 
 
 def test_memory_channel_tutorial_ip_port(built):
-    out = _run(["pair", str(_free_port())])
+    """examples/tutorials/03-memory-channel: put, get and putPackets/unpackPackets between two processes
+    meeting at "ip:port", exact; then the tutorial's timing -- 1000 graph-captured launches per kernel
+    at 1 KiB, 1 MiB and 128 MiB with its own log line (docs/tutorials/03-memory-channel.md:26-34
+    publishes 344.8 GB/s put, 321.5 get, 131.7 put-packets at 128 MiB)."""
+    out = _run(["pair", str(_free_port())], timeout=180)
     assert "rank 0 pair OK" in out and "rank 1 pair OK" in out and "pair OK" in out
+    rows = [json.loads(x.split(" ", 1)[1]) for x in out.splitlines() if x.startswith("PAIR_JSON ")]
+    assert [(r["kernel"], r["bytes"]) for r in rows] == [
+        (k, b) for k in ("Bidir Put", "Bidir Get", "Bidir Put Packets") for b in (1024, 1 << 20, 128 << 20)], out
+    assert all(r["us_per_iter"] > 0 for r in rows), rows
+    print([x for x in out.splitlines() if "[Bidir" in x])
 
 
 def test_port_channel_tutorial_graph_replays(built):
