@@ -371,16 +371,7 @@ RegisteredMemory RegisteredMemory::deserialize(const std::vector<char>& data) {
 }
 
 // ---- Connection --------------------------------------------------------------------------------------
-// CudaIpcConnection (connection.cc:85-195): copies on a non-blocking stream of this GPU.  Token
-// values of updateAndSync are staged in a pinned ring, one slot per value (HIP reads a pinned source
-// when the copy runs, not when it is queued, so one shared word could publish a later value early);
-// a slot is reused only after a stream synchronize retired the copies of the previous lap.
-// The copy stream of a communicator's connections.  One stream for all of them (the reference's CUDA
-// branch, connection.cc:126-130), not one per connection (its HIP branch): HIP multiplexes a
-// process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues, and a connection stream that lands
-// on the queue of a kernel spinning for that connection's data never runs -- the PortChannel
-// all-to-all hung with 4 ranks on one GPU.
-// The connections' copy stream.  MSCCLPP_AMD_COPY_STREAM_PRIORITY=high creates it at the device's
+// Creating the connections' copy stream: MSCCLPP_AMD_COPY_STREAM_PRIORITY=high creates it at the device's
 // greatest stream priority (an A/B of DESIGN.md §9: whether the hardware scheduler then picks the
 // proxy's copies up sooner while other processes' kernels hold the GPU); default: normal priority.
 static hipError_t createCopyStream(hipStream_t* s) {
@@ -395,6 +386,15 @@ static hipError_t createCopyStream(hipStream_t* s) {
   return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
 }
 
+// CudaIpcConnection (connection.cc:85-195): copies on a non-blocking stream of this GPU.  Token
+// values of updateAndSync are staged in a pinned ring, one slot per value (HIP reads a pinned source
+// when the copy runs, not when it is queued, so one shared word could publish a later value early);
+// a slot is reused only after a stream synchronize retired the copies of the previous lap.
+// The copy stream of a communicator's connections.  One stream for all of them (the reference's CUDA
+// branch, connection.cc:126-130), not one per connection (its HIP branch): HIP multiplexes a
+// process's streams onto GPU_MAX_HW_QUEUES (4) hardware queues, and a connection stream that lands
+// on the queue of a kernel spinning for that connection's data never runs -- the PortChannel
+// all-to-all hung with 4 ranks on one GPU.
 struct SharedCopyStream {
   hipStream_t stream = nullptr;
   ~SharedCopyStream() {
@@ -838,7 +838,12 @@ Host2DeviceSemaphore::Host2DeviceSemaphore(const Semaphore& semaphore, uint64_t 
     : semaphore_(semaphore) {
   if (!semaphore.valid()) throw Error("Host2DeviceSemaphore: empty Semaphore", ErrorCode::InvalidUsage);
   gpuCheck(hipMalloc((void**)&expectedInboundToken_, sizeof(uint64_t)), "hipMalloc");
-  memsetSync(expectedInboundToken_, 0, sizeof(uint64_t));
+  try {
+    memsetSync(expectedInboundToken_, 0, sizeof(uint64_t));
+  } catch (...) {  // the destructor does not run for a throwing constructor
+    (void)hipFree(expectedInboundToken_);
+    throw;
+  }
   budget_ = budget ? budget : semaphore.pimpl()->budget;
   err_ = err ? err : semaphore.pimpl()->err;
 }
@@ -869,7 +874,12 @@ MemoryDevice2DeviceSemaphore::MemoryDevice2DeviceSemaphore(const Semaphore& sema
     : semaphore_(semaphore) {
   if (!semaphore.valid()) throw Error("MemoryDevice2DeviceSemaphore: empty Semaphore", ErrorCode::InvalidUsage);
   gpuCheck(hipMalloc((void**)&expectedInboundToken_, sizeof(uint64_t)), "hipMalloc");
-  memsetSync(expectedInboundToken_, 0, sizeof(uint64_t));
+  try {
+    memsetSync(expectedInboundToken_, 0, sizeof(uint64_t));
+  } catch (...) {  // the destructor does not run for a throwing constructor
+    (void)hipFree(expectedInboundToken_);
+    throw;
+  }
   budget_ = budget ? budget : semaphore.pimpl()->budget;
   err_ = err ? err : semaphore.pimpl()->err;
 }
