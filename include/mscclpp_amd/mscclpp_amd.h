@@ -280,7 +280,10 @@ int mscclppAmdLaunchPortChannelPut(void* chans, int nchans, const uint64_t* dstO
                                    uint64_t chunk, int mode, void* stream);
 
 /* MemoryChannel device-surface self-test on one GPU (two in-process ranks): mode 0 LL16 packet
- * ping-pong, 1 LL8 ping-pong, 2 put + signal/wait round trip.  *failures = mismatching words. */
+ * ping-pong, 1 LL8 ping-pong, 2 put + signal/wait round trip.  *failures = mismatching words.
+ * Modes 3 / 4: rank 0 unpacks LL16 / LL8 packets of flag 7 that rank 1 never puts; the wait ends at
+ * a 20 ms budget and devErr[0..3] (4 words) receives the error record (code, flag, packet byte,
+ * flag seen). */
 int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int* failures, uint32_t* devErr);
 /* put, get and putPackets + unpackPackets (LL16, LL8) of `bytes` (multiple of 16, meant to exceed
  * 4 GiB) on one GPU, nblocks x 256 lanes as one thread group; bad[0..3] = words that differ from the

@@ -17,6 +17,17 @@ __global__ void memChanSelfTestKernel(MemoryChannelDeviceHandle* chans, int* b0,
   int* sendBuff = rank == 0 ? b0 : b1;
   const int putOffset = rank == 0 ? 0 : 10000000;
   const int getOffset = rank == 0 ? 10000000 : 0;
+  if (mode == 3 || mode == 4) {
+    // a packet that never comes: rank 0 unpacks LL16 (mode 3) / LL8 (mode 4) packets of flag 7 that
+    // rank 1 never puts; the wait ends at the handle's budget with the error record filled in
+    if (rank == 0) {
+      if (mode == 3)
+        ch.unpackPackets<LL16Packet>(0, 0, nElem * sizeof(int), threadIdx.x, blockDim.x, 7u);
+      else
+        ch.unpackPackets<LL8Packet>(0, 0, nElem * sizeof(int), threadIdx.x, blockDim.x, 7u);
+    }
+    return;
+  }
   if (mode <= 1) {
     for (int i = 0; i < nTries; ++i) {
       const uint32_t flag = (uint32_t)i + 1;
@@ -217,9 +228,10 @@ extern "C" int mscclppAmdLaunchMemChannelPingPong(const void* handle, int* buff,
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-// Returns 0 on success, the mismatch count in *failures, any device error code in *devErr.
+// Returns 0 on success, the mismatch count in *failures, any device error code in *devErr.  Modes 3
+// and 4 (a packet that never arrives, LL16 / LL8) copy the whole error record into devErr[0..3].
 extern "C" int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int* failures, uint32_t* devErr) {
-  if (!failures || !devErr || nElem <= 0 || nElem % 2 || mode < 0 || mode > 2) return 4;
+  if (!failures || !devErr || nElem <= 0 || nElem % 2 || mode < 0 || mode > 4) return 4;
   const size_t bytes = (size_t)nElem * 4;
   int *b[2] = {nullptr, nullptr}, *ret = nullptr;
   void* pk[2] = {nullptr, nullptr};
@@ -250,9 +262,9 @@ extern "C" int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int
     MemoryChannelDeviceHandle h[2];
     for (int r = 0; r < 2; ++r) {
       const int p = 1 - r;
-      h[r].semaphore_ = {tok + r, tok + p, exp + r, 200000000ull /* 2 s */, err};
+      h[r].semaphore_ = {tok + r, tok + p, exp + r, mode >= 3 ? 2000000ull /* 20 ms */ : 200000000ull /* 2 s */, err};
       // packet modes: dst_ = peer's packet buffer; mode 2: dst_ = peer's data buffer
-      h[r].dst_ = mode <= 1 ? pk[p] : (void*)b[p];
+      h[r].dst_ = mode != 2 ? pk[p] : (void*)b[p];
       h[r].src_ = b[r];
       h[r].packetBuffer_ = pk[r];
     }
@@ -263,7 +275,7 @@ extern "C" int mscclppAmdMemChannelSelfTest(int mode, int nElem, int nTries, int
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(failures, ret, 4, hipMemcpyDeviceToHost));
-  CK(hipMemcpy(devErr, err, 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(devErr, err, mode >= 3 ? 16 : 4, hipMemcpyDeviceToHost));
 done:
 #undef CK
   for (int r = 0; r < 2; ++r) {
