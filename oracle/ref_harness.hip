@@ -233,19 +233,86 @@ struct RefBench2 {
 
 // One stream per rank for the process's life (so cases do not churn hardware queues), each made to
 // own its queue before the first real launch (a queue is created at a stream's first submission);
-// plus a stream for diagnostics that never waits behind a spinning rank.
+// plus a stream for diagnostics that never waits behind a spinning rank, and the pinned words it
+// copies into (allocated here, never freed: hipHostFree synchronizes the device, which waits forever
+// behind a rank that spins).
 static hipStream_t gRankStream[8];
 static hipStream_t gDiagStream;
+static uint64_t* gDiagPinned;
+static uint32_t* gMeet;  // uncached device words: [0, 8) arrivals, [8, 16) met
+static uint32_t gMeetGen;
+static int gStreamRecreations;
 
-static bool rankStreams() {
-  if (gDiagStream) return true;
+static bool createRankStreams() {
   for (auto& s : gRankStream) {
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return false;
     hipLaunchKernelGGL((refReduceKernel<3, 0>), dim3(1), dim3(64), 0, s, nullptr, nullptr, (size_t)0);
     if (hipGetLastError() != hipSuccess) return false;
   }
+  for (auto& s : gRankStream)
+    if (hipStreamSynchronize(s) != hipSuccess) return false;
+  return true;
+}
+
+static bool rankStreams() {
+  if (gDiagStream) return true;
+  if (!createRankStreams()) return false;
+  if (hipHostMalloc(reinterpret_cast<void**>(&gDiagPinned), sizeof(uint64_t) * 8, hipHostMallocDefault) !=
+          hipSuccess ||
+      hipExtMallocWithFlags(reinterpret_cast<void**>(&gMeet), 16 * sizeof(uint32_t), hipDeviceMallocUncached) !=
+          hipSuccess ||
+      hipMemset(gMeet, 0, 16 * sizeof(uint32_t)) != hipSuccess)
+    return false;
   if (hipStreamCreateWithFlags(&gDiagStream, hipStreamNonBlocking) != hipSuccess) return false;
   return hipDeviceSynchronize() == hipSuccess;
+}
+
+// The precondition of every launch below: the n ranks spin on each other, so their kernels must run
+// at the same time, which two streams behind one hardware queue cannot (the second waits for the
+// first to finish).  Each rank stream runs a one-wave kernel that announces itself and waits, at most
+// `budget` ticks of the 100 MHz clock, until all n have; met[r] = 1 if it saw them all.
+__global__ void refStreamsMeetKernel(uint32_t* meet, int r, int n, uint32_t gen, uint64_t budget) {
+  if (threadIdx.x != 0) return;
+  __hip_atomic_store(meet + r, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool all = false;
+  while (!all && __builtin_amdgcn_s_memrealtime() - t0 < budget) {
+    all = true;
+    for (int q = 0; q < n; ++q)
+      all = all && __hip_atomic_load(meet + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == gen;
+    if (!all) __builtin_amdgcn_s_sleep(2);
+  }
+  __hip_atomic_store(meet + 8 + r, all ? 1u : 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// 0 if rank streams 0 .. n-1 ran the meet kernel concurrently, 5 if not, 1 on a HIP error.  Every
+// meet kernel ends by itself (100 ms budget), so this never leaves anything spinning.
+static int streamsMeet(int n) {
+  const uint32_t gen = ++gMeetGen;
+  for (int r = 0; r < n; ++r) {
+    hipLaunchKernelGGL(refStreamsMeetKernel, dim3(1), dim3(64), 0, gRankStream[r], gMeet, r, n, gen,
+                       (uint64_t)10000000);
+    if (hipGetLastError() != hipSuccess) return 1;
+  }
+  for (int r = 0; r < n; ++r)
+    if (hipStreamSynchronize(gRankStream[r]) != hipSuccess) return 1;
+  uint32_t met[8] = {};
+  if (hipMemcpy(met, gMeet + 8, sizeof(uint32_t) * n, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  for (int r = 0; r < n; ++r)
+    if (met[r] != 1) return 5;
+  return 0;
+}
+
+// streamsMeet, and on a failure fresh rank streams (new queues) and again, twice at most.
+static int ensureConcurrent(int n) {
+  int rc = streamsMeet(n);
+  for (int k = 0; k < 2 && rc == 5; ++k) {
+    for (auto& s : gRankStream) (void)hipStreamDestroy(s);
+    if (!createRankStreams()) return 1;
+    ++gStreamRecreations;
+    rc = streamsMeet(n);
+  }
+  return rc;
 }
 
 void refBench2Close(void* handle);
@@ -295,10 +362,8 @@ void* refBench2Open(const char* hsaco, int n) { return refBench2OpenTyped(hsaco,
 // read on the diagnostic stream while the others may still spin.  0 on success.
 int refBench2Diag(void* handle, int* done, uint64_t* flags) {
   auto* h = static_cast<RefBench2*>(handle);
-  if (!h) return 1;
-  uint64_t* pinned = nullptr;
-  if (hipHostMalloc(reinterpret_cast<void**>(&pinned), sizeof(uint64_t) * h->n, hipHostMallocDefault) != hipSuccess)
-    return 1;
+  if (!h || !gDiagPinned) return 1;
+  uint64_t* pinned = gDiagPinned;
   int rc = 0;
   for (int r = 0; r < h->n && rc == 0; ++r) {
     done[r] = hipStreamQuery(gRankStream[r]) == hipSuccess;
@@ -318,9 +383,32 @@ int refBench2Diag(void* handle, int* done, uint64_t* flags) {
   }
   if (rc == 0)
     for (int r = 0; r < h->n; ++r) flags[r] = pinned[r];
-  if (rc != 2) (void)hipHostFree(pinned);  // a copy still in flight keeps its target
   return rc;
 }
+
+// After a timeout: lets spinning ranks finish before the process leaves, by filling the words they
+// wait on from the diagnostic stream -- every 32-bit word of ptrs[0 .. nptr) := value (for allreduce2
+// the packet scratch and the call's flag, so every flag word matches; for allreduce1 the inbound
+// tokens and 0x7fffffff, above any expected count).  0 if rank streams 0 .. n-1 then drain within
+// timeoutMs, 2 if not.  The data the ranks then produce is garbage; the caller reports the timeout.
+int refReleaseSpin(void* const* ptrs, int nptr, uint64_t words, uint32_t value, int n, int timeoutMs) {
+  if (!gDiagStream || n < 1 || n > 8) return 1;
+  for (int k = 0; k < nptr; ++k)
+    if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ptrs[k]), (int)value, words, gDiagStream) != hipSuccess)
+      return 1;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int r = 0; r < n;) {
+    if (hipStreamQuery(gRankStream[r]) != hipErrorNotReady) {
+      ++r;
+      continue;
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeoutMs)) return 2;
+  }
+  return 0;
+}
+
+// How many times ensureConcurrent replaced the rank streams in this process.
+int refStreamRecreations() { return gStreamRecreations; }
 
 // Packet scratch the way the reference allocates it on AMD (GpuBuffer -> hipExtMallocWithFlags with
 // hipDeviceMallocUncached, src/core/gpu_utils.cc): the ranks' kernels run on different XCDs, whose
@@ -350,7 +438,8 @@ void refBench2Close(void* handle) {
 // One AllReduce call on every rank.  bufs/scratch/results: n device pointers each (scratch zeroed by
 // the caller before the first call, 4 * nelems / 2 LL16 packets); nelems ints per rank.  Returns 0,
 // 4 on a shape the kernel cannot take (it would index past its channel array or split a packet), 1 on
-// a HIP error, 2 if the ranks have not finished after timeoutMs.
+// a HIP error, 2 if the ranks have not finished after timeoutMs, 5 (nothing launched) if the rank
+// streams could not run kernels concurrently even on fresh streams (ensureConcurrent).
 int refBench2Run(void* handle, void* const* bufs, void* const* scratch, void* const* results, uint64_t nelems,
                  int blocksPerPeer, int threads, int timeoutMs) {
   auto* h = static_cast<RefBench2*>(handle);
@@ -371,6 +460,7 @@ int refBench2Run(void* handle, void* const* bufs, void* const* scratch, void* co
     if (hipMemcpy(h->chans[r], hc.data(), sizeof(hc[0]) * nPeers, hipMemcpyHostToDevice) != hipSuccess) return 1;
   }
   if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (const int mc = ensureConcurrent(n)) return mc;
   for (int r = 0; r < n; ++r) {
     MemoryChannelDeviceHandle* c = h->chans[r];
     void* buff = bufs[r];
@@ -427,6 +517,7 @@ int refBench1Run(void* handle, void* const* bufs, void* const* tokens, void* con
     if (hipMemcpy(h->chans[r], hc.data(), sizeof(hc[0]) * nPeers, hipMemcpyHostToDevice) != hipSuccess) return 1;
   }
   if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (const int mc = ensureConcurrent(n)) return mc;
   for (int r = 0; r < n; ++r) {
     MemoryChannelDeviceHandle* c = h->chans[r];
     void* buff = bufs[r];

@@ -43,11 +43,36 @@ def _lib():
     L.refMallocUncached.argtypes = [ctypes.c_uint64]
     L.refMallocUncached.restype = vp
     L.refFree.argtypes = [vp]
+    L.refReleaseSpin.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+    L.refReleaseSpin.restype = ctypes.c_int
+    L.refStreamRecreations.restype = ctypes.c_int
     return L
 
 
 def _ptrs(ts):
     return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+
+def _check_run(L, rc, rec, call, n, wait_ptrs, words, value, h=None):
+    """rc of refBench2Run / refBench1Run.  5: the n rank streams could not run kernels at the same time
+    (nothing was launched) -- exit 4, the test skips.  2: ranks still spinning after the run's timeout --
+    report which (allreduce2: done flags and globalFlag, read on the diagnostic stream), fill the words
+    they wait on (wait_ptrs, `words` 32-bit words each, := value) so they finish, and exit 3."""
+    if rc == 5:
+        print(json.dumps({"streams_not_concurrent": rec, "call": call,
+                          "recreations": L.refStreamRecreations()}), flush=True)
+        os._exit(4)
+    if rc == 2:
+        diag = {"timeout": rec, "call": call}
+        if h is not None:
+            done, flags = (ctypes.c_int * n)(), (ctypes.c_uint64 * n)()
+            diag["diag_rc"] = L.refBench2Diag(h, done, flags)
+            diag["done"], diag["globalFlag"] = list(done), list(flags)
+        print(json.dumps(diag), flush=True)
+        arr = (ctypes.c_void_p * len(wait_ptrs))(*wait_ptrs)
+        print(json.dumps({"release_rc": L.refReleaseSpin(arr, len(wait_ptrs), words, value, n, 5000)}), flush=True)
+        os._exit(3)
+    assert rc == 0, f"reference run returned {rc}"
 
 
 def run_case(L, m, n, count, blocks_per_peer, threads):
@@ -70,16 +95,7 @@ def run_case(L, m, n, count, blocks_per_peer, threads):
             rout = [torch.zeros_like(d) for d in dins]
             torch.cuda.synchronize()
             rc = L.refBench2Run(h, _ptrs(dins), _ptrs(rscr), _ptrs(rout), count, blocks_per_peer, threads, 20000)
-            if rc == 2:  # ranks still spinning: say which and with what flag, then leave without waiting
-                done, flags = (ctypes.c_int * n)(), (ctypes.c_uint64 * n)()
-                drc = L.refBench2Diag(h, done, flags)
-                print(json.dumps({"timeout": rec, "call": call, "diag_rc": drc, "done": list(done),
-                                  "globalFlag": list(flags)}), flush=True)
-                import subprocess
-                ps = subprocess.run(["ps", "-eo", "pid,ppid,etimes,stat,cmd"], stdout=subprocess.PIPE, text=True)
-                print("\n".join(x[:200] for x in ps.stdout.splitlines() if "python" in x or "PID" in x), flush=True)
-                os._exit(3)
-            assert rc == 0, f"refBench2Run returned {rc}"
+            _check_run(L, rc, rec, call, n, rptr, sb // 4, flag, h)
             douts = [torch.zeros_like(d) for d in dins]
             ours.all_reduce(dins, douts, m.ALGO_TEST_K6)
             torch.cuda.synchronize()
@@ -183,10 +199,7 @@ def run_typed_case(L, kind, n, nwords, blocks_per_peer, threads):
             rout = [torch.zeros_like(d) for d in dins]
             torch.cuda.synchronize()
             rc = L.refBench2Run(h, _ptrs(dins), _ptrs(rscr), _ptrs(rout), nwords, blocks_per_peer, threads, 20000)
-            if rc == 2:
-                print(json.dumps({"timeout": rec, "call": call}), flush=True)
-                os._exit(3)
-            assert rc == 0, f"refBench2Run returned {rc}"
+            _check_run(L, rc, rec, call, n, rptr, sb // 4, flag, h)
             douts = [torch.zeros_like(d) for d in dins]
             ours.all_reduce([d.view(tdt) for d in dins], [o.view(tdt) for o in douts], m.ALGO_TEST_K6)
             torch.cuda.synchronize()
@@ -267,10 +280,7 @@ def run_bench1_case(L, kind, n, nwords, nblocks, threads, read_only):
                 v.copy_(torch.from_numpy(a.view(np.int32).copy()))
             torch.cuda.synchronize()
             rc = L.refBench1Run(h, arr(bufs), arr(toks), arr(exps), nwords, nblocks, threads, read_only, 20000)
-            if rc == 2:
-                print(json.dumps({"timeout": rec, "call": call}), flush=True)
-                os._exit(3)
-            assert rc == 0, f"refBench1Run returned {rc}"
+            _check_run(L, rc, rec, call, n, toks, 2 * (n - 1), 0x7FFFFFFF)
             exp = O.bench_allreduce1(dtype, ins, nwords)
             alt, _ = O.bench_allreduce2(dtype, ins, nwords, 1, 32 * nwords, order=0)
             for r in range(n):
@@ -297,8 +307,13 @@ def main():
     cases = json.loads(sys.argv[1])
     typed = json.loads(sys.argv[2]) if len(sys.argv) > 2 else []
     bench1 = json.loads(sys.argv[3]) if len(sys.argv) > 3 else []
+    import faulthandler
+
     import mscclpp_amd as m
 
+    # a wedge anywhere else (a synchronize, an allocation) names its Python frame before the test's
+    # 150 s timeout kills this process
+    faulthandler.dump_traceback_later(120, exit=False)
     torch.cuda.set_device(0)
     L = _lib()
     for n, count, bpp, threads in cases:
@@ -307,6 +322,8 @@ def main():
         print(json.dumps(run_typed_case(L, kind, n, nwords, bpp, threads)), flush=True)
     for kind, n, nwords, nblocks, threads, read_only in bench1:
         print(json.dumps(run_bench1_case(L, kind, n, nwords, nblocks, threads, read_only)), flush=True)
+    faulthandler.cancel_dump_traceback_later()
+    print(f"STREAM RECREATIONS {L.refStreamRecreations()}", flush=True)
     print("WORKER OK", flush=True)
 
 
