@@ -28,13 +28,28 @@ int mscclppAmdMemChannelPingPong(ncclComm_t comm, int nElem, int iters, int ll8,
     if (comm->nranks != 2) return (int)ncclInvalidArgument;
     const int rank = comm->rank, peer = 1 - rank;
     const size_t bytes = (size_t)nElem * 4;
-    int* buff = (int*)allocUncached(bytes);         // GpuBuffer on AMD: uncached (gpu_utils.cc:139-147)
-    void* pkt = allocUncached(bytes * 2);           // LL16: nElem / 2 16-byte packets; LL8: nElem 8-byte
-    int* ret = nullptr;
-    HIPCHECK(hipMalloc((void**)&ret, sizeof(int)));
+    // released on every exit, a throw from the setup or a launch included
+    struct Resources {
+      int* buff = nullptr;
+      void* pkt = nullptr;
+      int* ret = nullptr;
+      hipStream_t st = nullptr;
+      ~Resources() {
+        if (st) (void)hipStreamDestroy(st);
+        if (ret) (void)hipFree(ret);
+        if (pkt) releaseUncached(pkt, nullptr);
+        if (buff) releaseUncached(buff, nullptr);
+      }
+    } res;
+    res.buff = (int*)allocUncached(bytes);  // GpuBuffer on AMD: uncached (gpu_utils.cc:139-147)
+    res.pkt = allocUncached(bytes * 2);     // LL16: nElem / 2 16-byte packets; LL8: nElem 8-byte
+    HIPCHECK(hipMalloc((void**)&res.ret, sizeof(int)));
+    HIPCHECK(hipStreamCreateWithFlags(&res.st, hipStreamNonBlocking));
+    int* const buff = res.buff;
+    void* const pkt = res.pkt;
+    int* const ret = res.ret;
+    const hipStream_t st = res.st;
     memsetSync(ret, 0, sizeof(int));
-    hipStream_t st = nullptr;
-    HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     double us = 0;
     int bad = 0;
     uint32_t rec[4] = {0, 0, 0, 0};
@@ -65,10 +80,6 @@ int mscclppAmdMemChannelPingPong(ncclComm_t comm, int nElem, int iters, int ll8,
       HIPCHECK(hipMemcpy(rec, comm->err, sizeof(rec), hipMemcpyDeviceToHost));
       comm->boot->barrier();  // the peer is done with my packet buffer before its mapping closes
     }
-    (void)hipStreamDestroy(st);
-    (void)hipFree(ret);
-    releaseUncached(pkt, nullptr);
-    releaseUncached(buff, nullptr);
     out[0] = us;
     out[1] = (bad == 0 && rec[0] == 0) ? 1.0 : 0.0;
     for (int k = 0; k < 4 && 2 + k < outLen; ++k) out[2 + k] = (double)rec[k];
