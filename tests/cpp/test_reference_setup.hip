@@ -28,14 +28,20 @@
 //               three calls each on fresh inputs whose sums are exact
 // Exit status 0 and "<mode> OK" on success.
 #include <hip/hip_runtime.h>
+#include <signal.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <mscclpp/atomic_device.hpp>
@@ -197,6 +203,52 @@ __global__ void bidirPutPacketKernel(mscclpp::MemoryChannelDeviceHandle* ch, siz
   ch->unpackPackets(0, off, copyBytes, tid, blockDim.x * gridDim.x, flag);
 }
 
+// Watchdog over one timed graph of a pair rank: if the graph has not completed after `seconds`, it
+// prints what the rank's waits see -- the device error record, this module's DeviceSyncer words
+// (count, generation, timed out) and the channel's inbound / expected tokens, copied on a stream of
+// its own into pinned words allocated up front -- and ends the rank (exit 3), so a stall names its
+// wait instead of running into the test's timeout.
+struct GraphWatchdog {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  std::thread th;
+  GraphWatchdog(int rank, const char* what, size_t bytes, int seconds, hipStream_t diag, uint32_t* pinned,
+                const void* err, const void* syncer, const void* inbound, const void* expected) {
+    th = std::thread([this, rank, what, bytes, seconds, diag, pinned, err, syncer, inbound, expected] {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        if (cv.wait_for(lk, std::chrono::seconds(seconds), [this] { return done; })) return;
+      }
+      std::memset(pinned, 0xFF, 12 * sizeof(uint32_t));
+      bool ok = hipMemcpyAsync(pinned, err, 16, hipMemcpyDeviceToHost, diag) == hipSuccess &&
+                hipMemcpyAsync(pinned + 4, syncer, 12, hipMemcpyDeviceToHost, diag) == hipSuccess &&
+                hipMemcpyAsync(pinned + 8, inbound, 8, hipMemcpyDeviceToHost, diag) == hipSuccess &&
+                hipMemcpyAsync(pinned + 10, expected, 8, hipMemcpyDeviceToHost, diag) == hipSuccess;
+      const auto t0 = std::chrono::steady_clock::now();
+      while (ok && hipStreamQuery(diag) == hipErrorNotReady)
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) ok = false;
+      uint64_t in = 0, ex = 0;
+      std::memcpy(&in, pinned + 8, 8);
+      std::memcpy(&ex, pinned + 10, 8);
+      std::printf("rank %d [%s] bytes %zu: graph not done after %d s; error %u (flag %u, byte %u, seen %u); "
+                  "DeviceSyncer count %u gen %u timedOut %u; inbound token %llu, expected %llu%s\n",
+                  rank, what, bytes, seconds, pinned[0], pinned[1], pinned[2], pinned[3], pinned[4], pinned[5],
+                  pinned[6], (unsigned long long)in, (unsigned long long)ex, ok ? "" : " (diagnostic copy incomplete)");
+      std::fflush(stdout);
+      std::_Exit(3);
+    });
+  }
+  ~GraphWatchdog() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      done = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+};
+
 static std::vector<int> pattern(int rank, size_t n, int round) {
   std::vector<int> v(n);
   for (size_t i = 0; i < n; ++i) v[i] = (rank + 1) * 1000003 + (int)i * 7 + round * 31;
@@ -230,8 +282,17 @@ static int pairWorker(int myRank, const std::string& ipPort) {
   mscclpp::RegisteredMemory remoteRegMem = remoteRegMemFuture.get();
   mscclpp::RegisteredMemory remotePktRegMem = remotePktRegMemFuture.get();
 
-  mscclpp::MemoryChannel memChan(sema, /*dst*/ remoteRegMem, /*src*/ localRegMem);
-  mscclpp::MemoryChannel memPktChan(sema, /*dst*/ remotePktRegMem, /*src*/ localRegMem,
+  // Both channels on ONE MemoryDevice2DeviceSemaphore.  The tutorial builds each from the Semaphore
+  // (bidir_memory_channel.cu:128-130), and a MemoryChannel made from a Semaphore gets a device
+  // semaphore of its own (memory_channel.cc:25-27 -> semaphore.cc:216-217): two expected counters over
+  // one inbound token.  After the put / get kernels' 12,000 signals, the packet kernel's handshake
+  // then passes without waiting, and a rank that starts launch f + 1 overwrites packets its peer is
+  // still unpacking for flag f -- seen here at 128 MiB (round 6): rank 1 waiting for flag 2012 at a
+  // packet that already held 2013, rank 0 waiting for 2013.  Sharing the device semaphore (the
+  // reference's other constructor, memory_channel.cc:17-19) keeps one counter, as the tutorial means.
+  auto d2dSema = std::make_shared<mscclpp::MemoryDevice2DeviceSemaphore>(sema);
+  mscclpp::MemoryChannel memChan(d2dSema, /*dst*/ remoteRegMem, /*src*/ localRegMem);
+  mscclpp::MemoryChannel memPktChan(d2dSema, /*dst*/ remotePktRegMem, /*src*/ localRegMem,
                                     /*packetBuffer*/ localPktRegMem.data());
   auto h = memChan.deviceHandle();
   auto hp = memPktChan.deviceHandle();
@@ -291,6 +352,12 @@ static int pairWorker(int myRank, const std::string& ipPort) {
   // peer never overwrites what a rank still reads; its rows carry that extra round trip.)
   const int iter = 1000;
   uint32_t flag = 4;
+  hipStream_t diag;
+  MSCCLPP_CUDATHROW(hipStreamCreateWithFlags(&diag, hipStreamNonBlocking));
+  uint32_t* pinned = nullptr;
+  MSCCLPP_CUDATHROW(hipHostMalloc((void**)&pinned, 64, hipHostMallocDefault));
+  void* syncerAddr = nullptr;
+  MSCCLPP_CUDATHROW(hipGetSymbolAddress(&syncerAddr, HIP_SYMBOL(devSyncer)));
   for (int k = 0; k < 3; ++k) {
     const char* name = k == 0 ? "Bidir Put" : k == 1 ? "Bidir Get" : "Bidir Put Packets";
     for (size_t bytes : {(size_t)1024, (size_t)1 << 20, maxBytes}) {
@@ -315,7 +382,22 @@ static int pairWorker(int myRank, const std::string& ipPort) {
       MSCCLPP_CUDATHROW(hipEventRecord(t0, stream));
       MSCCLPP_CUDATHROW(hipGraphLaunch(exec, stream));
       MSCCLPP_CUDATHROW(hipEventRecord(t1, stream));
-      MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+      {
+        const auto& sem = (k == 2 ? hp : h).semaphore_;
+        GraphWatchdog wd(myRank, name, bytes, 60, diag, pinned, comm.deviceErrorWord(), syncerAddr, sem.inboundToken,
+                         sem.expectedInboundToken);
+        MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+      }
+      // a wait that ran out of budget in any of the 1000 launches fails the run here, naming the
+      // kernel, the size and the error record (code, flag, packet byte, flag seen)
+      uint32_t rec[4] = {0, 0, 0, 0};
+      MSCCLPP_CUDATHROW(hipMemcpy(rec, comm.deviceErrorWord(), sizeof(rec), hipMemcpyDeviceToHost));
+      if (rec[0]) {
+        std::printf("rank %d [%s] bytes %zu: device error %u (flag %u, byte %u, seen %u)\n", myRank, name, bytes,
+                    rec[0], rec[1], rec[2], rec[3]);
+        std::fflush(stdout);
+      }
+      CHECK(rec[0] == 0);
       if (myRank == 0) {
         float ms = 0;
         MSCCLPP_CUDATHROW(hipEventElapsedTime(&ms, t0, t1));
@@ -334,6 +416,8 @@ static int pairWorker(int myRank, const std::string& ipPort) {
     }
   }
   MSCCLPP_CUDATHROW(hipStreamDestroy(stream));
+  MSCCLPP_CUDATHROW(hipStreamDestroy(diag));
+  MSCCLPP_CUDATHROW(hipHostFree(pinned));
   bootstrap->barrier();
   std::printf("rank %d pair OK\n", myRank);
   std::fflush(stdout);
@@ -540,6 +624,14 @@ static int portWorker(int myRank, const std::string& ipPort) {
     MSCCLPP_CUDATHROW(hipGraphLaunch(graphExec, stream));
     MSCCLPP_CUDATHROW(hipEventRecord(end, stream));
     MSCCLPP_CUDATHROW(hipStreamSynchronize(stream));
+    uint32_t rec[4] = {0, 0, 0, 0};
+    MSCCLPP_CUDATHROW(hipMemcpy(rec, comm.deviceErrorWord(), sizeof(rec), hipMemcpyDeviceToHost));
+    if (rec[0]) {
+      std::printf("rank %d [Bidir PutWithSignal] bytes %zu: device error %u (%u, %u, %u)\n", myRank, copyBytes, rec[0],
+                  rec[1], rec[2], rec[3]);
+      std::fflush(stdout);
+    }
+    CHECK(rec[0] == 0);
     if (myRank == 0) {  // the tutorial's line (bidir_port_channel.cu:155-161)
       float ms = 0;
       MSCCLPP_CUDATHROW(hipEventElapsedTime(&ms, start, end));
@@ -624,19 +716,43 @@ static int executorWorker(int rank, mscclpp::UniqueId id, const std::string& pla
   return 0;
 }
 
+// Two ranks in forked children.  A rank that throws says where (its own line) and exits 1; the first
+// rank to fail ends the other at once (SIGKILL), which would otherwise wait out the spin budget of
+// every remaining launch of its captured graphs for a peer that is gone.
 static int forkPair(const std::function<int(int)>& worker, const char* name) {
   std::vector<pid_t> pids;
   for (int r = 0; r < 2; ++r) {
     const pid_t pid = fork();
     CHECK(pid >= 0);
-    if (pid == 0) std::_Exit(worker(r));
+    if (pid == 0) {
+      int rc = 1;
+      try {
+        rc = worker(r);
+      } catch (const std::exception& e) {
+        std::printf("rank %d %s threw: %s\n", r, name, e.what());
+      }
+      std::fflush(stdout);
+      std::_Exit(rc);
+    }
     pids.push_back(pid);
   }
-  int bad = 0;
-  for (pid_t pid : pids) {
+  int bad = 0, left = 2;
+  while (left > 0) {
     int st = 0;
-    waitpid(pid, &st, 0);
-    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) bad++;
+    const pid_t pid = waitpid(-1, &st, 0);
+    if (pid < 0) break;
+    const int r = pid == pids[0] ? 0 : pid == pids[1] ? 1 : -1;
+    if (r < 0) continue;
+    --left;
+    if (WIFEXITED(st) && WEXITSTATUS(st) == 0) continue;
+    ++bad;
+    std::printf("rank %d %s ended with %s %d\n", r, name, WIFEXITED(st) ? "exit status" : "signal",
+                WIFEXITED(st) ? WEXITSTATUS(st) : WTERMSIG(st));
+    if (left > 0) {
+      std::printf("rank %d %s: stopping rank %d\n", r, name, 1 - r);
+      (void)kill(pids[1 - r], SIGKILL);
+    }
+    std::fflush(stdout);
   }
   std::printf(bad ? "%s FAILED\n" : "%s OK\n", name);
   return bad ? 1 : 0;

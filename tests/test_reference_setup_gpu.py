@@ -19,10 +19,23 @@ EXE = os.path.join(ROOT, "tests", "bin", "test_reference_setup")
 
 def _run(args, timeout=120):
     env = dict(os.environ, MSCCLPP_AMD_SPIN_TIMEOUT_MS="5000")
-    r = subprocess.run([EXE] + args, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout,
-                       env=env)
-    assert r.returncode == 0, r.stdout[-3000:]
+    try:
+        r = subprocess.run([EXE] + args, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           timeout=timeout, env=env)
+    except subprocess.TimeoutExpired as e:  # say what the ranks printed last, not only that time ran out
+        out = e.output.decode(errors="replace") if isinstance(e.output, bytes) else (e.output or "")
+        raise AssertionError(f"{args[0]} timed out after {timeout} s; output tail:\n{out[-3000:]}\n"
+                             f"{_other_processes()}") from None
+    assert r.returncode == 0, r.stdout[-3000:] + "\n" + _other_processes()
     return r.stdout
+
+
+def _other_processes():
+    """The box's other python / test-binary processes (a leftover of an earlier test that still holds
+    the GPU shows here)."""
+    ps = subprocess.run(["ps", "-eo", "pid,ppid,etimes,stat,args"], stdout=subprocess.PIPE, text=True)
+    keep = [x[:200] for x in ps.stdout.splitlines()[1:] if any(k in x for k in ("python", "tests/bin", "tools/"))]
+    return "processes:\n" + "\n".join(keep)
 
 
 def _free_port():
