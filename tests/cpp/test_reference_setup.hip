@@ -296,6 +296,16 @@ static int pairWorker(int myRank, const std::string& ipPort) {
                                     /*packetBuffer*/ localPktRegMem.data());
   auto h = memChan.deviceHandle();
   auto hp = memPktChan.deviceHandle();
+  // the semantics above, as the reference has them: channels on one device semaphore share its
+  // expected counter; a channel made from the Semaphore itself has a counter of its own over the
+  // same inbound token
+  CHECK(h.semaphore_.expectedInboundToken == hp.semaphore_.expectedInboundToken);
+  {
+    mscclpp::MemoryChannel own(sema, remoteRegMem, localRegMem);
+    const auto ho = own.deviceHandle();
+    CHECK(ho.semaphore_.inboundToken == h.semaphore_.inboundToken);
+    CHECK(ho.semaphore_.expectedInboundToken != h.semaphore_.expectedInboundToken);
+  }
   auto dh = mscclpp::detail::gpuCallocShared<mscclpp::MemoryChannelDeviceHandle>();
   auto dhp = mscclpp::detail::gpuCallocShared<mscclpp::MemoryChannelDeviceHandle>();
   mscclpp::gpuMemcpy(dh.get(), &h, 1, hipMemcpyHostToDevice);
