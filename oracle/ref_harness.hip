@@ -353,6 +353,15 @@ void* refBench2OpenTyped(const char* hsaco, int n, int elemBytes) {
         return nullptr;
       }
   }
+  // every rank starts at the kernel's initial flag (allreduce.cu:223), written here rather than
+  // trusted to the load: ranks at different flags would wait for each other's packets forever
+  for (int r = 0; r < n; ++r) {
+    const uint64_t one = 1;
+    if (hipMemcpy(flags[r], &one, sizeof(one), hipMemcpyHostToDevice) != hipSuccess) {
+      refBench2Close(h);
+      return nullptr;
+    }
+  }
   return h;
 }
 
