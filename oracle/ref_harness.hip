@@ -11,6 +11,7 @@
 // Built by oracle/build_ref.sh into oracle/_ref/libref.so; used only by tests/.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <vector>
@@ -444,15 +445,10 @@ void refBench2Close(void* handle) {
   delete h;
 }
 
-// One AllReduce call on every rank.  bufs/scratch/results: n device pointers each (scratch zeroed by
-// the caller before the first call, 4 * nelems / 2 LL16 packets); nelems ints per rank.  Returns 0,
-// 4 on a shape the kernel cannot take (it would index past its channel array or split a packet), 1 on
-// a HIP error, 2 if the ranks have not finished after timeoutMs, 5 (nothing launched) if the rank
-// streams could not run kernels concurrently even on fresh streams (ensureConcurrent).
-int refBench2Run(void* handle, void* const* bufs, void* const* scratch, void* const* results, uint64_t nelems,
-                 int blocksPerPeer, int threads, int timeoutMs) {
-  auto* h = static_cast<RefBench2*>(handle);
-  if (!h) return 1;
+// Channel handles of allreduce2 (each rank's n - 1 channels: dst the peer's scratch, src its buffer,
+// packetBuffer its own scratch), after the shape checks.  0, 4 (shape) or 1 (HIP error).
+static int setupBench2(RefBench2* h, void* const* bufs, void* const* scratch, uint64_t nelems, int blocksPerPeer,
+                       int threads) {
   const int n = h->n, nPeers = n - 1;
   if (nelems == 0 || nelems % (2 * (uint64_t)n) != 0 || nelems > (1ull << 30) || blocksPerPeer < 1 ||
       blocksPerPeer * nPeers > 64 || threads < 64 || threads > 1024 || threads % 64 != 0)
@@ -468,20 +464,76 @@ int refBench2Run(void* handle, void* const* bufs, void* const* scratch, void* co
     }
     if (hipMemcpy(h->chans[r], hc.data(), sizeof(hc[0]) * nPeers, hipMemcpyHostToDevice) != hipSuccess) return 1;
   }
-  if (hipDeviceSynchronize() != hipSuccess) return 1;
-  if (const int mc = ensureConcurrent(n)) return mc;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
+static int launchBench2(RefBench2* h, int r, void* const* bufs, void* const* scratch, void* const* results,
+                        uint64_t nelems, int blocksPerPeer, int threads) {
+  MemoryChannelDeviceHandle* c = h->chans[r];
+  void* buff = bufs[r];
+  void* scr = scratch[r];
+  void* res = results[r];
+  int rank = r, world = h->n;
+  size_t ne = nelems * 4 / (uint64_t)h->elemBytes;  // TYPE elements
+  void* args[] = {&c, &buff, &scr, &res, &rank, &world, &ne};
+  return hipModuleLaunchKernel(h->fn[r], blocksPerPeer * (h->n - 1), 1, 1, threads, 1, 1, 0, gRankStream[r], args,
+                               nullptr) == hipSuccess
+             ? 0
+             : 1;
+}
+
+// Channel handles of allreduce1 (semaphore tokens; channel p of rank r reaches rank p < r ? p : p + 1,
+// as :200), after the shape checks.  0, 4 or 1.
+static int setupBench1(RefBench2* h, void* const* bufs, void* const* tokens, void* const* expected, uint64_t nelems,
+                       int nblocks, int threads) {
+  const int n = h->n, nPeers = n - 1;
+  if (nelems == 0 || nelems > (1ull << 30) || nblocks < 1 || nblocks > 16 || threads < 64 || threads > 1024 ||
+      threads % 64 != 0 || (uint64_t)nblocks * threads < 2 * (uint64_t)nPeers)
+    return 4;
   for (int r = 0; r < n; ++r) {
-    MemoryChannelDeviceHandle* c = h->chans[r];
-    void* buff = bufs[r];
-    void* scr = scratch[r];
-    void* res = results[r];
-    int rank = r, world = n;
-    size_t ne = nelems * 4 / (uint64_t)h->elemBytes;  // TYPE elements
-    void* args[] = {&c, &buff, &scr, &res, &rank, &world, &ne};
-    if (hipModuleLaunchKernel(h->fn[r], blocksPerPeer * nPeers, 1, 1, threads, 1, 1, 0, gRankStream[r], args,
-                              nullptr) != hipSuccess)
-      return 1;
+    std::vector<MemoryChannelDeviceHandle> hc(nPeers);
+    for (int p = 0; p < nPeers; ++p) {
+      const int remote = p < r ? p : p + 1;
+      std::memset(static_cast<void*>(&hc[p]), 0, sizeof(hc[p]));
+      hc[p].semaphore_.inboundToken = static_cast<uint64_t*>(tokens[r]) + p;
+      hc[p].semaphore_.remoteInboundToken = static_cast<uint64_t*>(tokens[remote]) + (r < remote ? r : r - 1);
+      hc[p].semaphore_.expectedInboundToken = static_cast<uint64_t*>(expected[r]) + p;
+      hc[p].dst_ = bufs[remote];
+      hc[p].src_ = bufs[r];
+      hc[p].packetBuffer_ = nullptr;
+    }
+    if (hipMemcpy(h->chans[r], hc.data(), sizeof(hc[0]) * nPeers, hipMemcpyHostToDevice) != hipSuccess) return 1;
   }
+  return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
+static int launchBench1(RefBench2* h, int r, void* const* bufs, uint64_t nelems, int nblocks, int threads,
+                        int readOnly) {
+  MemoryChannelDeviceHandle* c = h->chans[r];
+  void* buff = bufs[r];
+  int rank = r, world = h->n, ro = readOnly;
+  size_t ne = nelems * 4 / (uint64_t)h->elemBytes;  // TYPE elements
+  void* args[] = {&c, &buff, &rank, &world, &ne, &ro};
+  return hipModuleLaunchKernel(h->fn1[r], nblocks, 1, 1, threads, 1, 1, 0, gRankStream[r], args, nullptr) ==
+                 hipSuccess
+             ? 0
+             : 1;
+}
+
+// One AllReduce call on every rank.  bufs/scratch/results: n device pointers each (scratch zeroed by
+// the caller before the first call, 4 * nelems / 2 LL16 packets); nelems ints per rank.  Returns 0,
+// 4 on a shape the kernel cannot take (it would index past its channel array or split a packet), 1 on
+// a HIP error, 2 if the ranks have not finished after timeoutMs, 5 (nothing launched) if the rank
+// streams could not run kernels concurrently even on fresh streams (ensureConcurrent).
+int refBench2Run(void* handle, void* const* bufs, void* const* scratch, void* const* results, uint64_t nelems,
+                 int blocksPerPeer, int threads, int timeoutMs) {
+  auto* h = static_cast<RefBench2*>(handle);
+  if (!h) return 1;
+  const int n = h->n;
+  if (const int rc = setupBench2(h, bufs, scratch, nelems, blocksPerPeer, threads)) return rc;
+  if (const int mc = ensureConcurrent(n)) return mc;
+  for (int r = 0; r < n; ++r)
+    if (launchBench2(h, r, bufs, scratch, results, nelems, blocksPerPeer, threads)) return 1;
   const auto t0 = std::chrono::steady_clock::now();
   for (int r = 0; r < n;) {
     const hipError_t e = hipStreamQuery(gRankStream[r]);
@@ -507,36 +559,11 @@ int refBench1Run(void* handle, void* const* bufs, void* const* tokens, void* con
                  int nblocks, int threads, int readOnly, int timeoutMs) {
   auto* h = static_cast<RefBench2*>(handle);
   if (!h) return 1;
-  const int n = h->n, nPeers = n - 1;
-  if (nelems == 0 || nelems > (1ull << 30) || nblocks < 1 || nblocks > 16 || threads < 64 || threads > 1024 ||
-      threads % 64 != 0 || (uint64_t)nblocks * threads < 2 * (uint64_t)nPeers)
-    return 4;
-  for (int r = 0; r < n; ++r) {
-    std::vector<MemoryChannelDeviceHandle> hc(nPeers);
-    for (int p = 0; p < nPeers; ++p) {
-      const int remote = p < r ? p : p + 1;
-      std::memset(static_cast<void*>(&hc[p]), 0, sizeof(hc[p]));
-      hc[p].semaphore_.inboundToken = static_cast<uint64_t*>(tokens[r]) + p;
-      hc[p].semaphore_.remoteInboundToken = static_cast<uint64_t*>(tokens[remote]) + (r < remote ? r : r - 1);
-      hc[p].semaphore_.expectedInboundToken = static_cast<uint64_t*>(expected[r]) + p;
-      hc[p].dst_ = bufs[remote];
-      hc[p].src_ = bufs[r];
-      hc[p].packetBuffer_ = nullptr;
-    }
-    if (hipMemcpy(h->chans[r], hc.data(), sizeof(hc[0]) * nPeers, hipMemcpyHostToDevice) != hipSuccess) return 1;
-  }
-  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  const int n = h->n;
+  if (const int rc = setupBench1(h, bufs, tokens, expected, nelems, nblocks, threads)) return rc;
   if (const int mc = ensureConcurrent(n)) return mc;
-  for (int r = 0; r < n; ++r) {
-    MemoryChannelDeviceHandle* c = h->chans[r];
-    void* buff = bufs[r];
-    int rank = r, world = n, ro = readOnly;
-    size_t ne = nelems * 4 / (uint64_t)h->elemBytes;  // TYPE elements
-    void* args[] = {&c, &buff, &rank, &world, &ne, &ro};
-    if (hipModuleLaunchKernel(h->fn1[r], nblocks, 1, 1, threads, 1, 1, 0, gRankStream[r], args, nullptr) !=
-        hipSuccess)
-      return 1;
-  }
+  for (int r = 0; r < n; ++r)
+    if (launchBench1(h, r, bufs, nelems, nblocks, threads, readOnly)) return 1;
   const auto t0 = std::chrono::steady_clock::now();
   for (int r = 0; r < n;) {
     const hipError_t e = hipStreamQuery(gRankStream[r]);
