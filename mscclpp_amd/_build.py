@@ -32,8 +32,13 @@ def _headers():
     )
 
 
+# MSCCLPP_AMD_FORCE_REBUILD=1: rebuild every artefact from its sources, whatever the timestamps
+FORCE = os.environ.get("MSCCLPP_AMD_FORCE_REBUILD") == "1"
+BUILT = []  # what this process compiled or linked (build_all's summary)
+
+
 def _newer(target, deps):
-    if not os.path.exists(target):
+    if FORCE or not os.path.exists(target):
         return True
     t = os.path.getmtime(target)
     return any(os.path.getmtime(d) > t for d in deps)
@@ -43,6 +48,8 @@ def _run(cmd):
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
         raise RuntimeError("build failed: " + " ".join(cmd) + "\n" + r.stdout)
+    out = cmd[cmd.index("-o") + 1] if "-o" in cmd else cmd[-1]
+    BUILT.append(os.path.relpath(out, ROOT))
     return r.stdout
 
 
@@ -142,18 +149,29 @@ def build_diag():
 
 
 def build_all(verbose=False):
+    """Builds what is out of date; returns a one-line summary of what was compiled or linked."""
+    del BUILT[:]
     build_oracle()
     build_library(verbose=verbose)
     build_audit()
     build_tests()
     build_diag()
     ref = os.path.join(ROOT, "oracle", "build_ref.sh")
+    ref_note = "oracle/_ref: skipped (no /root/reference)"
     if os.path.isdir("/root/reference") and os.path.exists(ref):
         # the reference-header harness (oracle/_ref) can only be built where /root/reference exists
-        r = subprocess.run(["bash", ref], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        env = dict(os.environ, REF_FORCE="1") if FORCE else None
+        r = subprocess.run(["bash", ref], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
         if verbose or r.returncode != 0:
             print(r.stdout, file=sys.stderr)
+        if r.returncode != 0:
+            raise RuntimeError("oracle/build_ref.sh failed:\n" + r.stdout)
+        ref_note = "oracle/_ref: " + ("; ".join(x for x in r.stdout.splitlines() if x.startswith("built")) or "up to date")
+    objs = sum(1 for b in BUILT if b.endswith(".o"))
+    rest = [b for b in BUILT if not b.endswith(".o")]
+    return (f"build: {objs} objects compiled, {len(rest)} artefacts linked ({', '.join(rest) or 'all up to date'}); "
+            + ref_note)
 
 
 if __name__ == "__main__":
-    build_all(verbose=True)
+    print(build_all(verbose=True))

@@ -13,7 +13,9 @@ if [ ! -d "$REF/include/mscclpp" ]; then
   exit 0
 fi
 # -D__HIP_PLATFORM_AMD__ selects the reference's HIP branch (gpu_data_types.hpp:50)
-if ! { [ "$OUT/libref.so" -nt "$HERE/ref_harness.hip" ] && [ "$OUT/libref.so" -nt "$HERE/build_ref.sh" ]; }; then
+# REF_FORCE=1 (MSCCLPP_AMD_FORCE_REBUILD=1 in mscclpp_amd/_build.py): rebuild whatever the timestamps
+FORCE=${REF_FORCE:-0}
+if [ "$FORCE" = 1 ] || ! { [ "$OUT/libref.so" -nt "$HERE/ref_harness.hip" ] && [ "$OUT/libref.so" -nt "$HERE/build_ref.sh" ]; }; then
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -D__HIP_PLATFORM_AMD__ \
     -I"$REF/include" "$HERE/ref_harness.hip" -o "$OUT/libref.so"
   echo "built $OUT/libref.so"
@@ -27,7 +29,7 @@ for spec in int:int float:float half:__half; do
   name=${spec%%:*}
   type=${spec#*:}
   obj="$OUT/bench_allreduce_$name.hsaco"
-  if [ -f "$BENCH_CU" ] && ! { [ "$obj" -nt "$BENCH_CU" ] && [ "$obj" -nt "$HERE/build_ref.sh" ]; }; then
+  if [ -f "$BENCH_CU" ] && { [ "$FORCE" = 1 ] || ! { [ "$obj" -nt "$BENCH_CU" ] && [ "$obj" -nt "$HERE/build_ref.sh" ]; }; }; then
     /opt/rocm/bin/hipcc --genco --offload-arch=gfx950 -O3 -std=c++17 -D__HIP_PLATFORM_AMD__ -DTYPE="$type" \
       -I"$REF/include" "$BENCH_CU" -o "$obj"
     echo "built $obj"
