@@ -5,7 +5,7 @@ lies (oracle/build_ref.sh -> oracle/_ref/bench_allreduce_int.hsaco, TYPE=int) an
 GPU (one code object and one stream per rank, channels holding the peers' plain scratch pointers).
 
 On the same inputs, for three calls (flag 1, 2, 3: both double-buffer halves and a wrap back), the
-reference kernel's outputs equal this library's k6 (n = 2 ... 8, 16 ints to 4 MiB) and the CPU oracle's restatement bit for bit, and
+reference kernel's outputs equal this library's k6 (n = 2 ... 8, 16 ints to 48 MiB per rank) and the CPU oracle's restatement bit for bit, and
 after the first call every rank's whole packet scratch image (input packets, reduced-result packets,
 flag words) is identical across all three.  This pins the oracle (tests/oracle_lib.py
 mscclpp_test_ll) on the reference's own device code, not only on its host-side fixtures.
@@ -33,7 +33,8 @@ REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref.so")
 
 # (ranks, int32 elements per rank, blocks per peer, threads per block); count % (2 n) == 0
 CASES = [(2, 4096, 2, 1024), (3, 1536, 4, 256), (4, 8192, 2, 512), (8, 6144, 1, 1024), (8, 65536, 4, 1024),
-         (8, 16, 1, 64), (5, 10000, 2, 512), (6, 12288, 1, 1024), (7, 28672, 3, 256), (2, 1 << 20, 8, 1024)]
+         (8, 16, 1, 64), (5, 10000, 2, 512), (6, 12288, 1, 1024), (7, 28672, 3, 256), (2, 1 << 20, 8, 1024),
+         (8, 12 << 20, 4, 512)]  # the last: BASELINE's 48 MiB bucket per rank
 
 
 # TYPE=float / __half builds of the same kernel: (type, ranks, 32-bit words per rank, blocks per peer,
