@@ -42,7 +42,7 @@ CASES = [(2, 4096, 2, 1024), (3, 1536, 4, 256), (4, 8192, 2, 512), (8, 6144, 1, 
 TYPED_CASES = [("f16", 2, 4096, 2, 1024), ("f16", 3, 6144, 2, 512), ("f16", 8, 16384, 2, 1024),
                ("f16", 5, 10240, 1, 256), ("f32", 2, 4096, 2, 1024), ("f32", 4, 8192, 1, 512),
                ("f32", 8, 16384, 3, 1024), ("f32", 7, 14336, 2, 256), ("f32", 3, 12, 1, 64),
-               ("f16", 6, 245760, 3, 1024)]
+               ("f16", 6, 245760, 3, 1024), ("f16", 8, 12 << 20, 4, 512)]  # last: the 48 MiB fp16 bucket
 TYPED_HSACO = [os.path.join(ROOT, "oracle", "_ref", f"bench_allreduce_{t}.hsaco") for t in ("float", "half")]
 
 
