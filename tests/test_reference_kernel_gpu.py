@@ -93,7 +93,7 @@ def test_reference_allreduce2_fp16_fp32_order_and_rounding(built):
 BENCH1_CASES = [("i32", 2, 4096, 2, 1024, 0), ("i32", 5, 10240, 3, 512, 1), ("f16", 2, 4096, 2, 1024, 0),
                 ("f16", 3, 6144, 4, 256, 0), ("f16", 8, 16384, 2, 1024, 1), ("f32", 4, 8192, 2, 512, 0),
                 ("f32", 7, 14336, 1, 1024, 1), ("f32", 8, 32768, 4, 1024, 0), ("f16", 6, 24576, 2, 512, 1),
-                ("i32", 8, 1 << 20, 4, 1024, 0)]
+                ("i32", 8, 1 << 20, 4, 1024, 0), ("f16", 8, 12 << 20, 8, 1024, 1)]  # last: the 48 MiB fp16 bucket
 
 
 def test_reference_allreduce1_order_and_rounding(built):
