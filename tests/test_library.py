@@ -169,3 +169,13 @@ def test_flag_alignment_and_mix_sizes_rejected_without_gpu(built):
             v.peerScratch[q] = v.peerOutput[q] = v.peerInput[q] = v.peerTokens[q] = 1 << 20
     assert L.mscclppAmdAllReduceLaunch(m.ALGO_ALLPAIR, arr, 2, 2, 1024, m.F16, m.SUM, 0, 0, 1000, None) == 4
     assert L.mscclppAmdMixStream(fake, fake, fake, fake, fake, 4096 + 16, 0, None) == 4
+
+
+def test_build_all_reports_what_it_built(built):
+    """build() prints one line naming what it compiled and linked (the driver's build check can tell a
+    real build from an up-to-date tree); right after the session build nothing is out of date."""
+    from mscclpp_amd import _build
+
+    line = _build.build_all()
+    assert line.startswith("build: 0 objects compiled, 0 artefacts linked (all up to date)"), line
+    assert "oracle/_ref:" in line
