@@ -577,4 +577,81 @@ int refBench1Run(void* handle, void* const* bufs, void* const* tokens, void* con
   return 0;
 }
 
+// `calls` allreduce2 calls queued back to back on every rank stream (rank by rank, call by call), with
+// no host synchronisation between them -- how the reference's benchmark times it (bench_time: one
+// graph of niter launches).  flagsOut[r] = each rank's globalFlag afterwards (on a timeout: as read
+// on the diagnostic stream while the ranks still spun).  Returns as refBench2Run; on 2 the ranks were
+// then released by filling every scratch word with each remaining call's flag in turn (scratchWords
+// 32-bit words per rank), 3 if even that did not drain them.
+// between: what runs on every rank stream between two calls -- 0 nothing, 1 a 1024-workgroup kernel
+// that does nothing, 2 the same kernel with a system-scope acquire fence in every wave (each XCD's L2
+// invalidated: workgroups are spread over all eight).
+__global__ void refBetweenKernel(int inv) {
+  if (inv) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+int refBench2RunBackToBack(void* handle, void* const* bufs, void* const* scratch, void* const* results, uint64_t nelems,
+                           int blocksPerPeer, int threads, int calls, int timeoutMs, uint64_t scratchWords,
+                           int between, uint64_t* flagsOut) {
+  auto* h = static_cast<RefBench2*>(handle);
+  if (!h || calls < 1 || calls > 64 || !flagsOut || !gDiagPinned) return 1;
+  const int n = h->n;
+  if (const int rc = setupBench2(h, bufs, scratch, nelems, blocksPerPeer, threads)) return rc;
+  if (const int mc = ensureConcurrent(n)) return mc;
+  std::vector<void*> g(n, nullptr);
+  for (int r = 0; r < n; ++r) {
+    size_t bytes = 0;
+    if (hipModuleGetGlobal(reinterpret_cast<hipDeviceptr_t*>(&g[r]), &bytes, h->mod[r], "globalFlag") != hipSuccess)
+      return 1;
+  }
+  uint64_t flag0 = 0;
+  if (hipMemcpy(&flag0, g[0], sizeof(flag0), hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  int rc = 0;
+  for (int c = 0; c < calls && rc == 0; ++c)
+    for (int r = 0; r < n && rc == 0; ++r) {
+      if (c > 0 && between > 0) {
+        hipLaunchKernelGGL(refBetweenKernel, dim3(1024), dim3(64), 0, gRankStream[r], between == 2 ? 1 : 0);
+        if (hipGetLastError() != hipSuccess) rc = 1;
+      }
+      if (rc == 0) rc = launchBench2(h, r, bufs, scratch, results, nelems, blocksPerPeer, threads);
+    }
+  auto drained = [&](int ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < n;) {
+      if (hipStreamQuery(gRankStream[r]) != hipErrorNotReady) {
+        ++r;
+        continue;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(ms)) return false;
+    }
+    return true;
+  };
+  if (!drained(timeoutMs)) {
+    for (int r = 0; r < n; ++r)
+      (void)hipMemcpyAsync(gDiagPinned + r, g[r], sizeof(uint64_t), hipMemcpyDeviceToHost, gDiagStream);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hipStreamQuery(gDiagStream) == hipErrorNotReady &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5)) {
+    }
+    for (int r = 0; r < n; ++r) flagsOut[r] = gDiagPinned[r];
+    // ranks may wait for different calls' flags at once, one past the last included (a workgroup that
+    // read a flag already incremented): two passes over flag0 .. flag0 + calls
+    bool ok = false;
+    for (int pass = 0; pass < 2 && !ok; ++pass)
+      for (int c = 0; c <= calls && !ok; ++c) {
+        for (int r = 0; r < n; ++r)
+          (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(scratch[r]), (int)(uint32_t)(flag0 + c),
+                                  scratchWords, gDiagStream);
+        ok = drained(200);
+      }
+    return ok ? 2 : 3;
+  }
+  for (int r = 0; r < n; ++r)
+    if (hipMemcpy(&flagsOut[r], g[r], sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return 1;
+  return rc;
+}
+
 }  // extern "C"
