@@ -417,6 +417,24 @@ int refReleaseSpin(void* const* ptrs, int nptr, uint64_t words, uint32_t value, 
   return 0;
 }
 
+// After refReleaseSpin ended a stalled allreduce2 call: the state a retry of that call needs -- every
+// rank's packet scratch zeroed (the release filled it with the call's flag) and every rank's
+// globalFlag set to `flag` (a workgroup that read an already incremented flag may have moved one
+// rank on).  0 on success.
+int refBench2Reset(void* handle, void* const* scratch, uint64_t bytes, uint64_t flag) {
+  auto* h = static_cast<RefBench2*>(handle);
+  if (!h) return 1;
+  for (int r = 0; r < h->n; ++r) {
+    void* g = nullptr;
+    size_t gb = 0;
+    if (hipMemset(scratch[r], 0, bytes) != hipSuccess ||
+        hipModuleGetGlobal(reinterpret_cast<hipDeviceptr_t*>(&g), &gb, h->mod[r], "globalFlag") != hipSuccess ||
+        hipMemcpy(g, &flag, sizeof(flag), hipMemcpyHostToDevice) != hipSuccess)
+      return 1;
+  }
+  return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+
 // How many times ensureConcurrent replaced the rank streams in this process.
 int refStreamRecreations() { return gStreamRecreations; }
 

@@ -33,6 +33,12 @@ L.refFree.argtypes = [vp]
 L.refBench2RunBackToBack.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_uint64, ctypes.c_int, vp]
 L.refBench2RunBackToBack.restype = ctypes.c_int
+L.refBench2Reset.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint64]
+L.refBench2Reset.restype = ctypes.c_int
+L.refBench2Run.argtypes = [vp, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+L.refBench2Run.restype = ctypes.c_int
+L.refReleaseSpin.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
+L.refReleaseSpin.restype = ctypes.c_int
 HSACO = os.path.join(ROOT, "oracle", "_ref", "bench_allreduce_int.hsaco")
 CALLS = int(os.environ.get("CALLS", 8))
 dev = torch.device("cuda", 0)
@@ -59,9 +65,23 @@ def case(n, words, bpp, threads, between=0):
         rec = {"n": n, "words": words, "blocks_per_peer": bpp, "threads": threads, "calls": CALLS, "rc": rc,
                "between": ["nothing", "noop_kernel", "l2_invalidate_kernel"][between],
                "globalFlag": list(flags)}
+        want = sum(x.long() for x in ins).int()
         if rc == 0:
-            want = sum(x.long() for x in ins).int()
             rec["outputs_equal_sum"] = all(bool(torch.equal(o, want)) for o in outs)
+        elif rc == 2:  # the worker's recovery (tests/ref_kernel_worker.py _run_bench2): reset, one more call
+            for o in outs:
+                o.zero_()
+            torch.cuda.synchronize()
+            r1 = L.refBench2Reset(h, arr(scr), sb, 1)
+            r2 = L.refBench2Run(h, arr([x.data_ptr() for x in ins]), arr(scr), arr([o.data_ptr() for o in outs]),
+                                words, bpp, threads, 3000) if r1 == 0 else -1
+            rec["after_reset_rc"] = r2
+            if r2 == 0:
+                rec["after_reset_outputs_equal_sum"] = all(bool(torch.equal(o, want)) for o in outs)
+            elif r2 == 2:  # a second stall: release it as the worker does, then report it as a stop
+                rec["after_reset_released"] = any(L.refReleaseSpin(arr(scr), n, sb // 4, v, n, 3000) == 0
+                                                  for v in (1, 2, 1))
+                rc = 3
         print(json.dumps(rec), flush=True)
         if rc not in (0, 2):  # ranks that could not be released: leave without waiting on them
             print("STOPPED", flush=True)

@@ -46,7 +46,31 @@ def _lib():
     L.refReleaseSpin.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
     L.refReleaseSpin.restype = ctypes.c_int
     L.refStreamRecreations.restype = ctypes.c_int
+    L.refBench2Reset.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint64]
+    L.refBench2Reset.restype = ctypes.c_int
     return L
+
+
+def _run_bench2(L, h, n, ins, rptr, outs, words, bpp, threads, flag, sb, rec, call):
+    """One allreduce2 call (refBench2Run).  The kernel has a race of its own: block 0
+    bumps the one globalFlag when it ends, and a workgroup of the same call that starts later reads the
+    next flag, so the ranks can stall one flag apart.  A stalled call is reported, its ranks released
+    (scratch := the flag, then the flag + 1 a late workgroup waits for), scratch and flags reset, and the
+    call run once more; the comparison is made on that run, and the record counts the retries."""
+    rc = L.refBench2Run(h, _ptrs(ins), _ptrs(rptr), _ptrs(outs), words, bpp, threads, 20000)
+    if rc == 2:
+        done, flags = (ctypes.c_int * n)(), (ctypes.c_uint64 * n)()
+        drc = L.refBench2Diag(h, done, flags)
+        arr = (ctypes.c_void_p * n)(*[p.data_ptr() for p in rptr])
+        released = any(L.refReleaseSpin(arr, n, sb // 4, v, n, 3000) == 0 for v in (flag, flag + 1, flag))
+        print(json.dumps({"reference_stall": rec, "call": call, "diag_rc": drc, "done": list(done),
+                          "globalFlag": list(flags), "released": released}), flush=True)
+        if not released:
+            os._exit(3)
+        assert L.refBench2Reset(h, arr, sb, flag) == 0, "refBench2Reset failed"
+        rec["reference_stalls_retried"] = rec.get("reference_stalls_retried", 0) + 1
+        rc = L.refBench2Run(h, _ptrs(ins), _ptrs(rptr), _ptrs(outs), words, bpp, threads, 20000)
+    return rc
 
 
 def _ptrs(ts):
@@ -86,6 +110,8 @@ def run_case(L, m, n, count, blocks_per_peer, threads):
     rptr = [L.refMallocUncached(sb) for _ in range(n)]
     assert all(rptr), "refMallocUncached failed"
     rscr = [m.device_view(p, sb).view(torch.int32) for p in rptr]
+    # the state a retried call starts from (_run_bench2), here on every case: zero scratch, flag 1
+    assert L.refBench2Reset(h, (ctypes.c_void_p * n)(*rptr), sb, 1) == 0, "refBench2Reset failed"
     rec = {"n": n, "count": count, "blocks_per_peer": blocks_per_peer, "threads": threads}
     try:
         for call, flag in enumerate((1, 2, 3)):
@@ -94,7 +120,7 @@ def run_case(L, m, n, count, blocks_per_peer, threads):
             dins = [torch.from_numpy(a).to(dev) for a in ins]
             rout = [torch.zeros_like(d) for d in dins]
             torch.cuda.synchronize()
-            rc = L.refBench2Run(h, _ptrs(dins), _ptrs(rscr), _ptrs(rout), count, blocks_per_peer, threads, 20000)
+            rc = _run_bench2(L, h, n, dins, rscr, rout, count, blocks_per_peer, threads, flag, sb, rec, call)
             _check_run(L, rc, rec, call, n, rptr, sb // 4, flag, h)
             douts = [torch.zeros_like(d) for d in dins]
             ours.all_reduce(dins, douts, m.ALGO_TEST_K6)
@@ -190,6 +216,7 @@ def run_typed_case(L, kind, n, nwords, blocks_per_peer, threads):
     assert m.scratch_required(m.ALGO_TEST_K6, n, nwords * 4, mdt) == sb
     ours = m.InProcessRanks(n, sb)  # this library's k6 on the same inputs: the product kernel, typed
     rscr = [m.device_view(p, sb).view(torch.int32) for p in rptr]
+    assert L.refBench2Reset(h, (ctypes.c_void_p * n)(*rptr), sb, 1) == 0, "refBench2Reset failed"
     rec = {"type": kind, "n": n, "words": nwords, "blocks_per_peer": blocks_per_peer, "threads": threads,
            "nan_words": 0, "inf_words": 0, "order_sensitive_words": 0, "k6_compared": True}
     try:
@@ -198,7 +225,7 @@ def run_typed_case(L, kind, n, nwords, blocks_per_peer, threads):
             dins = [torch.from_numpy(a.view(np.int32).copy()).to(dev) for a in ins]
             rout = [torch.zeros_like(d) for d in dins]
             torch.cuda.synchronize()
-            rc = L.refBench2Run(h, _ptrs(dins), _ptrs(rscr), _ptrs(rout), nwords, blocks_per_peer, threads, 20000)
+            rc = _run_bench2(L, h, n, dins, rscr, rout, nwords, blocks_per_peer, threads, flag, sb, rec, call)
             _check_run(L, rc, rec, call, n, rptr, sb // 4, flag, h)
             douts = [torch.zeros_like(d) for d in dins]
             ours.all_reduce([d.view(tdt) for d in dins], [o.view(tdt) for o in douts], m.ALGO_TEST_K6)

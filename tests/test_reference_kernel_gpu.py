@@ -16,7 +16,10 @@ harness checks that before every launch (a one-wave kernel per rank stream that 
 others running, 100 ms budget; on a failure fresh streams, twice).  If the rank streams still cannot
 run together nothing is launched and the test skips with that reason instead of wedging; a run that
 does time out reports which ranks spin, then fills the words they wait on so they finish before the
-worker exits."""
+worker exits.  allreduce2 has a race of its own (one globalFlag that block 0 bumps when it ends; a
+workgroup of the same call that starts later reads the next flag): a call that stalls on
+it is reported, released, reset and run once more, the comparison is made on that run, and the case
+record counts it (`reference_stalls_retried`)."""
 import json
 import os
 import subprocess
