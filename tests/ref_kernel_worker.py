@@ -51,17 +51,17 @@ def _lib():
     return L
 
 
-def _run_bench2(L, h, n, ins, rptr, outs, words, bpp, threads, flag, sb, rec, call):
+def _run_bench2(L, h, n, ins, scratch, outs, words, bpp, threads, flag, sb, rec, call):
     """One allreduce2 call (refBench2Run).  The kernel has a race of its own: block 0
     bumps the one globalFlag when it ends, and a workgroup of the same call that starts later reads the
     next flag, so the ranks can stall one flag apart.  A stalled call is reported, its ranks released
     (scratch := the flag, then the flag + 1 a late workgroup waits for), scratch and flags reset, and the
     call run once more; the comparison is made on that run, and the record counts the retries."""
-    rc = L.refBench2Run(h, _ptrs(ins), _ptrs(rptr), _ptrs(outs), words, bpp, threads, 20000)
+    rc = L.refBench2Run(h, _ptrs(ins), _ptrs(scratch), _ptrs(outs), words, bpp, threads, 20000)
     if rc == 2:
         done, flags = (ctypes.c_int * n)(), (ctypes.c_uint64 * n)()
         drc = L.refBench2Diag(h, done, flags)
-        arr = (ctypes.c_void_p * n)(*[p.data_ptr() for p in rptr])
+        arr = (ctypes.c_void_p * n)(*[p.data_ptr() for p in scratch])
         released = any(L.refReleaseSpin(arr, n, sb // 4, v, n, 3000) == 0 for v in (flag, flag + 1, flag))
         print(json.dumps({"reference_stall": rec, "call": call, "diag_rc": drc, "done": list(done),
                           "globalFlag": list(flags), "released": released}), flush=True)
@@ -69,7 +69,7 @@ def _run_bench2(L, h, n, ins, rptr, outs, words, bpp, threads, flag, sb, rec, ca
             os._exit(3)
         assert L.refBench2Reset(h, arr, sb, flag) == 0, "refBench2Reset failed"
         rec["reference_stalls_retried"] = rec.get("reference_stalls_retried", 0) + 1
-        rc = L.refBench2Run(h, _ptrs(ins), _ptrs(rptr), _ptrs(outs), words, bpp, threads, 20000)
+        rc = L.refBench2Run(h, _ptrs(ins), _ptrs(scratch), _ptrs(outs), words, bpp, threads, 20000)
     return rc
 
 
