@@ -63,8 +63,9 @@ def _run_bench2(L, h, n, ins, scratch, outs, words, bpp, threads, flag, sb, rec,
         drc = L.refBench2Diag(h, done, flags)
         arr = (ctypes.c_void_p * n)(*[p.data_ptr() for p in scratch])
         released = any(L.refReleaseSpin(arr, n, sb // 4, v, n, 3000) == 0 for v in (flag, flag + 1, flag))
-        print(json.dumps({"reference_stall": rec, "call": call, "diag_rc": drc, "done": list(done),
-                          "globalFlag": list(flags), "released": released}), flush=True)
+        # not a case record: the test reads the lines that start with "{"
+        print("REFERENCE_STALL " + json.dumps({"case": rec, "call": call, "diag_rc": drc, "done": list(done),
+                                               "globalFlag": list(flags), "released": released}), flush=True)
         if not released:
             os._exit(3)
         assert L.refBench2Reset(h, arr, sb, flag) == 0, "refBench2Reset failed"
